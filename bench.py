@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident block-checksum throughput on MI355X.
+
+Metric (BASELINE.json): GiB/s block-checksummed (weak + MD4), device-resident.
+Workload: BASELINE.json configs[1] -- 1024 x 1 MiB random files, 700-byte
+blocks, receiver block-sum generation -- per GPU (weak scaling: rank r owns
+its own 1024 files).  One step = one launch of the block-sum kernel over the
+rank's 1 GiB batch, inputs already resident in HBM; two input arenas are
+alternated so the 256 MiB Infinity Cache cannot serve repeats.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.  Extra objects: roofline (HIP-event kernel
+time vs the HBM roofline), cpu_baseline (the scalar C restatement on host
+cores, bounded sample), host_path (PCIe-inclusive rate), and for N > 1 the
+RCCL sums gather.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+FILES_PER_GPU = 1024
+FILE_BYTES = 1 << 20
+BLOCK_LEN = 700
+SEED = 0x1BADB002
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")  # control plane only; data moves over RCCL
+    torch.cuda.set_device(local)
+    import rsync_amd
+
+    eng = rsync_amd.Engine(local)
+    stream = torch.cuda.Stream(device=local)
+    sptr = stream.cuda_stream
+
+    # ---- workload: this rank's 1024 files, global file ids rank*1024 + f
+    n = FILES_PER_GPU
+    arena_bytes = n * FILE_BYTES
+    arenas = [eng.alloc(arena_bytes) for _ in range(2)]
+    for a in arenas:
+        for f in range(n):
+            eng.fill_splitmix64(a, FILE_BYTES, rank * n + f + 1, offset=f * FILE_BYTES, stream=sptr)
+    plan = eng.plan([(f * FILE_BYTES, FILE_BYTES, BLOCK_LEN) for f in range(n)], arena_bytes)
+    recs = eng.alloc(plan.total_records * rsync_amd.RECORD_BYTES)
+    eng.synchronize(sptr)
+
+    def step(i):
+        plan.run(arenas[i & 1], SEED, recs, stream=sptr)
+
+    for i in range(args.warmup):
+        step(i)
+    eng.synchronize(sptr)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(args.steps):
+        step(i)
+    ev1.record(stream)
+    eng.synchronize(sptr)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    wall = t1 - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    if world > 1:
+        tt = torch.tensor([wall, kernel_ms], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall, kernel_ms = float(tt[0]), float(tt[1])
+
+    in_bytes = float(arena_bytes)
+    out_bytes = float(plan.total_records * rsync_amd.RECORD_BYTES)
+    value = world * in_bytes * args.steps / wall / GIB
+    achieved = (in_bytes + out_bytes) / (kernel_ms * 1e-3) / 1e9
+
+    extra = {}
+    # ---- RCCL gather of every rank's records to rank 0 (the one exchange step)
+    if world > 1:
+        uid = [rsync_amd.Engine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(world, rank, uid[0])
+        sizes = [int(out_bytes)] * world
+        recv = eng.alloc(sum(sizes)) if rank == 0 else None
+        eng.gather_bytes(recs, sizes, recv, 0, stream=sptr)
+        eng.synchronize(sptr)
+        dist.barrier()
+        g0 = time.perf_counter()
+        reps = 10
+        for _ in range(reps):
+            eng.gather_bytes(recs, sizes, recv, 0, stream=sptr)
+        eng.synchronize(sptr)
+        dist.barrier()
+        gather_ms = (time.perf_counter() - g0) * 1e3 / reps
+        gt = torch.tensor([gather_ms], dtype=torch.float64)
+        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+        gather_ms = float(gt[0])
+        step_ms = wall * 1e3 / args.steps
+        extra["gather"] = {"bytes_to_root": int(out_bytes) * (world - 1), "ms": round(gather_ms, 4),
+                           "kernel_plus_gather_gib_s": round(world * in_bytes / ((step_ms + gather_ms) * 1e-3) / GIB, 2)}
+
+    # ---- PCIe-inclusive host path (rank 0, N = 1): host buffers in, records out
+    if rank == 0 and world == 1 and not args.no_host_path:
+        import cases
+        files = [cases.splitmix64_bytes(f + 1, FILE_BYTES) for f in range(256)]
+        eng.block_sums(files[:8], SEED, BLOCK_LEN)  # warm the staging buffers
+        h0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            _, host_rec, _ = eng.block_sums(files, SEED, BLOCK_LEN)
+        hdt = (time.perf_counter() - h0) / reps
+        extra["host_path"] = {"gib_s": round(256 * FILE_BYTES / hdt / GIB, 3),
+                              "sample": "256 x 1 MiB host buffers, H2D + kernel + D2H, pinned staging"}
+
+    # ---- CPU baseline: the scalar C restatement (oracle) on 1 host core
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        import cases
+        from oracle import oracle as orc
+        lib = orc.lib()
+        done_bytes, t_cpu, f = 0, 0.0, 0
+        sample_parity = True
+        out = np.empty(1498 * 20, np.uint8)
+        while t_cpu < args.cpu_seconds and f < n:
+            data = cases.splitmix64_bytes(f + 1, FILE_BYTES)
+            c0 = time.perf_counter()
+            lib.orc_block_sums(orc._ptr(data), data.size, BLOCK_LEN, orc._i32(SEED), orc._ptr(out))
+            t_cpu += time.perf_counter() - c0
+            done_bytes += data.size
+            if f < 4:  # spot parity of the benchmarked GPU output
+                got = recs.download(1498 * 20, offset=plan.first_record[f] * 20)
+                sample_parity &= bool((got == out).all())
+            f += 1
+        cpu = {"value": round(done_bytes / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+               "sample": f"{f} of the 1024 x 1 MiB files at B=700, oracle/rsg_oracle.c orc_block_sums "
+                         f"(scalar C restatement of generator.go:325-350), 1 thread, {t_cpu:.1f} s",
+               "gpu_parity_on_sample": sample_parity}
+
+    if rank == 0:
+        traffic = None
+        tp = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(tp):
+            try:
+                traffic = json.load(open(tp)).get("block_sums_kernel_cfg2_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": "GiB/s block-checksummed (weak+MD4), device-resident, at 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (splitmix64 bytes generated on device)",
+            "config": {"workload": "cfg2: receiver block sums, 1024 x 1 MiB files per GPU, B=700, weak+MD4",
+                       "files_per_gpu": n, "file_bytes": FILE_BYTES, "block_len": BLOCK_LEN,
+                       "records_per_gpu": plan.total_records, "parallelism": f"files sharded, {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel_ms": round(kernel_ms, 4),
+                         "algorithmic_bytes_per_launch": int(in_bytes + out_bytes)},
+            "cpu_baseline": cpu,
+        }
+        line.update(extra)
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,199 @@
+/*
+ * rsg.h -- C ABI of the MI355X (gfx950) rsync block-checksum engine.
+ *
+ * This is the drop-in boundary between the gokrazy/rsync host code and the
+ * HIP kernels.  The reference has no FFI of its own (it is pure Go, SURVEY.md
+ * F1); every entry point below names the Go function whose work it replaces,
+ * and INTEGRATION.md shows the cgo binding a maintainer would add.
+ *
+ * Conventions
+ *  - Plain C types only: pointers + sizes, no torch or HIP types.  `stream`
+ *    parameters are a hipStream_t passed as void* (NULL = the context's own
+ *    stream).
+ *  - Every call returns rsg_status (0 = OK, negative = error) and never
+ *    aborts; the message of the last failure on a context is returned by
+ *    rsg_last_error(ctx) (Go maps it to `error`, as the reference's functions
+ *    return errors and never panic by design).
+ *  - The caller owns every buffer.  Nothing retains a caller pointer after
+ *    return (cgo pointer rules), except where a *_device call documents that
+ *    work is still queued on `stream`.
+ *  - Threading: a context serialises its own calls with a mutex; separate
+ *    contexts run concurrently (the loopback generator and sender goroutines of
+ *    clientmaincmd.go:209-228 use one context each).  Each call selects its
+ *    device itself, so Go may migrate OS threads freely.
+ *  - All checksum arithmetic runs on the GPU.  There is no CPU fallback: with
+ *    no usable gfx950 device, rsg_ctx_create fails with RSG_ERR_NODEV.
+ */
+#ifndef RSG_H
+#define RSG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSG_ABI_VERSION 1
+/* One wire record: int32 LE sum1 then sum2[16] (generator.go:341-346). */
+#define RSG_RECORD_BYTES 20
+#define RSG_SUM2_BYTES 16
+/* Literal token piece size, internal/sender/flist.go:52. */
+#define RSG_CHUNK_SIZE (256 * 1024)
+/* SumHead.ReadFrom limit on block_len, types.go:40. */
+#define RSG_MAX_BLOCK_LEN (1 << 29)
+
+typedef int32_t rsg_status;
+#define RSG_OK 0
+#define RSG_ERR_INVALID (-1)   /* bad argument: a Go `error`, nothing ran   */
+#define RSG_ERR_NOMEM (-2)     /* device or pinned allocation failed         */
+#define RSG_ERR_HIP (-3)       /* HIP runtime error, see rsg_last_error      */
+#define RSG_ERR_NODEV (-4)     /* no gfx950 device at that ordinal           */
+#define RSG_ERR_TRUNCATED (-5) /* output capacity too small; size reported   */
+
+typedef struct rsg_ctx rsg_ctx;
+typedef struct rsg_plan rsg_plan;
+
+/* SumHead, types.go:19-36.  Field order is the wire order of
+ * SumHead.WriteTo (types.go:79-86): count, block_len, s2len, rem. */
+typedef struct rsg_sum_head {
+    int32_t count;
+    int32_t block_len;
+    int32_t s2len;
+    int32_t rem;
+} rsg_sum_head;
+
+/* One basis file of a batched block-sum job.
+ *  device calls: `offset` is the byte offset of the file in the device arena;
+ *  host calls:   `data` points at the file bytes in host memory.
+ * block_len = 0 selects the reference sizing SumSizesSqroot
+ * (rsynccommon.go:14-37); block_len > 0 is an explicit B. */
+typedef struct rsg_file {
+    const uint8_t *data;
+    uint64_t offset;
+    uint64_t len;
+    int32_t block_len;
+    int32_t reserved;
+} rsg_file;
+
+/* One match of the sender search: matched(h, ms, head, offset, i) with i >= 0
+ * (match.go:149,233). */
+typedef struct rsg_match {
+    int64_t offset;
+    int32_t index;
+    int32_t reserved;
+} rsg_match;
+
+/* ------------------------------------------------------------------ misc */
+int32_t rsg_abi_version(void);
+/* Number of visible gfx950 devices (0 when none). */
+int32_t rsg_device_count(void);
+
+/* SumSizesSqroot (rsynccommon.go:14-37) or an explicit block length.
+ * Host arithmetic only. */
+rsg_status rsg_sum_head_for(int64_t file_len, int32_t block_len, rsg_sum_head *out);
+
+/* ------------------------------------------------------------ context */
+rsg_status rsg_ctx_create(int32_t device, rsg_ctx **out);
+void rsg_ctx_destroy(rsg_ctx *ctx);
+/* Last error message of ctx (or of the calling thread when ctx == NULL). */
+const char *rsg_last_error(const rsg_ctx *ctx);
+/* Pinned host memory for zero-copy staging of file reads (generator.go:335
+ * reads each block into a Go buffer; reading into this memory instead saves
+ * one copy on the host path). */
+rsg_status rsg_alloc_pinned(rsg_ctx *ctx, uint64_t bytes, void **out);
+rsg_status rsg_free_pinned(rsg_ctx *ctx, void *p);
+/* Device memory helpers for callers that have no allocator of their own. */
+rsg_status rsg_alloc_device(rsg_ctx *ctx, uint64_t bytes, void **out);
+rsg_status rsg_free_device(rsg_ctx *ctx, void *p);
+rsg_status rsg_memcpy_h2d(rsg_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+rsg_status rsg_memcpy_d2h(rsg_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+rsg_status rsg_synchronize(rsg_ctx *ctx, void *stream);
+/* Synthetic data: dst[0..n) = splitmix64(seed) little-endian byte stream
+ * (SURVEY.md appendix), generated on the device. */
+rsg_status rsg_fill_splitmix64(rsg_ctx *ctx, void *d_dst, uint64_t n, uint64_t seed, void *stream);
+
+/* ------------------------------------------ receiver: block sums (★ a2,a3,a7)
+ * Replaces the per-block loop of (*receiver.Transfer).generateAndSendSums
+ * (generator.go:325-350: Checksum1 + Checksum2(seed) per block) for a whole
+ * batch of files.  Output: for file i, heads[i] and head.count records of
+ * RSG_RECORD_BYTES starting at record first_record[i]; records of consecutive
+ * files are contiguous, in file order.  The Go caller writes, per file in
+ * file-list order, idx, SumHead, then that file's records (generator.go:317-321),
+ * chunked <= 256 KiB per Write on the mux writer (wire.go:46-62). */
+
+/* Host arithmetic: heads, first_record (may be NULL) and the total record count. */
+rsg_status rsg_plan_block_sums(const rsg_file *files, uint64_t nfiles, rsg_sum_head *heads,
+                               uint64_t *first_record, uint64_t *total_records);
+
+/* Device-resident plan: uploads the per-file descriptors once, for repeated
+ * launches over the same file layout in a device arena of arena_bytes. */
+rsg_status rsg_plan_create(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles,
+                           uint64_t arena_bytes, rsg_plan **out);
+void rsg_plan_destroy(rsg_plan *plan);
+uint64_t rsg_plan_total_records(const rsg_plan *plan);
+
+/* Launch the block-sum kernel for `plan` over d_arena, writing
+ * total_records * 20 bytes at d_records.  Asynchronous on `stream`. */
+rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void *d_arena,
+                                  int32_t seed, void *d_records, void *stream);
+
+/* One-shot device call: plan + launch + wait. */
+rsg_status rsg_block_sums_device(rsg_ctx *ctx, const void *d_arena, uint64_t arena_bytes,
+                                 const rsg_file *files, uint64_t nfiles, int32_t seed,
+                                 void *d_records, uint64_t records_cap);
+
+/* Host buffers in (rsg_file.data), host records out: stages through pinned
+ * memory, overlapping H2D, kernel and D2H.  Synchronous. */
+rsg_status rsg_block_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, int32_t seed,
+                               uint8_t *records, uint64_t records_cap);
+
+/* ---------------------------------------------- sender: hash search (★ a11)
+ * Replaces the per-byte search of (*sender.Transfer).hashSearch
+ * (match.go:21-230) for one source file against the receiver's sums:
+ *   head            SumHead read by receiveSums (sender.go:118-151)
+ *   sum1[count]     SumBuf.Sum1 in block-index order
+ *   sum2[count*16]  SumBuf.Sum2 (only the first head->s2len bytes compared)
+ *   targets[count]  the Go `targets` order: block indices sorted by
+ *                   Tag(sum1) (sender.go:60-75); its tie order among equal
+ *                   tags decides which duplicate block is reported.
+ * Output: the greedy match list in offset order, exactly the (offset, i >= 0)
+ * pairs hashSearch passes to matched().  The literal/match token bytes follow
+ * from it with rsg_encode_tokens; the whole-file MD4 stays with the caller
+ * (match.go:52-53,262-269 feeds it incrementally).
+ * *n_matches is always set; RSG_ERR_TRUNCATED when it exceeds match_cap. */
+rsg_status rsg_hash_search_host(rsg_ctx *ctx, const uint8_t *src, uint64_t src_len,
+                                const rsg_sum_head *head, const uint32_t *sum1, const uint8_t *sum2,
+                                const int32_t *targets, int32_t seed, rsg_match *matches,
+                                uint64_t match_cap, uint64_t *n_matches);
+/* Same with the source already resident at d_src on the device. */
+rsg_status rsg_hash_search_device(rsg_ctx *ctx, const void *d_src, uint64_t src_len,
+                                  const rsg_sum_head *head, const uint32_t *sum1,
+                                  const uint8_t *sum2, const int32_t *targets, int32_t seed,
+                                  rsg_match *matches, uint64_t match_cap, uint64_t *n_matches);
+
+/* Token stream of simpleSendToken (token.go:4-31) as matched() emits it
+ * (match.go:233-282): literal runs in <= 256 KiB pieces (int32 LE n + n bytes),
+ * a match as int32 -(i+1), terminated by int32 0 (match.go:212).  Host byte
+ * formatting, no checksum work.  out == NULL queries *out_len. */
+rsg_status rsg_encode_tokens(const uint8_t *src, uint64_t src_len, const rsg_sum_head *head,
+                             const rsg_match *matches, uint64_t n_matches, uint8_t *out,
+                             uint64_t out_cap, uint64_t *out_len);
+
+/* ------------------------------------------ multi-GPU sums gather
+ * Files shard across the GPUs of one node with no data-path collective; the
+ * only exchange is the final gather of each rank's records to the root over
+ * RCCL (xGMI).  The caller exchanges the 128-byte unique id out of band (the
+ * Go host over its own control channel; bench.py over torch.distributed). */
+rsg_status rsg_comm_unique_id(uint8_t id[128]);
+rsg_status rsg_comm_init(rsg_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
+/* Ragged gather: rank r sends send_bytes[r] bytes from d_send; the root receives
+ * them back to back at d_recv (offsets = exclusive prefix of send_bytes).
+ * send_bytes has nranks entries on every rank.  Asynchronous on `stream`. */
+rsg_status rsg_gather_bytes(rsg_ctx *ctx, const void *d_send, const uint64_t *send_bytes,
+                            void *d_recv, int32_t root, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSG_H */

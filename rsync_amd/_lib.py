@@ -1,0 +1,111 @@
+"""ctypes binding of librsg.so (include/rsg.h).
+
+Importing this module loads the in-tree HIP library and fails loudly if it is
+missing: the package has no CPU fallback for any checksum work.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librsg.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+        "(make -C rsync_amd/csrc). rsync_amd has no CPU fallback.")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+RECORD_BYTES = 20
+CHUNK_SIZE = 256 * 1024
+ABI_VERSION = 1
+
+OK = 0
+ERR_INVALID = -1
+ERR_NOMEM = -2
+ERR_HIP = -3
+ERR_NODEV = -4
+ERR_TRUNCATED = -5
+
+
+class SumHead(ctypes.Structure):
+    """rsync.SumHead (types.go:19-36), wire field order (types.go:79-86)."""
+    _fields_ = [("count", ctypes.c_int32), ("block_len", ctypes.c_int32),
+                ("s2len", ctypes.c_int32), ("rem", ctypes.c_int32)]
+
+    def astuple(self):
+        return (self.count, self.block_len, self.s2len, self.rem)
+
+    def __repr__(self):
+        return f"SumHead(count={self.count}, block_len={self.block_len}, s2len={self.s2len}, rem={self.rem})"
+
+
+class File(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("offset", ctypes.c_uint64), ("len", ctypes.c_uint64),
+                ("block_len", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class Match(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_int64), ("index", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+_vp = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+_i32 = ctypes.c_int32
+_st = ctypes.c_int32
+
+_PROTOS = {
+    "rsg_abi_version": (ctypes.c_int32, []),
+    "rsg_device_count": (ctypes.c_int32, []),
+    "rsg_sum_head_for": (_st, [ctypes.c_int64, _i32, ctypes.POINTER(SumHead)]),
+    "rsg_ctx_create": (_st, [_i32, ctypes.POINTER(_vp)]),
+    "rsg_ctx_destroy": (None, [_vp]),
+    "rsg_last_error": (ctypes.c_char_p, [_vp]),
+    "rsg_alloc_pinned": (_st, [_vp, _u64, ctypes.POINTER(_vp)]),
+    "rsg_free_pinned": (_st, [_vp, _vp]),
+    "rsg_alloc_device": (_st, [_vp, _u64, ctypes.POINTER(_vp)]),
+    "rsg_free_device": (_st, [_vp, _vp]),
+    "rsg_memcpy_h2d": (_st, [_vp, _vp, _vp, _u64]),
+    "rsg_memcpy_d2h": (_st, [_vp, _vp, _vp, _u64]),
+    "rsg_synchronize": (_st, [_vp, _vp]),
+    "rsg_fill_splitmix64": (_st, [_vp, _vp, _u64, _u64, _vp]),
+    "rsg_plan_block_sums": (_st, [ctypes.POINTER(File), _u64, ctypes.POINTER(SumHead),
+                                  ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
+    "rsg_plan_create": (_st, [_vp, ctypes.POINTER(File), _u64, _u64, ctypes.POINTER(_vp)]),
+    "rsg_plan_destroy": (None, [_vp]),
+    "rsg_plan_total_records": (_u64, [_vp]),
+    "rsg_block_sums_planned": (_st, [_vp, _vp, _vp, _i32, _vp, _vp]),
+    "rsg_block_sums_device": (_st, [_vp, _vp, _u64, ctypes.POINTER(File), _u64, _i32, _vp, _u64]),
+    "rsg_block_sums_host": (_st, [_vp, ctypes.POINTER(File), _u64, _i32, _vp, _u64]),
+    "rsg_hash_search_host": (_st, [_vp, _vp, _u64, ctypes.POINTER(SumHead), _vp, _vp, _vp, _i32,
+                                   ctypes.POINTER(Match), _u64, ctypes.POINTER(_u64)]),
+    "rsg_hash_search_device": (_st, [_vp, _vp, _u64, ctypes.POINTER(SumHead), _vp, _vp, _vp, _i32,
+                                     ctypes.POINTER(Match), _u64, ctypes.POINTER(_u64)]),
+    "rsg_encode_tokens": (_st, [_vp, _u64, ctypes.POINTER(SumHead), ctypes.POINTER(Match), _u64,
+                                _vp, _u64, ctypes.POINTER(_u64)]),
+    "rsg_comm_unique_id": (_st, [_vp]),
+    "rsg_comm_init": (_st, [_vp, _i32, _i32, _vp]),
+    "rsg_gather_bytes": (_st, [_vp, _vp, ctypes.POINTER(_u64), _vp, _i32, _vp]),
+}
+
+for _name, (_res, _args) in _PROTOS.items():
+    _f = getattr(lib, _name)  # AttributeError here = symbol missing from librsg.so
+    _f.restype = _res
+    _f.argtypes = _args
+
+EXPORTED = tuple(_PROTOS)
+
+
+class RsgError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"rsg error {status}: {msg}")
+        self.status = status
+
+
+def check(status: int, ctx=None):
+    if status != OK:
+        msg = lib.rsg_last_error(ctx)
+        raise RsgError(status, msg.decode(errors="replace") if msg else "")
+    return status

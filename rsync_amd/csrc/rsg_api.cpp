@@ -1,0 +1,597 @@
+// rsg_api.cpp -- C-ABI of librsg.so: contexts, block-sum plans, the host
+// (PCIe-inclusive) pipeline, token encoding and the RCCL sums gather.
+// Declarations and contracts: include/rsg.h.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+
+#include "rsg_host.h"
+
+using rsg::DevFile;
+using rsg::kBlockSumThreads;
+using rsg::kRecordBytes;
+
+static thread_local std::string g_thread_err;
+
+namespace rsgh {
+
+rsg_status fail(rsg_ctx *ctx, rsg_status code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    g_thread_err = buf;
+    return code;
+}
+
+rsg_status hip_fail(rsg_ctx *ctx, hipError_t e, const char *what) {
+    return fail(ctx, e == hipErrorOutOfMemory ? RSG_ERR_NOMEM : RSG_ERR_HIP, "%s: %s (%d)", what,
+                hipGetErrorString(e), (int)e);
+}
+
+rsg_status ensure_dev(rsg_ctx *ctx, DevBuf &b, uint64_t bytes) {
+    if (bytes <= b.cap) return RSG_OK;
+    if (b.p) {
+        RSG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        hipFree(b.p);
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    uint64_t want = std::max<uint64_t>(bytes, 4096);
+    RSG_HIP(ctx, hipMalloc(&b.p, want));
+    b.cap = want;
+    return RSG_OK;
+}
+
+rsg_status ensure_pin(rsg_ctx *ctx, PinBuf &b, uint64_t bytes) {
+    if (bytes <= b.cap) return RSG_OK;
+    if (b.p) {
+        hipHostFree(b.p);
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    uint64_t want = std::max<uint64_t>(bytes, 4096);
+    RSG_HIP(ctx, hipHostMalloc(&b.p, want, hipHostMallocDefault));
+    b.cap = want;
+    return RSG_OK;
+}
+
+// rsynccommon.SumSizesSqroot, rsynccommon.go:14-37, or an explicit B.
+bool head_for(int64_t len, int32_t block_len, rsg_sum_head *out) {
+    if (len < 0 || block_len < 0 || block_len > RSG_MAX_BLOCK_LEN) return false;
+    int32_t b = block_len;
+    if (b == 0) {
+        double r = sqrt((double)len);
+        b = r >= 2147483647.0 ? 2147483647 : (int32_t)r;  // int32(math.Sqrt(...)), :22
+        if (b < 700) b = 700;                             // blockSize, :11
+    }
+    int64_t count = (len + ((int64_t)b - 1)) / (int64_t)b;  // :33
+    if (count > INT32_MAX) return false;
+    out->count = (int32_t)count;
+    out->block_len = b;
+    out->s2len = 16;                      // checksumLength, :31
+    out->rem = (int32_t)(len % (int64_t)b);  // :34
+    return true;
+}
+
+rsg_status build_plan(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, uint64_t arena_bytes,
+                      bool use_offsets, HostPlan &plan) {
+    if (nfiles && !files) return fail(ctx, RSG_ERR_INVALID, "files is NULL");
+    if (nfiles >= 0xFFFFFFFFull) return fail(ctx, RSG_ERR_INVALID, "too many files");
+    plan.files.resize(nfiles);
+    uint64_t total = 0, off = 0;
+    bool aligned = true;
+    for (uint64_t i = 0; i < nfiles; i++) {
+        rsg_sum_head h;
+        if (!head_for((int64_t)files[i].len, files[i].block_len, &h))
+            return fail(ctx, RSG_ERR_INVALID, "file %llu: bad length %llu / block_len %d",
+                        (unsigned long long)i, (unsigned long long)files[i].len, files[i].block_len);
+        DevFile &f = plan.files[i];
+        if (use_offsets) {
+            f.offset = files[i].offset;
+            if (files[i].offset > arena_bytes || files[i].len > arena_bytes - files[i].offset)
+                return fail(ctx, RSG_ERR_INVALID, "file %llu: [%llu, +%llu) outside the arena of %llu bytes",
+                            (unsigned long long)i, (unsigned long long)files[i].offset,
+                            (unsigned long long)files[i].len, (unsigned long long)arena_bytes);
+        } else {
+            f.offset = off;
+            off += (files[i].len + 15) & ~15ull;
+        }
+        f.len = files[i].len;
+        f.first_block = total;
+        f.blen = (uint32_t)h.block_len;
+        f.nblocks = (uint32_t)h.count;
+        if (h.count) {
+            if (f.offset & 3) aligned = false;
+            if (h.count > 1 && (f.blen & 3)) aligned = false;
+        }
+        total += (uint64_t)h.count;
+    }
+    plan.total_blocks = total;
+    plan.aligned = aligned;
+    plan.arena_bytes = use_offsets ? arena_bytes : off;
+    const uint64_t nwg = (total + kBlockSumThreads - 1) / kBlockSumThreads;
+    if (nwg >= 0x7FFFFFFFull) return fail(ctx, RSG_ERR_INVALID, "batch too large (%llu blocks)",
+                                          (unsigned long long)total);
+    plan.nwg = (uint32_t)nwg;
+    plan.wg_file.assign(nwg + 1, 0);
+    // wg_file[w] = file owning block min(w*256, total-1).
+    uint64_t f = 0;
+    for (uint64_t w = 0; w <= nwg && total; w++) {
+        uint64_t b = std::min<uint64_t>(w * kBlockSumThreads, total - 1);
+        while (f + 1 < nfiles && plan.files[f + 1].first_block <= b) f++;
+        // skip zero-block files that share first_block with a later file
+        plan.wg_file[w] = (uint32_t)f;
+    }
+    return RSG_OK;
+}
+
+rsg_status launch_plan(rsg_ctx *ctx, const HostPlan &plan, const void *d_files, const void *d_wg,
+                       const void *d_arena, int32_t seed, void *d_records, hipStream_t stream) {
+    if (plan.total_blocks == 0) return RSG_OK;
+    if (!d_arena || !d_records) return fail(ctx, RSG_ERR_INVALID, "NULL device pointer");
+    const bool aligned = plan.aligned && (((uintptr_t)d_arena & 3u) == 0);
+    RSG_HIP(ctx, rsg::launch_block_sums((const uint8_t *)d_arena, plan.arena_bytes, (const DevFile *)d_files,
+                                        (const uint32_t *)d_wg, plan.total_blocks, plan.nwg, aligned,
+                                        (uint32_t)seed, (uint8_t *)d_records, stream));
+    return RSG_OK;
+}
+
+}  // namespace rsgh
+
+using namespace rsgh;
+
+namespace {
+
+struct Lock {
+    rsg_ctx *c;
+    explicit Lock(rsg_ctx *ctx) : c(ctx) { c->mu.lock(); }
+    ~Lock() { c->mu.unlock(); }
+};
+
+#define RSG_ENTER(ctx)                                                             \
+    if (!(ctx)) return fail(nullptr, RSG_ERR_INVALID, "NULL context");            \
+    Lock lock_((ctx));                                                             \
+    RSG_HIP((ctx), hipSetDevice((ctx)->device))
+
+hipStream_t pick_stream(rsg_ctx *ctx, void *stream) {
+    return stream ? (hipStream_t)stream : ctx->stream;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t rsg_abi_version(void) { return RSG_ABI_VERSION; }
+
+int32_t rsg_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    int good = 0;
+    for (int i = 0; i < n; i++) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, i) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) good++;
+    }
+    return good;
+}
+
+rsg_status rsg_sum_head_for(int64_t file_len, int32_t block_len, rsg_sum_head *out) {
+    if (!out) return fail(nullptr, RSG_ERR_INVALID, "out is NULL");
+    if (!head_for(file_len, block_len, out))
+        return fail(nullptr, RSG_ERR_INVALID, "bad length %lld / block_len %d", (long long)file_len, block_len);
+    return RSG_OK;
+}
+
+rsg_status rsg_ctx_create(int32_t device, rsg_ctx **out) {
+    if (!out) return fail(nullptr, RSG_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+        return fail(nullptr, RSG_ERR_NODEV, "no HIP device visible (%s)", hipGetErrorString(e));
+    if (device < 0 || device >= n) return fail(nullptr, RSG_ERR_NODEV, "device %d of %d", device, n);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(nullptr, RSG_ERR_NODEV, "device %d is %s, not gfx950 (MI355X)", device, prop.gcnArchName);
+    rsg_ctx *c = new (std::nothrow) rsg_ctx();
+    if (!c) return fail(nullptr, RSG_ERR_NOMEM, "context allocation");
+    c->device = device;
+    if ((e = hipSetDevice(device)) != hipSuccess || (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->side[0], hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->side[1], hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->side_done[0], hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->side_done[1], hipEventDisableTiming)) != hipSuccess) {
+        rsg_status s = hip_fail(nullptr, e, "context streams");
+        rsg_ctx_destroy(c);
+        return s;
+    }
+    *out = c;
+    return RSG_OK;
+}
+
+void rsg_ctx_destroy(rsg_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    for (int i = 0; i < 2; i++)
+        if (c->side[i]) hipStreamSynchronize(c->side[i]);
+    DevBuf *dbs[] = {&c->d_files, &c->d_wg, &c->d_in[0], &c->d_in[1], &c->d_out[0], &c->d_out[1],
+                     &c->d_desc[0], &c->d_desc[1], &c->d_agg, &c->d_prefix, &c->d_bits, &c->d_counts,
+                     &c->d_list, &c->d_table, &c->d_filter, &c->d_misc};
+    for (DevBuf *b : dbs)
+        if (b->p) hipFree(b->p);
+    PinBuf *pbs[] = {&c->h_in[0], &c->h_in[1], &c->h_out[0], &c->h_out[1], &c->h_desc[0], &c->h_desc[1], &c->h_misc};
+    for (PinBuf *b : pbs)
+        if (b->p) hipHostFree(b->p);
+    if (c->comm) ncclCommDestroy(c->comm);
+    for (int i = 0; i < 2; i++) {
+        if (c->side_done[i]) hipEventDestroy(c->side_done[i]);
+        if (c->side[i]) hipStreamDestroy(c->side[i]);
+    }
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char *rsg_last_error(const rsg_ctx *ctx) { return ctx ? ctx->err.c_str() : g_thread_err.c_str(); }
+
+rsg_status rsg_alloc_pinned(rsg_ctx *ctx, uint64_t bytes, void **out) {
+    RSG_ENTER(ctx);
+    if (!out) return fail(ctx, RSG_ERR_INVALID, "out is NULL");
+    RSG_HIP(ctx, hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    return RSG_OK;
+}
+
+rsg_status rsg_free_pinned(rsg_ctx *ctx, void *p) {
+    RSG_ENTER(ctx);
+    if (p) RSG_HIP(ctx, hipHostFree(p));
+    return RSG_OK;
+}
+
+rsg_status rsg_alloc_device(rsg_ctx *ctx, uint64_t bytes, void **out) {
+    RSG_ENTER(ctx);
+    if (!out) return fail(ctx, RSG_ERR_INVALID, "out is NULL");
+    RSG_HIP(ctx, hipMalloc(out, bytes ? bytes : 1));
+    return RSG_OK;
+}
+
+rsg_status rsg_free_device(rsg_ctx *ctx, void *p) {
+    RSG_ENTER(ctx);
+    if (p) RSG_HIP(ctx, hipFree(p));
+    return RSG_OK;
+}
+
+rsg_status rsg_memcpy_h2d(rsg_ctx *ctx, void *dst, const void *src, uint64_t bytes) {
+    RSG_ENTER(ctx);
+    if (bytes) RSG_HIP(ctx, hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return RSG_OK;
+}
+
+rsg_status rsg_memcpy_d2h(rsg_ctx *ctx, void *dst, const void *src, uint64_t bytes) {
+    RSG_ENTER(ctx);
+    if (bytes) RSG_HIP(ctx, hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return RSG_OK;
+}
+
+rsg_status rsg_synchronize(rsg_ctx *ctx, void *stream) {
+    RSG_ENTER(ctx);
+    RSG_HIP(ctx, hipStreamSynchronize(pick_stream(ctx, stream)));
+    return RSG_OK;
+}
+
+rsg_status rsg_fill_splitmix64(rsg_ctx *ctx, void *d_dst, uint64_t n, uint64_t seed, void *stream) {
+    RSG_ENTER(ctx);
+    if (n && !d_dst) return fail(ctx, RSG_ERR_INVALID, "NULL destination");
+    RSG_HIP(ctx, rsg::launch_fill_splitmix64((uint8_t *)d_dst, n, seed, pick_stream(ctx, stream)));
+    return RSG_OK;
+}
+
+// ---------------------------------------------------------------- block sums
+rsg_status rsg_plan_block_sums(const rsg_file *files, uint64_t nfiles, rsg_sum_head *heads,
+                               uint64_t *first_record, uint64_t *total_records) {
+    if (nfiles && !files) return fail(nullptr, RSG_ERR_INVALID, "files is NULL");
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < nfiles; i++) {
+        rsg_sum_head h;
+        if (!head_for((int64_t)files[i].len, files[i].block_len, &h))
+            return fail(nullptr, RSG_ERR_INVALID, "file %llu: bad length/block_len", (unsigned long long)i);
+        if (heads) heads[i] = h;
+        if (first_record) first_record[i] = total;
+        total += (uint64_t)h.count;
+    }
+    if (total_records) *total_records = total;
+    return RSG_OK;
+}
+
+rsg_status rsg_plan_create(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, uint64_t arena_bytes,
+                           rsg_plan **out) {
+    RSG_ENTER(ctx);
+    if (!out) return fail(ctx, RSG_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    rsg_plan *p = new (std::nothrow) rsg_plan();
+    if (!p) return fail(ctx, RSG_ERR_NOMEM, "plan allocation");
+    p->ctx = ctx;
+    rsg_status s = build_plan(ctx, files, nfiles, arena_bytes, true, p->host);
+    if (s != RSG_OK) {
+        delete p;
+        return s;
+    }
+    hipError_t e;
+    if ((e = hipMalloc(&p->d_files, std::max<uint64_t>(p->host.files.size(), 1) * sizeof(DevFile))) != hipSuccess ||
+        (e = hipMalloc(&p->d_wg, p->host.wg_file.size() * sizeof(uint32_t) + 4)) != hipSuccess ||
+        (e = hipMemcpy(p->d_files, p->host.files.data(), p->host.files.size() * sizeof(DevFile),
+                       hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(p->d_wg, p->host.wg_file.data(), p->host.wg_file.size() * sizeof(uint32_t),
+                       hipMemcpyHostToDevice)) != hipSuccess) {
+        rsg_plan_destroy(p);
+        return hip_fail(ctx, e, "plan upload");
+    }
+    *out = p;
+    return RSG_OK;
+}
+
+void rsg_plan_destroy(rsg_plan *p) {
+    if (!p) return;
+    if (p->ctx) hipSetDevice(p->ctx->device);
+    if (p->d_files) hipFree(p->d_files);
+    if (p->d_wg) hipFree(p->d_wg);
+    delete p;
+}
+
+uint64_t rsg_plan_total_records(const rsg_plan *p) { return p ? p->host.total_blocks : 0; }
+
+rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void *d_arena, int32_t seed,
+                                  void *d_records, void *stream) {
+    RSG_ENTER(ctx);
+    if (!plan || plan->ctx != ctx) return fail(ctx, RSG_ERR_INVALID, "plan belongs to another context");
+    return launch_plan(ctx, plan->host, plan->d_files, plan->d_wg, d_arena, seed, d_records,
+                       pick_stream(ctx, stream));
+}
+
+rsg_status rsg_block_sums_device(rsg_ctx *ctx, const void *d_arena, uint64_t arena_bytes, const rsg_file *files,
+                                 uint64_t nfiles, int32_t seed, void *d_records, uint64_t records_cap) {
+    RSG_ENTER(ctx);
+    HostPlan plan;
+    rsg_status s = build_plan(ctx, files, nfiles, arena_bytes, true, plan);
+    if (s != RSG_OK) return s;
+    if (plan.total_blocks > records_cap)
+        return fail(ctx, RSG_ERR_TRUNCATED, "need %llu records, capacity %llu",
+                    (unsigned long long)plan.total_blocks, (unsigned long long)records_cap);
+    if ((s = ensure_dev(ctx, ctx->d_files, plan.files.size() * sizeof(DevFile) + 32)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_wg, plan.wg_file.size() * sizeof(uint32_t) + 4)) != RSG_OK) return s;
+    RSG_HIP(ctx, hipMemcpyAsync(ctx->d_files.p, plan.files.data(), plan.files.size() * sizeof(DevFile),
+                                hipMemcpyHostToDevice, ctx->stream));
+    RSG_HIP(ctx, hipMemcpyAsync(ctx->d_wg.p, plan.wg_file.data(), plan.wg_file.size() * sizeof(uint32_t),
+                                hipMemcpyHostToDevice, ctx->stream));
+    if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, d_arena, seed, d_records, ctx->stream)) != RSG_OK)
+        return s;
+    RSG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return RSG_OK;
+}
+
+// Host path: files are cut at block boundaries into pieces, pieces are packed
+// into batches of <= kBatchBytes, and two batches are in flight on two streams
+// (host memcpy into pinned staging | H2D + kernel + D2H of the other slot).
+rsg_status rsg_block_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, int32_t seed,
+                               uint8_t *records, uint64_t records_cap) {
+    RSG_ENTER(ctx);
+    const uint64_t kBatchBytes = 64ull << 20;
+    const uint64_t kBatchRecords = 1ull << 22;
+    std::vector<rsg_sum_head> heads(nfiles);
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < nfiles; i++) {
+        if (files[i].len && !files[i].data) return fail(ctx, RSG_ERR_INVALID, "file %llu: NULL data", (unsigned long long)i);
+        if (!head_for((int64_t)files[i].len, files[i].block_len, &heads[i]))
+            return fail(ctx, RSG_ERR_INVALID, "file %llu: bad length/block_len", (unsigned long long)i);
+        total += (uint64_t)heads[i].count;
+    }
+    if (total > records_cap)
+        return fail(ctx, RSG_ERR_TRUNCATED, "need %llu records, capacity %llu", (unsigned long long)total,
+                    (unsigned long long)records_cap);
+    if (total && !records) return fail(ctx, RSG_ERR_INVALID, "records is NULL");
+
+    struct Piece { uint64_t file, b0, b1; };
+    struct Batch { std::vector<Piece> pieces; uint64_t bytes = 0, recs = 0, rec_begin = 0; };
+    std::vector<Batch> batches(1);
+    uint64_t rec = 0;
+    for (uint64_t i = 0; i < nfiles; i++) {
+        const uint64_t B = (uint64_t)heads[i].block_len, cnt = (uint64_t)heads[i].count;
+        uint64_t b0 = 0;
+        while (b0 < cnt) {
+            Batch *bt = &batches.back();
+            uint64_t room_b = bt->bytes < kBatchBytes ? (kBatchBytes - bt->bytes) / B : 0;
+            uint64_t room_r = kBatchRecords - bt->recs;
+            uint64_t take = std::min(std::min(room_b, room_r), cnt - b0);
+            if (take == 0) {
+                if (bt->pieces.empty()) take = 1;  // a single block larger than a batch
+                else {
+                    batches.emplace_back();
+                    batches.back().rec_begin = rec;
+                    continue;
+                }
+            }
+            const uint64_t start = b0 * B, end = std::min<uint64_t>((b0 + take) * B, files[i].len);
+            bt->pieces.push_back({i, b0, b0 + take});
+            bt->bytes += ((end - start) + 15) & ~15ull;
+            bt->recs += take;
+            rec += take;
+            b0 += take;
+        }
+    }
+    rsg_status s;
+    uint64_t max_bytes = 16, max_recs = 1, max_pieces = 1;
+    for (auto &b : batches) {
+        max_bytes = std::max(max_bytes, b.bytes + 16);
+        max_recs = std::max(max_recs, b.recs);
+        max_pieces = std::max<uint64_t>(max_pieces, b.pieces.size());
+    }
+    const uint64_t max_nwg = (max_recs + kBlockSumThreads - 1) / kBlockSumThreads + 1;
+    const uint64_t desc_bytes = max_pieces * sizeof(DevFile) + (max_nwg + 1) * 4 + 64;
+    for (int k = 0; k < 2; k++) {
+        if ((s = ensure_dev(ctx, ctx->d_in[k], max_bytes)) != RSG_OK) return s;
+        if ((s = ensure_dev(ctx, ctx->d_out[k], max_recs * kRecordBytes)) != RSG_OK) return s;
+        if ((s = ensure_dev(ctx, ctx->d_desc[k], desc_bytes)) != RSG_OK) return s;
+        if ((s = ensure_pin(ctx, ctx->h_in[k], max_bytes)) != RSG_OK) return s;
+        if ((s = ensure_pin(ctx, ctx->h_out[k], max_recs * kRecordBytes)) != RSG_OK) return s;
+        if ((s = ensure_pin(ctx, ctx->h_desc[k], desc_bytes)) != RSG_OK) return s;
+    }
+    int64_t pending[2] = {-1, -1};  // batch index in flight per slot
+    auto drain = [&](int slot) -> rsg_status {
+        if (pending[slot] < 0) return RSG_OK;
+        RSG_HIP(ctx, hipEventSynchronize(ctx->side_done[slot]));
+        const Batch &b = batches[(size_t)pending[slot]];
+        memcpy(records + b.rec_begin * kRecordBytes, ctx->h_out[slot].p, b.recs * kRecordBytes);
+        pending[slot] = -1;
+        return RSG_OK;
+    };
+    for (size_t bi = 0; bi < batches.size(); bi++) {
+        const Batch &b = batches[bi];
+        if (b.recs == 0) continue;
+        const int slot = (int)(bi & 1);
+        if ((s = drain(slot)) != RSG_OK) return s;
+        // stage pieces as virtual files in the pinned arena
+        std::vector<rsg_file> vf(b.pieces.size());
+        uint8_t *stage = (uint8_t *)ctx->h_in[slot].p;
+        uint64_t off = 0;
+        for (size_t j = 0; j < b.pieces.size(); j++) {
+            const Piece &pc = b.pieces[j];
+            const uint64_t B = (uint64_t)heads[pc.file].block_len;
+            const uint64_t start = pc.b0 * B, end = std::min<uint64_t>(pc.b1 * B, files[pc.file].len);
+            memcpy(stage + off, files[pc.file].data + start, end - start);
+            vf[j].data = nullptr;
+            vf[j].offset = off;
+            vf[j].len = end - start;
+            vf[j].block_len = (int32_t)B;
+            off += ((end - start) + 15) & ~15ull;
+        }
+        HostPlan plan;
+        if ((s = build_plan(ctx, vf.data(), vf.size(), off, true, plan)) != RSG_OK) return s;
+        uint8_t *hd = (uint8_t *)ctx->h_desc[slot].p;
+        const uint64_t fbytes = plan.files.size() * sizeof(DevFile);
+        const uint64_t wg_off = (fbytes + 63) & ~63ull;
+        memcpy(hd, plan.files.data(), fbytes);
+        memcpy(hd + wg_off, plan.wg_file.data(), plan.wg_file.size() * 4);
+        hipStream_t st = ctx->side[slot];
+        uint8_t *dd = (uint8_t *)ctx->d_desc[slot].p;
+        RSG_HIP(ctx, hipMemcpyAsync(dd, hd, wg_off + plan.wg_file.size() * 4, hipMemcpyHostToDevice, st));
+        RSG_HIP(ctx, hipMemcpyAsync(ctx->d_in[slot].p, stage, off, hipMemcpyHostToDevice, st));
+        if ((s = launch_plan(ctx, plan, dd, dd + wg_off, ctx->d_in[slot].p, seed, ctx->d_out[slot].p, st)) != RSG_OK)
+            return s;
+        RSG_HIP(ctx, hipMemcpyAsync(ctx->h_out[slot].p, ctx->d_out[slot].p, b.recs * kRecordBytes,
+                                    hipMemcpyDeviceToHost, st));
+        RSG_HIP(ctx, hipEventRecord(ctx->side_done[slot], st));
+        pending[slot] = (int64_t)bi;
+    }
+    if ((s = drain(0)) != RSG_OK) return s;
+    if ((s = drain(1)) != RSG_OK) return s;
+    return RSG_OK;
+}
+
+// ---------------------------------------------------------------- tokens
+rsg_status rsg_encode_tokens(const uint8_t *src, uint64_t src_len, const rsg_sum_head *head,
+                             const rsg_match *matches, uint64_t n_matches, uint8_t *out, uint64_t out_cap,
+                             uint64_t *out_len) {
+    if (!head || !out_len || (n_matches && !matches) || (src_len && !src))
+        return fail(nullptr, RSG_ERR_INVALID, "NULL argument");
+    const int64_t B = head->block_len;
+    uint64_t pos = 0, last = 0;
+    bool fits = true;
+    auto put = [&](const void *p, uint64_t n) {
+        if (out && pos + n <= out_cap) memcpy(out + pos, p, n);
+        else if (out) fits = false;
+        pos += n;
+    };
+    auto put_i32 = [&](int32_t v) {
+        uint8_t b[4] = {(uint8_t)v, (uint8_t)(v >> 8), (uint8_t)(v >> 16), (uint8_t)(v >> 24)};
+        put(b, 4);
+    };
+    // simpleSendToken, token.go:4-31
+    auto literal = [&](uint64_t from, uint64_t n) {
+        for (uint64_t l = 0; l < n;) {
+            uint64_t n1 = std::min<uint64_t>(RSG_CHUNK_SIZE, n - l);
+            put_i32((int32_t)n1);
+            put(src + from + l, n1);
+            l += n1;
+        }
+    };
+    for (uint64_t m = 0; m < n_matches; m++) {
+        const int64_t off = matches[m].offset;
+        const int32_t i = matches[m].index;
+        if (i < 0 || i >= head->count || off < (int64_t)last || (uint64_t)off > src_len)
+            return fail(nullptr, RSG_ERR_INVALID, "match %llu out of order or range", (unsigned long long)m);
+        const int64_t len = (i == head->count - 1 && head->rem != 0) ? head->rem : B;
+        if ((uint64_t)(off + len) > src_len) return fail(nullptr, RSG_ERR_INVALID, "match %llu past end", (unsigned long long)m);
+        literal(last, (uint64_t)off - last);  // matched(): literal run then token
+        put_i32(-(i + 1));
+        last = (uint64_t)(off + len);
+    }
+    literal(last, src_len - last);  // matched(size, -1), match.go:212
+    put_i32(0);
+    *out_len = pos;
+    if (!fits) return fail(nullptr, RSG_ERR_TRUNCATED, "token stream needs %llu bytes", (unsigned long long)pos);
+    return RSG_OK;
+}
+
+// ---------------------------------------------------------------- RCCL gather
+rsg_status rsg_comm_unique_id(uint8_t id[128]) {
+    if (!id) return fail(nullptr, RSG_ERR_INVALID, "id is NULL");
+    ncclUniqueId u;
+    ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess) return fail(nullptr, RSG_ERR_HIP, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+    memcpy(id, u.internal, 128);
+    return RSG_OK;
+}
+
+rsg_status rsg_comm_init(rsg_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t id[128]) {
+    RSG_ENTER(ctx);
+    if (!id || nranks < 1 || rank < 0 || rank >= nranks) return fail(ctx, RSG_ERR_INVALID, "bad rank/nranks");
+    if (ctx->comm) {
+        ncclCommDestroy(ctx->comm);
+        ctx->comm = nullptr;
+    }
+    ncclUniqueId u;
+    memcpy(u.internal, id, 128);
+    ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, u, rank);
+    if (r != ncclSuccess) return fail(ctx, RSG_ERR_HIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    return RSG_OK;
+}
+
+rsg_status rsg_gather_bytes(rsg_ctx *ctx, const void *d_send, const uint64_t *send_bytes, void *d_recv,
+                            int32_t root, void *stream) {
+    RSG_ENTER(ctx);
+    if (!ctx->comm) return fail(ctx, RSG_ERR_INVALID, "rsg_comm_init not called");
+    if (!send_bytes || root < 0 || root >= ctx->nranks) return fail(ctx, RSG_ERR_INVALID, "bad gather arguments");
+    hipStream_t st = pick_stream(ctx, stream);
+    ncclResult_t r = ncclGroupStart();
+    if (ctx->rank == root) {
+        uint64_t off = 0;
+        for (int q = 0; q < ctx->nranks; q++) {
+            uint8_t *dst = (uint8_t *)d_recv + off;
+            if (send_bytes[q]) {
+                if (q == root) {
+                    hipError_t e = hipMemcpyAsync(dst, d_send, send_bytes[q], hipMemcpyDeviceToDevice, st);
+                    if (e != hipSuccess) { ncclGroupEnd(); return hip_fail(ctx, e, "gather self copy"); }
+                } else if (r == ncclSuccess) {
+                    r = ncclRecv(dst, send_bytes[q], ncclUint8, q, ctx->comm, st);
+                }
+            }
+            off += send_bytes[q];
+        }
+    } else if (send_bytes[ctx->rank] && r == ncclSuccess) {
+        r = ncclSend(d_send, send_bytes[ctx->rank], ncclUint8, root, ctx->comm, st);
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+        return fail(ctx, RSG_ERR_HIP, "rccl gather: %s", ncclGetErrorString(r != ncclSuccess ? r : r2));
+    return RSG_OK;
+}
+
+}  // extern "C"

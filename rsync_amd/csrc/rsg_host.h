@@ -1,0 +1,88 @@
+// rsg_host.h -- host-side internals of librsg.so shared by the C-ABI units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdint.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rsg.h"
+#include "rsg_internal.h"
+
+// Device buffer that only grows (reused across calls on one context).
+struct DevBuf {
+    void *p = nullptr;
+    uint64_t cap = 0;
+};
+
+// Pinned host buffer that only grows.
+struct PinBuf {
+    void *p = nullptr;
+    uint64_t cap = 0;
+};
+
+struct rsg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t side[2] = {nullptr, nullptr};  // host-path pipeline streams
+    hipEvent_t side_done[2] = {nullptr, nullptr};
+    std::recursive_mutex mu;
+    std::string err;
+    // scratch reused by one-shot calls
+    DevBuf d_files, d_wg;
+    DevBuf d_in[2], d_out[2], d_desc[2];
+    PinBuf h_in[2], h_out[2], h_desc[2];
+    // sender scratch
+    DevBuf d_agg, d_prefix, d_bits, d_counts, d_list, d_table, d_filter, d_misc;
+    PinBuf h_misc;
+    // multi-GPU
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+};
+
+// Plan of a block-sum batch (host side + resident device copies).
+struct HostPlan {
+    std::vector<rsg::DevFile> files;
+    std::vector<uint32_t> wg_file;  // nwg + 1 entries
+    uint64_t total_blocks = 0;
+    uint32_t nwg = 0;
+    bool aligned = true;      // every block start is 4-byte aligned (arena base aside)
+    uint64_t arena_bytes = 0;
+};
+
+struct rsg_plan {
+    rsg_ctx *ctx = nullptr;
+    HostPlan host;
+    void *d_files = nullptr;
+    void *d_wg = nullptr;
+};
+
+namespace rsgh {
+
+rsg_status fail(rsg_ctx *ctx, rsg_status code, const char *fmt, ...);
+rsg_status hip_fail(rsg_ctx *ctx, hipError_t e, const char *what);
+rsg_status ensure_dev(rsg_ctx *ctx, DevBuf &b, uint64_t bytes);
+rsg_status ensure_pin(rsg_ctx *ctx, PinBuf &b, uint64_t bytes);
+
+// Head of one file: reference sizing (block_len == 0) or an explicit B.
+bool head_for(int64_t len, int32_t block_len, rsg_sum_head *out);
+
+// Fill `plan` from files (device offsets when use_offsets, else packed at
+// 16-byte aligned offsets in the order given, which is how the host path lays
+// out its staging arena).  `packed_bytes` receives the arena size needed.
+rsg_status build_plan(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, uint64_t arena_bytes,
+                      bool use_offsets, HostPlan &plan);
+
+// Upload plan descriptors to (grown) device buffers and launch the kernel.
+rsg_status launch_plan(rsg_ctx *ctx, const HostPlan &plan, const void *d_files, const void *d_wg,
+                       const void *d_arena, int32_t seed, void *d_records, hipStream_t stream);
+
+}  // namespace rsgh
+
+#define RSG_HIP(ctx, expr)                                    \
+    do {                                                      \
+        hipError_t e_ = (expr);                               \
+        if (e_ != hipSuccess) return rsgh::hip_fail((ctx), e_, #expr); \
+    } while (0)

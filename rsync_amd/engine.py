@@ -1,0 +1,324 @@
+"""Host-side mirror of the reference's block-checksum surface over librsg.so.
+
+The reference (Go) keeps these entry points, which this module mirrors name
+for name so parity tests read like the reference's own code:
+
+  rsyncchecksum.Checksum1 / Checksum2      rsyncchecksum.go:29-58   -> checksum1 / checksum2
+  rsynccommon.SumSizesSqroot               rsynccommon.go:14-37     -> sum_sizes_sqroot
+  (*receiver.Transfer).generateAndSendSums generator.go:325-350     -> Engine.generate_and_send_sums
+  (*sender.Transfer).hashSearch            match.go:21-230          -> Engine.hash_search
+  matched / simpleSendToken                match.go:233, token.go:4 -> encode_tokens
+
+Every checksum is computed by the HIP kernels; nothing here hashes bytes on
+the CPU.  Errors surface as RsgError (the Go side maps them to `error`).
+"""
+from __future__ import annotations
+
+import ctypes
+import struct
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import File, Match, RsgError, SumHead, check, lib
+
+RECORD_BYTES = _lib.RECORD_BYTES
+
+
+def _u8(buf) -> np.ndarray:
+    if isinstance(buf, np.ndarray):
+        return np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
+    return np.frombuffer(memoryview(buf).cast("B"), dtype=np.uint8)
+
+
+def _ptr(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data) if a.size else ctypes.c_void_p(0)
+
+
+def _i32(x: int) -> int:
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x >= (1 << 31) else x
+
+
+def sum_sizes_sqroot(content_len: int, block_len: int = 0) -> SumHead:
+    """rsynccommon.SumSizesSqroot (rsynccommon.go:14-37); block_len > 0 overrides B."""
+    h = SumHead()
+    check(lib.rsg_sum_head_for(content_len, block_len, ctypes.byref(h)))
+    return h
+
+
+def device_count() -> int:
+    return int(lib.rsg_device_count())
+
+
+class DeviceBuffer:
+    """HBM allocation owned by an Engine (plain device pointer + size)."""
+
+    def __init__(self, engine: "Engine", nbytes: int):
+        self.engine = engine
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(lib.rsg_alloc_device(engine.ctx, max(self.nbytes, 1), ctypes.byref(p)), engine.ctx)
+        self.ptr = p.value
+
+    def upload(self, data, offset: int = 0):
+        a = _u8(data)
+        if offset + a.size > self.nbytes:
+            raise ValueError("upload past the end of the buffer")
+        if a.size:
+            check(lib.rsg_memcpy_h2d(self.engine.ctx, ctypes.c_void_p(self.ptr + offset), _ptr(a), a.size),
+                  self.engine.ctx)
+
+    def download(self, nbytes: Optional[int] = None, offset: int = 0) -> np.ndarray:
+        n = self.nbytes - offset if nbytes is None else int(nbytes)
+        out = np.empty(n, dtype=np.uint8)
+        if n:
+            check(lib.rsg_memcpy_d2h(self.engine.ctx, _ptr(out), ctypes.c_void_p(self.ptr + offset), n),
+                  self.engine.ctx)
+        return out
+
+    def free(self):
+        if self.ptr is not None:
+            lib.rsg_free_device(self.engine.ctx, ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            if self.ptr is not None and self.engine.ctx:
+                self.free()
+        except Exception:
+            pass
+
+
+class Plan:
+    """Device-resident block-sum plan for a fixed file layout in an arena."""
+
+    def __init__(self, engine: "Engine", files: Sequence[Tuple[int, int, int]], arena_bytes: int):
+        self.engine = engine
+        arr = (File * max(len(files), 1))()
+        for i, (off, ln, bl) in enumerate(files):
+            arr[i].offset, arr[i].len, arr[i].block_len = off, ln, bl
+        p = ctypes.c_void_p()
+        check(lib.rsg_plan_create(engine.ctx, arr, len(files), arena_bytes, ctypes.byref(p)), engine.ctx)
+        self.handle = p.value
+        self.total_records = int(lib.rsg_plan_total_records(ctypes.c_void_p(self.handle)))
+        heads = (SumHead * max(len(files), 1))()
+        first = (ctypes.c_uint64 * max(len(files), 1))()
+        check(lib.rsg_plan_block_sums(arr, len(files), heads, first, None))
+        self.heads = [heads[i] for i in range(len(files))]
+        self.first_record = [int(first[i]) for i in range(len(files))]
+
+    def run(self, arena: "DeviceBuffer | int", seed: int, records: "DeviceBuffer | int", stream=None):
+        aptr = arena.ptr if isinstance(arena, DeviceBuffer) else int(arena)
+        rptr = records.ptr if isinstance(records, DeviceBuffer) else int(records)
+        check(lib.rsg_block_sums_planned(self.engine.ctx, ctypes.c_void_p(self.handle), ctypes.c_void_p(aptr),
+                                         _i32(seed), ctypes.c_void_p(rptr), ctypes.c_void_p(stream or 0)),
+              self.engine.ctx)
+
+    def close(self):
+        if self.handle:
+            lib.rsg_plan_destroy(ctypes.c_void_p(self.handle))
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Conn:
+    """Writer side of rsyncwire.Conn (wire.go:131-159): int32 LE + raw bytes."""
+
+    def __init__(self, writer=None):
+        self.buf = bytearray() if writer is None else None
+        self.writer = writer
+
+    def write(self, b: bytes):
+        if self.buf is not None:
+            self.buf += b
+        else:
+            self.writer.write(b)
+
+    def write_int32(self, v: int):
+        self.write(struct.pack("<i", _i32(v)))
+
+
+class Engine:
+    """One device context (rsg_ctx): its own stream, scratch and RCCL comm."""
+
+    def __init__(self, device: int = 0):
+        p = ctypes.c_void_p()
+        check(lib.rsg_ctx_create(device, ctypes.byref(p)))
+        self.ctx = p
+        self.device = device
+
+    def close(self):
+        if self.ctx:
+            lib.rsg_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ memory
+    def alloc(self, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    def fill_splitmix64(self, buf: DeviceBuffer, nbytes: int, seed: int, offset: int = 0, stream=None):
+        check(lib.rsg_fill_splitmix64(self.ctx, ctypes.c_void_p(buf.ptr + offset), nbytes, seed & (2**64 - 1),
+                                      ctypes.c_void_p(stream or 0)), self.ctx)
+
+    def synchronize(self, stream=None):
+        check(lib.rsg_synchronize(self.ctx, ctypes.c_void_p(stream or 0)), self.ctx)
+
+    def plan(self, files: Sequence[Tuple[int, int, int]], arena_bytes: int) -> Plan:
+        return Plan(self, files, arena_bytes)
+
+    # ------------------------------------------------------------ receiver
+    def block_sums(self, files: Sequence, seed: int, block_len=0):
+        """Block sums of host buffers (the PCIe-inclusive path).
+        -> (heads, records bytes, first_record)."""
+        n = len(files)
+        bl = list(block_len) if isinstance(block_len, (list, tuple)) else [block_len] * n
+        arrs = [_u8(f) for f in files]
+        desc = (File * max(n, 1))()
+        for i, a in enumerate(arrs):
+            desc[i].data = a.ctypes.data if a.size else None
+            desc[i].len = a.size
+            desc[i].block_len = bl[i]
+        heads = (SumHead * max(n, 1))()
+        first = (ctypes.c_uint64 * max(n, 1))()
+        total = ctypes.c_uint64()
+        check(lib.rsg_plan_block_sums(desc, n, heads, first, ctypes.byref(total)))
+        out = np.empty(max(total.value, 1) * RECORD_BYTES, dtype=np.uint8)
+        check(lib.rsg_block_sums_host(self.ctx, desc, n, _i32(seed), _ptr(out), total.value), self.ctx)
+        return ([heads[i] for i in range(n)], out[: total.value * RECORD_BYTES].tobytes(),
+                [int(first[i]) for i in range(n)])
+
+    def block_sums_device(self, arena: DeviceBuffer, files: Sequence[Tuple[int, int, int]], seed: int,
+                          records: Optional[DeviceBuffer] = None):
+        """One-shot device-resident call. files = [(offset, len, block_len)]."""
+        n = len(files)
+        desc = (File * max(n, 1))()
+        for i, (off, ln, b) in enumerate(files):
+            desc[i].offset, desc[i].len, desc[i].block_len = off, ln, b
+        total = ctypes.c_uint64()
+        check(lib.rsg_plan_block_sums(desc, n, None, None, ctypes.byref(total)))
+        if records is None:
+            records = self.alloc(max(total.value, 1) * RECORD_BYTES)
+        check(lib.rsg_block_sums_device(self.ctx, ctypes.c_void_p(arena.ptr), arena.nbytes, desc, n, _i32(seed),
+                                        ctypes.c_void_p(records.ptr), records.nbytes // RECORD_BYTES), self.ctx)
+        return records, total.value
+
+    def generate_and_send_sums(self, conn: Conn, data, file_len: int, seed: int, block_len: int = 0):
+        """(*receiver.Transfer).generateAndSendSums (generator.go:325-350):
+        SumHead then count x (int32 sum1, sum2[16]) on conn."""
+        a = _u8(data)
+        if a.size != file_len:
+            raise RsgError(_lib.ERR_INVALID, f"short read: {a.size} of {file_len} bytes")
+        heads, rec, _ = self.block_sums([a], seed, block_len)
+        h = heads[0]
+        conn.write(struct.pack("<4i", *h.astuple()))  # SumHead.WriteTo, types.go:79-86
+        conn.write(rec)
+        return h
+
+    # ------------------------------------------------------------ sender
+    def hash_search(self, src, head, sum1, sum2, targets, seed: int) -> List[Tuple[int, int]]:
+        """(*sender.Transfer).hashSearch (match.go:21-230): the greedy match
+        list [(offset, block index)] in offset order."""
+        a = _u8(src)
+        h = head if isinstance(head, SumHead) else SumHead(*head)
+        s1 = np.ascontiguousarray(sum1, dtype=np.uint32)
+        s2 = np.ascontiguousarray(sum2, dtype=np.uint8).reshape(-1)
+        tg = np.ascontiguousarray(targets, dtype=np.int32)
+        cap = a.size // max(h.block_len, 1) + 2
+        out = (Match * cap)()
+        nm = ctypes.c_uint64()
+        check(lib.rsg_hash_search_host(self.ctx, _ptr(a), a.size, ctypes.byref(h), _ptr(s1), _ptr(s2), _ptr(tg),
+                                       _i32(seed), out, cap, ctypes.byref(nm)), self.ctx)
+        return [(out[i].offset, out[i].index) for i in range(nm.value)]
+
+    def hash_search_device(self, src: DeviceBuffer, src_len: int, head, sum1, sum2, targets, seed: int):
+        h = head if isinstance(head, SumHead) else SumHead(*head)
+        s1 = np.ascontiguousarray(sum1, dtype=np.uint32)
+        s2 = np.ascontiguousarray(sum2, dtype=np.uint8).reshape(-1)
+        tg = np.ascontiguousarray(targets, dtype=np.int32)
+        cap = src_len // max(h.block_len, 1) + 2
+        out = (Match * cap)()
+        nm = ctypes.c_uint64()
+        check(lib.rsg_hash_search_device(self.ctx, ctypes.c_void_p(src.ptr), src_len, ctypes.byref(h), _ptr(s1),
+                                         _ptr(s2), _ptr(tg), _i32(seed), out, cap, ctypes.byref(nm)), self.ctx)
+        return [(out[i].offset, out[i].index) for i in range(nm.value)]
+
+    # ------------------------------------------------------------ multi-GPU
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        check(lib.rsg_comm_unique_id(buf))
+        return buf.raw
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        buf = ctypes.create_string_buffer(bytes(uid), 128)
+        check(lib.rsg_comm_init(self.ctx, nranks, rank, buf), self.ctx)
+
+    def gather_bytes(self, send: DeviceBuffer, send_bytes: Sequence[int], recv: Optional[DeviceBuffer], root: int = 0,
+                     stream=None):
+        sb = (ctypes.c_uint64 * len(send_bytes))(*send_bytes)
+        check(lib.rsg_gather_bytes(self.ctx, ctypes.c_void_p(send.ptr), sb,
+                                   ctypes.c_void_p(recv.ptr if recv is not None else 0), root,
+                                   ctypes.c_void_p(stream or 0)), self.ctx)
+
+
+def encode_tokens(src, head, matches: Iterable[Tuple[int, int]]) -> bytes:
+    """Token bytes of matched()/simpleSendToken (match.go:233-282, token.go:4-31)."""
+    a = _u8(src)
+    h = head if isinstance(head, SumHead) else SumHead(*head)
+    ms = list(matches)
+    arr = (Match * max(len(ms), 1))()
+    for i, (o, ix) in enumerate(ms):
+        arr[i].offset, arr[i].index = o, ix
+    n = ctypes.c_uint64()
+    check(lib.rsg_encode_tokens(_ptr(a), a.size, ctypes.byref(h), arr, len(ms), None, 0, ctypes.byref(n)))
+    out = np.empty(max(n.value, 1), dtype=np.uint8)
+    check(lib.rsg_encode_tokens(_ptr(a), a.size, ctypes.byref(h), arr, len(ms), _ptr(out), n.value,
+                                ctypes.byref(n)))
+    return out[: n.value].tobytes()
+
+
+_default: Optional[Engine] = None
+
+
+def default_engine() -> Engine:
+    global _default
+    if _default is None:
+        _default = Engine(0)
+    return _default
+
+
+def checksum1(buf) -> int:
+    """rsyncchecksum.Checksum1 of one buffer, computed on the GPU (one block of len(buf))."""
+    a = _u8(buf)
+    if a.size == 0:
+        return 0
+    _, rec, _ = default_engine().block_sums([a], 0, a.size)
+    return struct.unpack_from("<I", rec, 0)[0]
+
+
+def checksum2(seed: int, buf) -> bytes:
+    """rsyncchecksum.Checksum2 = MD4(buf || int32_LE(seed)), computed on the GPU."""
+    a = _u8(buf)
+    if a.size == 0:
+        raise RsgError(_lib.ERR_INVALID, "checksum2 of an empty buffer: the block kernel needs >= 1 byte")
+    _, rec, _ = default_engine().block_sums([a], seed, a.size)
+    return rec[4:20]

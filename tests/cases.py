@@ -23,6 +23,23 @@ def splitmix64_bytes(seed: int, n: int) -> np.ndarray:
     return z.astype("<u8").view(np.uint8)[:n].copy()
 
 
+def splitmix64_range(seed: int, start: int, n: int) -> np.ndarray:
+    """Bytes [start, start+n) of the splitmix64(seed) stream (counter-based, so
+    any window of a huge synthetic file is cheap to regenerate)."""
+    w0 = start // 8
+    w1 = (start + n + 7) // 8
+    with np.errstate(over="ignore"):
+        st = (np.uint64(seed & M64) + np.arange(w0 + 1, w1 + 1, dtype=np.uint64)
+              * np.uint64(0x9E3779B97F4A7C15))
+        z = st
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    b = z.astype("<u8").view(np.uint8)
+    o = start - 8 * w0
+    return b[o:o + n].copy()
+
+
 def weak_kat_file() -> np.ndarray:
     """internal/rsyncchecksum/checksum_test.go:12-18,36: 0x11 x 1 MiB || 0xbb x 1 MiB
     || 0xee x 1 MiB."""

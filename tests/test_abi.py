@@ -1,0 +1,96 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every symbol
+include/rsg.h declares, and its host-only arithmetic (sizing, token encoding)
+matches the oracle.  No kernel is launched here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import cases
+from oracle import oracle as orc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    txt = open(os.path.join(ROOT, "include", "rsg.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(rsg_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from rsync_amd import _lib
+    syms = _header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(_lib.lib, s), s
+    assert set(syms) == set(_lib.EXPORTED)
+    assert _lib.lib.rsg_abi_version() == 1
+
+
+def test_no_device_fails_loudly():
+    import rsync_amd
+    if rsync_amd.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(rsync_amd.RsgError) as e:
+        rsync_amd.Engine(0)
+    assert e.value.status == -4
+
+
+def test_product_does_not_import_oracle():
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "rsync_amd")):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h")):
+                txt = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in txt.replace("oracle_", ""), f
+    from rsync_amd import _lib
+    out = os.popen(f"ldd {_lib.LIB_PATH}").read()
+    assert "liboracle" not in out
+
+
+@pytest.mark.parametrize("n,bl", [(0, 0), (1, 0), (490000, 0), (490001, 0), (1 << 20, 0), (1 << 30, 0),
+                                  (32 << 30, 0), (5, 700), (1 << 20, 700), (12345, 1773), (7, 1)])
+def test_sum_sizes(n, bl):
+    import rsync_amd
+    assert rsync_amd.sum_sizes_sqroot(n, bl).astuple() == orc.sum_head(n, bl)
+
+
+def test_sum_sizes_rejects_bad():
+    import rsync_amd
+    with pytest.raises(rsync_amd.RsgError):
+        rsync_amd.sum_sizes_sqroot(-1)
+    with pytest.raises(rsync_amd.RsgError):
+        rsync_amd.sum_sizes_sqroot(10, (1 << 29) + 1)
+
+
+@pytest.mark.parametrize("name", sorted(cases.match_cases()))
+def test_encode_tokens_matches_oracle(name):
+    """rsg_encode_tokens (host formatting) == the oracle's token stream given the
+    oracle's match list (match.go:233-282, token.go:4-31)."""
+    import rsync_amd
+    src, basis, blen, seed = cases.match_cases()[name]
+    head = orc.sum_head(basis.size, blen)
+    rec = orc.block_sums(basis, blen, seed)
+    s1, s2 = orc.parse_records(rec) if head[0] else (np.zeros(0, np.uint32), np.zeros((0, 16), np.uint8))
+    matches, tokens, _ = orc.hash_search(src, head, s1, s2, orc.stable_targets(s1), seed)
+    assert rsync_amd.encode_tokens(src, head, matches) == tokens
+
+
+def test_plan_block_sums_layout():
+    from rsync_amd import _lib
+    lens = cases.ragged_lengths()
+    arr = (_lib.File * len(lens))()
+    for i, n in enumerate(lens):
+        arr[i].len, arr[i].block_len = n, 700
+    heads = (_lib.SumHead * len(lens))()
+    first = (ctypes.c_uint64 * len(lens))()
+    total = ctypes.c_uint64()
+    _lib.check(_lib.lib.rsg_plan_block_sums(arr, len(lens), heads, first, ctypes.byref(total)))
+    acc = 0
+    for i, n in enumerate(lens):
+        assert heads[i].astuple() == orc.sum_head(n, 700)
+        assert first[i] == acc
+        acc += heads[i].count
+    assert total.value == acc

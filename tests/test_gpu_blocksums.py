@@ -1,0 +1,176 @@
+"""GPU parity of the receiver block-sum kernel (generator.go:325-350) against
+the oracle and the golden fixtures.  Everything goes through the C-ABI."""
+import hashlib
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import cases
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import rsync_amd
+    e = rsync_amd.Engine(0)
+    yield e
+    e.close()
+
+
+def load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+def test_weak_kat_through_gpu(eng):
+    """The reference's only pinned values (checksum_test.go:32-73): 1780 weak
+    sums of 1768-byte chunks, computed as blocks by the GPU kernel."""
+    g = load("weak_kat.json")
+    f = cases.weak_kat_file()
+    heads, rec, _ = eng.block_sums([f], 0, g["chunk"])
+    assert heads[0].count == 1780
+    s1 = np.frombuffer(rec, np.uint8).reshape(-1, 20)[:, :4].copy().view("<u4").reshape(-1)
+    for lo, hi, v in g["runs"]:
+        assert (s1[lo:hi + 1] == v).all(), (lo, hi)
+    assert rec == orc.block_sums(f, g["chunk"], 0)
+
+
+def test_cfg1_golden(eng):
+    g = load("block_sums.json")
+    data = cases.splitmix64_bytes(1, 1 << 20)
+    for key in ("cfg1_B1024", "cfg1_B700"):
+        e = g[key]
+        heads, rec, _ = eng.block_sums([data], e["seed"], e["block_len_arg"])
+        assert list(heads[0].astuple()) == e["head"]
+        assert hashlib.sha256(struct.pack("<4i", *heads[0].astuple()) + rec).hexdigest() == e["sha256_head_records"]
+
+
+def test_ragged_golden_host_path(eng):
+    g = load("block_sums.json")["ragged"]
+    for e in g:
+        d = cases.splitmix64_bytes(e["data_seed"], e["len"])
+        heads, rec, _ = eng.block_sums([d], e["seed"], e["block_len"])
+        assert list(heads[0].astuple()) == e["head"]
+        assert hashlib.sha256(rec).hexdigest() == e["sha256_records"], e
+
+
+def test_ragged_batch_one_call(eng):
+    """All ragged files in ONE batch (lanes of one wave straddle files)."""
+    lens = cases.ragged_lengths()
+    for blen, seed in ((700, cases.SEED), (1773, -1), (63, 7), (0, 0)):
+        files = [cases.splitmix64_bytes(2000 + i, n) for i, n in enumerate(lens)]
+        heads, rec, first = eng.block_sums(files, seed, blen)
+        want = b"".join(orc.block_sums(f, blen, seed) for f in files)
+        assert rec == want
+        for i, f in enumerate(files):
+            assert heads[i].astuple() == orc.sum_head(f.size, blen)
+
+
+def _device_case(eng, offsets, lens, blens, seed, arena_bytes=None):
+    end = max(o + n for o, n in zip(offsets, lens)) if lens else 0
+    arena_bytes = arena_bytes or end
+    host = np.zeros(arena_bytes, np.uint8)
+    datas = []
+    for i, (o, n) in enumerate(zip(offsets, lens)):
+        d = cases.splitmix64_bytes(3000 + i, n)
+        host[o:o + n] = d
+        datas.append(d)
+    arena = eng.alloc(arena_bytes)
+    arena.upload(host)
+    recs, total = eng.block_sums_device(arena, list(zip(offsets, lens, blens)), seed)
+    got = recs.download(total * 20).tobytes()
+    want = b"".join(orc.block_sums(d, b, seed) for d, b in zip(datas, blens))
+    return got, want
+
+
+def test_device_unaligned_offsets(eng):
+    """Files at odd arena offsets and odd block lengths: the funnel-shift path."""
+    lens = [5000, 701, 64, 3, 1773 * 3 + 2, 4096]
+    offs, o = [], 1
+    for n in lens:
+        offs.append(o)
+        o += n + 3
+    got, want = _device_case(eng, offs, lens, [700, 701, 13, 700, 1773, 1001], cases.SEED)
+    assert got == want
+
+
+def test_device_file_ends_at_arena_end(eng):
+    """The tail chunk's loads are guarded at the arena end (no over-read)."""
+    for n in (1, 63, 64, 65, 700, 701, 1999):
+        for off in (0, 1, 2, 3, 4):
+            got, want = _device_case(eng, [off], [n], [700], -1, arena_bytes=off + n)
+            assert got == want, (n, off)
+
+
+def test_device_aligned_multi_file(eng):
+    lens = [1 << 20] * 8 + [12345, 0, 77]
+    offs, o = [], 0
+    for n in lens:
+        offs.append(o)
+        o += (n + 15) & ~15
+    got, want = _device_case(eng, offs, lens, [700] * len(lens), cases.SEED)
+    assert got == want
+
+
+def test_planned_cfg2_sampled(eng):
+    """cfg2 at full size (1024 x 1 MiB @ B=700, generated on the device):
+    sampled files bit-exact vs the oracle, record count and layout exact."""
+    n_files, size = 1024, 1 << 20
+    arena = eng.alloc(n_files * size)
+    for f in range(n_files):
+        eng.fill_splitmix64(arena, size, f + 1, offset=f * size)
+    plan = eng.plan([(f * size, size, 700) for f in range(n_files)], n_files * size)
+    assert plan.total_records == n_files * 1498
+    recs = eng.alloc(plan.total_records * 20)
+    plan.run(arena, cases.SEED, recs)
+    eng.synchronize()
+    for f in (0, 1, 511, 1023):
+        got = recs.download(1498 * 20, offset=plan.first_record[f] * 20).tobytes()
+        assert got == orc.block_sums(cases.splitmix64_bytes(f + 1, size), 700, cases.SEED), f
+
+
+def test_large_block_sampled(eng):
+    """cfg5 shape (B = 128 KiB, 2049 MD4 compressions per lane) on a 1 GiB
+    device file: sampled blocks, including the last, vs the oracle."""
+    size, B = (1 << 30) + 1234, 131072
+    arena = eng.alloc(size)
+    eng.fill_splitmix64(arena, size, 55)
+    recs, total = eng.block_sums_device(arena, [(0, size, B)], cases.SEED)
+    assert total == (size + B - 1) // B
+    rng = np.random.default_rng(0)
+    picks = sorted(set(rng.integers(0, total, 24).tolist()) | {0, total - 1})
+    all_rec = recs.download(total * 20).reshape(-1, 20)
+    for b in picks:
+        n = min(B, size - b * B)
+        blk = cases.splitmix64_range(55, b * B, n)
+        assert all_rec[b].tobytes() == orc.block_sums(blk, B, cases.SEED), b
+
+
+def test_host_path_splits_large_file(eng):
+    """A file larger than one staging batch (64 MiB) is cut at block boundaries."""
+    d = cases.splitmix64_bytes(77, (150 << 20) + 333)
+    heads, rec, _ = eng.block_sums([d, d[:1000]], 5, 700)
+    assert rec == orc.block_sums(d, 700, 5) + orc.block_sums(d[:1000], 700, 5)
+
+
+def test_checksum_api(eng):
+    import rsync_amd
+    d = cases.splitmix64_bytes(9, 5000)
+    for n in (1, 3, 4, 55, 56, 64, 700, 5000):
+        assert rsync_amd.checksum1(d[:n]) == orc.checksum1(d[:n])
+        assert rsync_amd.checksum2(-7, d[:n]) == orc.checksum2(-7, d[:n])
+
+
+def test_generate_and_send_sums_wire(eng):
+    import rsync_amd
+    d = cases.splitmix64_bytes(1, 1 << 20)
+    conn = rsync_amd.Conn()
+    eng.generate_and_send_sums(conn, d, d.size, cases.SEED)
+    want = orc.head_bytes(orc.sum_sizes_sqroot(d.size)) + orc.block_sums(d, 0, cases.SEED)
+    assert bytes(conn.buf) == want
