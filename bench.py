@@ -42,10 +42,14 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--warmup-ms", type=float, default=60.0,
+                    help="keep warming up (beyond --warmup steps) until this much time has passed: the "
+                         "GPU takes ~15 ms of back-to-back launches to reach its steady memory clock")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--ab", action="store_true", help="A/B the block-sum kernel variants (interleaved rounds)")
     return ap.parse_args()
 
 
@@ -80,8 +84,13 @@ def main():
     def step(i):
         plan.run(arenas[i & 1], SEED, recs, stream=sptr)
 
-    for i in range(args.warmup):
-        step(i)
+    w0 = time.perf_counter()
+    warm = 0
+    while warm < args.warmup or (time.perf_counter() - w0) * 1e3 < args.warmup_ms:
+        step(warm)
+        warm += 1
+        if warm % 20 == 0:
+            eng.synchronize(sptr)
     eng.synchronize(sptr)
     if world > 1:
         dist.barrier()
@@ -105,12 +114,34 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall, kernel_ms = float(tt[0]), float(tt[1])
 
+    extra = {}
+    if args.ab:
+        from rsync_amd import _lib
+        names = {1: "staged_k1", 10: "diag_staged_memory_only",
+                 11: "diag_staged_hash_only", 13: "diag_linear_read", 14: "diag_linear_read_ldsdma",
+                 15: "diag_staged_memory_only_line_aligned", 16: "diag_staged_memory_only_packed"}
+        res = {v: [] for v in names}
+        for _ in range(5):
+            for v in names:
+                _lib.check(_lib.lib.rsg_set_block_sums_kernel(v))
+                for i in range(3):
+                    step(i)
+                a0 = torch.cuda.Event(enable_timing=True)
+                a1 = torch.cuda.Event(enable_timing=True)
+                a0.record(stream)
+                for i in range(args.steps):
+                    step(i)
+                a1.record(stream)
+                eng.synchronize(sptr)
+                res[v].append(a0.elapsed_time(a1) / args.steps)
+        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+        extra["ab_kernel_ms"] = {names[v]: [round(x, 4) for x in sorted(res[v])] for v in names}
+
     in_bytes = float(arena_bytes)
     out_bytes = float(plan.total_records * rsync_amd.RECORD_BYTES)
     value = world * in_bytes * args.steps / wall / GIB
     achieved = (in_bytes + out_bytes) / (kernel_ms * 1e-3) / 1e9
 
-    extra = {}
     # ---- RCCL gather of every rank's records to rank 0 (the one exchange step)
     if world > 1:
         uid = [rsync_amd.Engine.comm_unique_id() if rank == 0 else None]
@@ -187,6 +218,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_effective": warm,
             "ms_per_step": round(wall * 1e3 / args.steps, 4),
             "higher_is_better": True,
             "scaling": "weak",

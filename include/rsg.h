@@ -138,6 +138,14 @@ uint64_t rsg_plan_total_records(const rsg_plan *plan);
 rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void *d_arena,
                                   int32_t seed, void *d_records, void *stream);
 
+/* Tuning knob (process-wide): block-sum kernel variant.  -1 = automatic
+ * (default), 0 = direct per-lane loads, 1 = staged LDS-DMA slabs, 2 = staged
+ * with 4 blocks per lane, 3 = whole block in registers (blocks <= 703 bytes).
+ * These give identical results; only speed differs.  10..12 are timing
+ * diagnostics whose outputs are meaningless (memory-only / hashing-only).
+ * Unaligned batches always use variant 0. */
+rsg_status rsg_set_block_sums_kernel(int32_t variant);
+
 /* One-shot device call: plan + launch + wait. */
 rsg_status rsg_block_sums_device(rsg_ctx *ctx, const void *d_arena, uint64_t arena_bytes,
                                  const rsg_file *files, uint64_t nfiles, int32_t seed,

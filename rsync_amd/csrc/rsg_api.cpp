@@ -86,6 +86,7 @@ rsg_status build_plan(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, uint
     if (nfiles && !files) return fail(ctx, RSG_ERR_INVALID, "files is NULL");
     if (nfiles >= 0xFFFFFFFFull) return fail(ctx, RSG_ERR_INVALID, "too many files");
     plan.files.resize(nfiles);
+    plan.max_blen = 0;
     uint64_t total = 0, off = 0;
     bool aligned = true;
     for (uint64_t i = 0; i < nfiles; i++) {
@@ -108,6 +109,7 @@ rsg_status build_plan(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, uint
         f.first_block = total;
         f.blen = (uint32_t)h.block_len;
         f.nblocks = (uint32_t)h.count;
+        if (h.count && f.blen > plan.max_blen) plan.max_blen = f.blen;
         if (h.count) {
             if (f.offset & 3) aligned = false;
             if (h.count > 1 && (f.blen & 3)) aligned = false;
@@ -140,7 +142,7 @@ rsg_status launch_plan(rsg_ctx *ctx, const HostPlan &plan, const void *d_files, 
     const bool aligned = plan.aligned && (((uintptr_t)d_arena & 3u) == 0);
     RSG_HIP(ctx, rsg::launch_block_sums((const uint8_t *)d_arena, plan.arena_bytes, (const DevFile *)d_files,
                                         (const uint32_t *)d_wg, plan.total_blocks, plan.nwg, aligned,
-                                        (uint32_t)seed, (uint8_t *)d_records, stream));
+                                        plan.max_blen, (uint32_t)seed, (uint8_t *)d_records, stream));
     return RSG_OK;
 }
 
@@ -352,6 +354,13 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
     if (!plan || plan->ctx != ctx) return fail(ctx, RSG_ERR_INVALID, "plan belongs to another context");
     return launch_plan(ctx, plan->host, plan->d_files, plan->d_wg, d_arena, seed, d_records,
                        pick_stream(ctx, stream));
+}
+
+rsg_status rsg_set_block_sums_kernel(int32_t variant) {
+    if (variant < -1 || (variant > 3 && variant < 10) || variant > 16)
+        return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..3 or 10..16");
+    rsg::set_block_sums_variant(variant);
+    return RSG_OK;
 }
 
 rsg_status rsg_block_sums_device(rsg_ctx *ctx, const void *d_arena, uint64_t arena_bytes, const rsg_file *files,

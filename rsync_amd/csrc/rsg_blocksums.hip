@@ -18,6 +18,8 @@
 // wave); 20 bytes written per block.  Roofline: HBM read.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "rsg_internal.h"
 #include "rsg_md4.h"
@@ -81,19 +83,62 @@ __device__ __forceinline__ void hash_chunk(const uint32_t W[16], uint32_t w16, u
     md4_compress(h, X);
 }
 
-// ALIGNED: every block starts 4-byte aligned (all file offsets and block
-// lengths are multiples of 4), so message words are plain loads; otherwise
-// each word is funnel-shifted out of two aligned words (v_alignbyte_b32).
+// Tail of a block: chunk `nfull` holds the last r = n % 64 data bytes (words W,
+// plus w16 = the next aligned word when not ALIGNED), then the 4 seed bytes
+// (rsyncchecksum.go:56), then RFC 1320 padding (0x80, zeros, 64-bit bit length).
+// Word kd = r/4 holds the last rb = r%4 data bytes followed by seed bytes, word
+// kd+1 the rest of the seed and the 0x80; everything after is zero up to the
+// length words.  One or two compressions (two when r >= 52).
 template <bool ALIGNED>
-__global__ __launch_bounds__(kBlockSumThreads) void block_sums_kernel(
-    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
-    const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed,
-    uint8_t *__restrict__ out) {
-    const uint64_t g = (uint64_t)blockIdx.x * kBlockSumThreads + threadIdx.x;
-    if (g >= total_blocks) return;
+__device__ __forceinline__ void hash_tail(const uint32_t W[16], uint32_t w16, uint32_t sh, uint32_t n,
+                                          uint32_t seed, uint32_t h[4], int32_t &s1, uint32_t &t) {
+    const uint32_t nfull = n >> 6;
+    const uint32_t r = n & 63u, kd = r >> 2, rb = r & 3u;
+    const uint32_t mask = rb ? ((1u << (8 * rb)) - 1u) : 0u;
+    const uint32_t wB = rb ? ((seed >> (32 - 8 * rb)) | (0x80u << (8 * rb))) : 0x80u;
+    const uint32_t lenlo = (n + 4u) << 3, lenhi = (n + 4u) >> 29;
+    const bool two = r >= 52;
+    uint32_t X[16], XD[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t dk = ALIGNED ? W[k] : __builtin_amdgcn_alignbyte(k < 15 ? W[k + 1] : w16, W[k], sh);
+        const uint32_t wA = rb ? ((dk & mask) | (seed << (8 * rb))) : seed;
+        const uint32_t uk = (uint32_t)k;
+        X[k] = uk < kd ? dk : (uk == kd ? wA : (uk == kd + 1 ? wB : 0u));
+        XD[k] = uk < kd ? dk : (uk == kd ? (dk & mask) : 0u);
+    }
+    if (!two) { X[14] = lenlo; X[15] = lenhi; }
+    {
+        const int32_t s1b = s1;
+        int32_t tl = 0;
+        weak_chunk(XD, s1, tl);
+        t += (uint32_t)tl + (nfull << 6) * (uint32_t)(s1 - s1b);
+    }
+    md4_compress(h, X);
+    if (two) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) X[k] = 0;
+        X[0] = (kd + 1 == 16) ? wB : 0u;
+        X[14] = lenlo; X[15] = lenhi;
+        md4_compress(h, X);
+    }
+}
 
-    // File of block g: the largest f in [wg_file[wg], wg_file[wg+1]] with
-    // first_block <= g (zero-length files own no blocks and are skipped).
+// Record g = int32 LE Checksum1 then the 16 MD4 digest bytes (generator.go:341-346).
+__device__ __forceinline__ void store_record(uint8_t *out, uint64_t g, uint32_t n, int32_t s1, uint32_t t,
+                                             const uint32_t h[4]) {
+    const uint32_t s2 = n * (uint32_t)s1 - t;  // sum (n - i) x_i
+    const uint32_t sum1 = ((uint32_t)s1 & 0xffffu) | (s2 << 16);  // rsyncchecksum.go:50
+    uint32_t *o = reinterpret_cast<uint32_t *>(out + g * kRecordBytes);
+    o[0] = sum1;
+    o[1] = h[0]; o[2] = h[1]; o[3] = h[2]; o[4] = h[3];
+}
+
+// File of block g: the largest f in [wg_file[wg], wg_file[wg+1]] with
+// first_block <= g (zero-length files own no blocks and are skipped).
+// Returns the block's arena offset and length (generator.go:334).
+__device__ __forceinline__ void locate_block(const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file,
+                                             uint64_t g, uint64_t &off, uint32_t &n) {
     uint32_t lo = wg_file[blockIdx.x], hi = wg_file[blockIdx.x + 1];
     while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
@@ -103,23 +148,25 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_kernel(
     const uint64_t bi = g - F.first_block;
     const uint64_t boff = bi * F.blen;
     const uint64_t left = F.len - boff;
-    const uint32_t n = left < F.blen ? (uint32_t)left : F.blen;  // generator.go:334
+    n = left < F.blen ? (uint32_t)left : F.blen;
+    off = F.offset + boff;
+}
 
-    const uint8_t *p = arena + F.offset + boff;
-    const uintptr_t end = (uintptr_t)(arena + arena_bytes);
+// One lane hashes its whole block with its own 16-byte loads (one chunk of
+// prefetch).  ALIGNED: the block starts 4-byte aligned, so message words are
+// plain loads; otherwise each word is funnel-shifted out of two aligned words.
+template <bool ALIGNED>
+__device__ __forceinline__ void hash_block_direct(const uint8_t *arena, uintptr_t end, uint64_t off, uint32_t n,
+                                                  uint32_t seed, uint32_t h[4], int32_t &s1, uint32_t &t) {
+    const uint8_t *p = arena + off;
     const uint32_t sh = ALIGNED ? 0u : (uint32_t)((uintptr_t)p & 3u);
     const uint8_t *p0 = p - sh;
     const uint32_t nfull = n >> 6;
-
-    uint32_t h[4];
-    md4_init(h);
-    int32_t s1 = 0;  // sum x_i (wrapping, as the reference's uint32)
-    uint32_t t = 0;  // sum i*x_i
     uint32_t A[16], B[16];
     // Chunks 0..nfull-1 hold only file bytes.  Chunk c+1 is loaded before chunk
-    // c is hashed (one chunk of prefetch per lane); every load except the one
-    // of the tail chunk stays inside the block, so only that one is guarded.
-    // Unrolled by two so the double buffer needs no register copies.
+    // c is hashed; every load except the one of the tail chunk stays inside the
+    // block, so only that one is guarded.  Unrolled by two so the double buffer
+    // needs no register copies.
     uint32_t c = 0;
     if (nfull == 0) {
         load16_guarded(p0, end, A);
@@ -143,63 +190,402 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_kernel(
             for (int k = 0; k < 16; k++) A[k] = B[k];
         }
     }
-    const uint32_t *cur = A;
-
-    // Tail: r data bytes, then the 4 seed bytes (rsyncchecksum.go:56), then
-    // RFC 1320 padding (0x80, zeros, 64-bit bit length).  Word kd holds the
-    // last rb data bytes followed by seed bytes; word kd+1 the rest of the seed
-    // and the 0x80; everything after is zero up to the length words.
     const uint32_t extra = ALIGNED ? 0u : load_word_guarded(p0 + 64u * nfull + 64u, end);
-    const uint32_t r = n & 63u, kd = r >> 2, rb = r & 3u;
-    const uint32_t mask = rb ? ((1u << (8 * rb)) - 1u) : 0u;
-    const uint32_t wB = rb ? ((seed >> (32 - 8 * rb)) | (0x80u << (8 * rb))) : 0x80u;
-    const uint32_t lenlo = (n + 4u) << 3, lenhi = (n + 4u) >> 29;
-    const bool two = r >= 52;
-    uint32_t X[16], XD[16];
+    hash_tail<ALIGNED>(A, extra, sh, n, seed, h, s1, t);
+}
+
+// Variant "direct": one lane per block, per-lane loads.  Handles any
+// alignment; the staged kernel below falls back to it for edge waves.
+template <bool ALIGNED>
+__global__ __launch_bounds__(kBlockSumThreads) void block_sums_direct(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    const uint64_t g = (uint64_t)blockIdx.x * kBlockSumThreads + threadIdx.x;
+    if (g >= total_blocks) return;
+    uint64_t off;
+    uint32_t n;
+    locate_block(files, wg_file, g, off, n);
+    uint32_t h[4];
+    md4_init(h);
+    int32_t s1 = 0;  // sum x_i (wrapping, as the reference's uint32)
+    uint32_t t = 0;  // sum i*x_i
+    hash_block_direct<ALIGNED>(arena, (uintptr_t)(arena + arena_bytes), off, n, seed, h, s1, t);
+    store_record(out, g, n, s1, t, h);
+}
+
+// ---------------------------------------------------------------- staged variant
+// Coalesced HBM reads: a wave owns 64 consecutive blocks (one per lane) and
+// streams them through a private LDS slab 256 bytes (4 MD4 chunks) of every
+// block at a time.  The slab is filled by buffer_load_dwordx4 ... lds (LDS DMA,
+// no VGPRs in flight): each DMA wave-instruction fetches 4 contiguous 256-byte
+// pieces, so every cache line is consumed by one instruction instead of by 64
+// scattered per-lane loads.  Piece j (lane j's block) sits at j*272 in the slab:
+// the 16-byte pad makes the per-lane ds_read_b128 of one unit conflict-free
+// (bank = 4*(j + unit) mod 64 inside every 16-lane group).  While the wave
+// hashes segment s out of registers, segment s+1 is already in flight.
+constexpr uint32_t kSegBytes = 256;
+constexpr uint32_t kPiece = kSegBytes + 16;          // padded piece stride in LDS
+constexpr uint32_t kWaveSlab = 64 * kPiece;          // 17408 bytes per wave
+constexpr uint32_t kDmaPerSeg = kWaveSlab / 1024;    // 17 DMA instructions per segment
+static_assert(kWaveSlab % 1024 == 0, "slab must be a whole number of DMA instructions");
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const uint32_t dk = ALIGNED ? cur[k] : __builtin_amdgcn_alignbyte(k < 15 ? cur[k + 1] : extra, cur[k], sh);
-        const uint32_t wA = rb ? ((dk & mask) | (seed << (8 * rb))) : seed;
-        const uint32_t uk = (uint32_t)k;
-        X[k] = uk < kd ? dk : (uk == kd ? wA : (uk == kd + 1 ? wB : 0u));
-        XD[k] = uk < kd ? dk : (uk == kd ? (dk & mask) : 0u);
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint64_t o = __shfl_xor(v, m, 64);
+        v = o > v ? o : v;
     }
-    if (!two) { X[14] = lenlo; X[15] = lenhi; }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint64_t o = __shfl_xor(v, m, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+// MODE 0 = the product kernel.  Timing diagnostics (outputs meaningless):
+// MODE 1 = DMA + LDS reads only (memory ceiling of this access pattern),
+// MODE 2 = hashing only, no DMA (compute ceiling),
+// MODE 3 = as MODE 1 with every piece rounded down to a 128-byte line,
+// MODE 4 = as MODE 1 with the wave's blocks packed back to back (768 B apart).
+//
+// K = consecutive blocks per lane.  A line that straddles two blocks is
+// needed by the end of one block and the start of the next; when both blocks
+// belong to the same lane the two uses are one segment apart and the second
+// is an L2 hit, whereas across lanes they are a whole block apart and the line
+// is often refetched from HBM.  K = 4 cuts those refetches by 4x.
+template <int K, int MODE>
+__global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * kWaveSlab];
+    const uint32_t lane = threadIdx.x & 63u;
+    // readfirstlane: provably wave-uniform values keep the LDS base (M0) and
+    // the buffer descriptor in SGPRs (no waterfall loops around the DMA).
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t *slab = slab_all + wave * kWaveSlab;
+    const uint64_t wave_first = ((uint64_t)blockIdx.x * (kBlockSumThreads / 64) + wave) * 64u * K;
+    const uint64_t g0 = wave_first + (uint64_t)lane * K;
+
+    // Locate the lane's K blocks: binary search for the first, then walk.
+    uint64_t off[K];
+    uint32_t n[K];
     {
-        const int32_t s1b = s1;
-        int32_t tl = 0;
-        weak_chunk(XD, s1, tl);
-        t += (uint32_t)tl + (nfull << 6) * (uint32_t)(s1 - s1b);
-    }
-    md4_compress(h, X);
-    if (two) {
+        uint32_t lo = wg_file[blockIdx.x * K];
+        uint32_t hi = wg_file[min((blockIdx.x + 1) * K, nwg256)];
+        const uint64_t gq = g0 < total_blocks ? g0 : total_blocks - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (files[mid].first_block <= gq) lo = mid; else hi = mid - 1;
+        }
+        DevFile F = files[lo];
 #pragma unroll
-        for (int k = 0; k < 16; k++) X[k] = 0;
-        X[0] = (kd + 1 == 16) ? wB : 0u;
-        X[14] = lenlo; X[15] = lenhi;
-        md4_compress(h, X);
+        for (int k = 0; k < K; k++) {
+            const uint64_t g = g0 + k;
+            if (g < total_blocks) {
+                while (g >= F.first_block + F.nblocks) F = files[++lo];
+                const uint64_t boff = (g - F.first_block) * F.blen;
+                const uint64_t left = F.len - boff;
+                n[k] = left < F.blen ? (uint32_t)left : F.blen;  // generator.go:334
+                off[k] = F.offset + boff;
+            } else {
+                n[k] = 0;
+                off[k] = 0;
+            }
+        }
     }
 
-    const uint32_t s2 = n * (uint32_t)s1 - t;  // sum (n - i) x_i
-    const uint32_t sum1 = ((uint32_t)s1 & 0xffffu) | (s2 << 16);  // rsyncchecksum.go:50
-    uint32_t *o = reinterpret_cast<uint32_t *>(out + g * kRecordBytes);
-    o[0] = sum1;
-    o[1] = h[0]; o[2] = h[1]; o[3] = h[2]; o[4] = h[3];
+    // Wave-uniform choice of path: the staged path needs all 64*K blocks,
+    // every DMA read inside the arena and the wave's span addressable by a
+    // 32-bit buffer offset.  Otherwise (last partial wave, a file ending at
+    // the arena's end, giant spans) the wave runs the direct path.
+    uint32_t S[K];
+    uint64_t lo_off = ~0ull, hi_end = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t nseg = n[k] ? ((n[k] >> 6) >> 2) + 1 : 0;  // segments through the tail chunk
+        S[k] = __builtin_amdgcn_readfirstlane((uint32_t)wave_max_u64(nseg));
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        if (n[k]) {
+            lo_off = off[k] < lo_off ? off[k] : lo_off;
+            const uint64_t e = off[k] + (uint64_t)kSegBytes * S[k];
+            hi_end = e > hi_end ? e : hi_end;
+        }
+    }
+    const uint64_t base_v = wave_min_u64(lo_off);
+    const uint64_t base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(base_v >> 32)) << 32) |
+                          __builtin_amdgcn_readfirstlane((uint32_t)base_v);
+    const uint64_t top = wave_max_u64(hi_end);
+    const bool staged = (wave_first + 64u * K - 1 < total_blocks) && top <= arena_bytes &&
+                        (top - base) <= 0x7FFFFFFFull;
+    if (!staged) {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            if (n[k] == 0) continue;
+            uint32_t h[4];
+            md4_init(h);
+            int32_t s1 = 0;
+            uint32_t t = 0;
+            hash_block_direct<true>(arena, (uintptr_t)(arena + arena_bytes), off[k], n[k], seed, h, s1, t);
+            store_record(out, g0 + k, n[k], s1, t, h);
+        }
+        return;
+    }
+
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(arena + (MODE == 3 ? base & ~127ull : base)), (short)0,
+                                          0x7FFFFFFF, 0x00020000);
+    uint32_t rel[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) rel[k] = MODE == 3 ? (uint32_t)(off[k] - (base & ~127ull)) & ~127u
+                                       : MODE == 4 ? (lane * K + k) * 768u
+                                                   : (uint32_t)(off[k] - base);
+
+    // DMA instruction i, lane t fills slab bytes [16*(64 i + t), +16): piece
+    // j = (64 i + t) / 17 (lane j's block), unit u = (64 i + t) % 17.  u == 16
+    // is the pad: its offset is past num_records, so the buffer range check
+    // drops it without a memory request.
+    uint32_t voff[kDmaPerSeg];
+    auto build_voff = [&](uint32_t kb) {
+        uint32_t r = rel[0];
+#pragma unroll
+        for (int k = 1; k < K; k++) r = (kb == (uint32_t)k) ? rel[k] : r;
+#pragma unroll
+        for (uint32_t i = 0; i < kDmaPerSeg; i++) {
+            const uint32_t idx = 64u * i + lane;
+            const uint32_t j = idx / 17u, u = idx - 17u * j;
+            const uint32_t v = __shfl(r, (int)j, 64) + 16u * u;
+            voff[i] = u < 16u ? v : 0x80000000u;  // pad slot: out of range, no memory request
+        }
+    };
+    auto dma_segment = [&](uint32_t s) {
+#pragma unroll
+        for (uint32_t i = 0; i < kDmaPerSeg; i++)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rsrc, (__attribute__((address_space(3))) void *)(slab + 1024u * i), 16, voff[i], kSegBytes * s, 0, 0);
+    };
+    uint32_t R[64];
+    const uint8_t *mine = slab + lane * kPiece;
+    auto read_segment = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
+            R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+
+    // Flattened schedule over (block k, segment s); the DMA cursor runs one
+    // step ahead of the compute cursor.
+    uint32_t dk = 0, ds = 0;
+    auto next_cursor = [&](uint32_t &k, uint32_t &s) {
+        uint32_t sk = S[0];
+#pragma unroll
+        for (int q = 1; q < K; q++) sk = (k == (uint32_t)q) ? S[q] : sk;
+        if (++s >= sk) { s = 0; k++; }
+    };
+    build_voff(0);
+    if (MODE != 2) dma_segment(0);
+    next_cursor(dk, ds);
+    read_segment();
+#pragma unroll 1
+    for (uint32_t ck = 0; ck < (uint32_t)K; ck++) {
+        uint32_t nk = n[0];
+        uint32_t sk = S[0];
+#pragma unroll
+        for (int q = 1; q < K; q++) {
+            nk = (ck == (uint32_t)q) ? n[q] : nk;
+            sk = (ck == (uint32_t)q) ? S[q] : sk;
+        }
+        const uint32_t nfull = nk >> 6;
+        uint32_t h[4];
+        md4_init(h);
+        int32_t s1 = 0;
+        uint32_t t = 0;
+#pragma unroll 1
+        for (uint32_t cs = 0; cs < sk; cs++) {
+            const bool more = dk < (uint32_t)K;
+            if (more) {
+                if (ds == 0) build_voff(dk);
+                if (MODE != 2) dma_segment(ds);
+                next_cursor(dk, ds);
+            }
+            if (MODE == 1 || MODE == 3 || MODE == 4) {
+#pragma unroll
+                for (int q = 0; q < 64; q++) h[q & 3] ^= R[q];
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < 4; i++) {
+                    const uint32_t c = 4u * cs + i;
+                    if (c < nfull) hash_chunk<true>(R + 16 * i, 0u, 0u, c, h, s1, t);
+                    else if (c == nfull) hash_tail<true>(R + 16 * i, 0u, 0u, nk, seed, h, s1, t);
+                }
+            }
+            if (more) read_segment();
+        }
+        store_record(out, g0 + ck, nk, s1, t, h);
+    }
 }
+
+// ---------------------------------------------------------------- register-block variant
+// For blocks of at most kRegMaxBytes (the reference's default 700-byte blocks,
+// SumSizesSqroot for every file up to 490 000 bytes): each lane loads its whole
+// block into VGPRs with back-to-back 16-byte loads, so a wave requests its
+// entire 44.8 KB tile in one burst (every shared cache line is requested by
+// neighbouring lanes of the same burst, and DRAM rows are opened once), then
+// hashes from registers.  Two waves per SIMD alternate load and hash phases.
+constexpr uint32_t kRegChunks = 11;                  // data chunks held per lane
+constexpr uint32_t kRegMaxBytes = 64 * kRegChunks - 1;  // 703: tail chunk index <= 10
+
+template <int MODE>
+__global__ __launch_bounds__(kBlockSumThreads) void block_sums_regblock(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    const uint64_t g = (uint64_t)blockIdx.x * kBlockSumThreads + threadIdx.x;
+    if (g >= total_blocks) return;
+    uint64_t off;
+    uint32_t n;
+    locate_block(files, wg_file, g, off, n);
+    const uint8_t *p = arena + off;
+    const uintptr_t end = (uintptr_t)(arena + arena_bytes);
+    const uint32_t nvec = (n + 15) >> 4;  // 16-byte loads covering the block
+    uint32_t R[16 * kRegChunks];
+    if ((uintptr_t)p + 16u * nvec <= end) {
+#pragma unroll
+        for (uint32_t j = 0; j < 4 * kRegChunks; j++) {
+            if (j < nvec) {
+                const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(p + 16 * j);
+                R[4 * j + 0] = v.x; R[4 * j + 1] = v.y; R[4 * j + 2] = v.z; R[4 * j + 3] = v.w;
+            } else {
+                R[4 * j + 0] = R[4 * j + 1] = R[4 * j + 2] = R[4 * j + 3] = 0;
+            }
+        }
+    } else {  // the block's last vector would cross the arena end
+#pragma unroll
+        for (uint32_t j = 0; j < 4 * kRegChunks; j++)
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                R[4 * j + q] = j < nvec ? load_word_guarded(p + 16 * j + 4 * q, end) : 0u;
+    }
+    uint32_t h[4];
+    md4_init(h);
+    int32_t s1 = 0;
+    uint32_t t = 0;
+    const uint32_t nfull = n >> 6;
+    if (MODE == 1) {
+#pragma unroll
+        for (int q = 0; q < 16 * (int)kRegChunks; q++) h[q & 3] ^= R[q];
+    } else {
+#pragma unroll
+        for (uint32_t c = 0; c < kRegChunks; c++) {
+            if (c < nfull) hash_chunk<true>(R + 16 * c, 0u, 0u, c, h, s1, t);
+            else if (c == nfull) hash_tail<true>(R + 16 * c, 0u, 0u, n, seed, h, s1, t);
+        }
+    }
+    store_record(out, g, n, s1, t, h);
+}
+
+// ---------------------------------------------------------------- read ceilings
+// Timing diagnostics only: the fastest way to read the same arena with no
+// hashing, i.e. the empirical HBM-read roofline of this box for DESIGN.md.
+// LDS = false: coalesced global_load_dwordx4, 4 in flight per lane;
+// LDS = true: the same bytes through buffer_load_dwordx4 ... lds.
+template <bool LDS>
+__global__ __launch_bounds__(256) void diag_linear_read(const uint8_t *__restrict__ arena, uint64_t bytes,
+                                                        uint32_t *__restrict__ sink) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[4 * 4096];
+    const uint64_t per_iter = (uint64_t)gridDim.x * 256 * 64;  // 4 x 16 B per lane
+    uint32_t acc = 0;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 * 64; base + 256 * 64 <= bytes; base += per_iter) {
+        if (LDS) {
+            const uint64_t wb = base + wave * 4096;
+            const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)(arena + ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(wb >> 32)) << 32 |
+                                  __builtin_amdgcn_readfirstlane((uint32_t)wb))),
+                (short)0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    r, (__attribute__((address_space(3))) void *)(buf + wave * 4096 + 1024 * i), 16,
+                    (threadIdx.x & 63) * 16, 1024 * i, 0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            acc ^= *reinterpret_cast<const uint32_t *>(buf + wave * 4096 + (threadIdx.x & 63) * 4);
+        } else {
+            const u32x4a4 *q = reinterpret_cast<const u32x4a4 *>(arena + base + threadIdx.x * 16);
+            u32x4a4 v[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) v[i] = q[256 * i];
+#pragma unroll
+            for (int i = 0; i < 4; i++) acc ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
+        }
+    }
+    if (acc == 0x12345678u) sink[0] = acc;  // keep the loads alive
+}
+
+// Kernel variants (rsg_set_block_sums_kernel): -1 = automatic, 0 = direct,
+// 1 = staged K=1, 2 = staged K=4, 3 = register-block.  Timing diagnostics with
+// meaningless outputs: 10 = staged K=1 memory only, 11 = staged K=1 hashing
+// only, 12 = register-block memory only, 13/14 = linear read of the arena
+// (plain loads / LDS DMA).
+static int g_variant = -2;  // -2 = not yet read from RSG_BLOCKSUMS_KERNEL
 
 hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const DevFile *files,
                              const uint32_t *wg_file, uint64_t total_blocks, uint32_t nwg, bool aligned,
-                             uint32_t seed, uint8_t *out, hipStream_t stream) {
+                             uint32_t max_blen, uint32_t seed, uint8_t *out, hipStream_t stream) {
     if (total_blocks == 0) return hipSuccess;
+    if (g_variant == -2) {
+        const char *e = getenv("RSG_BLOCKSUMS_KERNEL");
+        g_variant = e ? atoi(e) : -1;
+    }
+    int v = g_variant;
+    if (v == -1) v = 1;  // automatic choice
+    if (!aligned && v < 13) v = 0;
+    if ((v == 3 || v == 12) && max_blen > kRegMaxBytes) v = 1;
     dim3 grid(nwg), block(kBlockSumThreads);
-    if (aligned)
-        hipLaunchKernelGGL(block_sums_kernel<true>, grid, block, 0, stream, arena, arena_bytes, files,
-                           wg_file, total_blocks, seed, out);
-    else
-        hipLaunchKernelGGL(block_sums_kernel<false>, grid, block, 0, stream, arena, arena_bytes, files,
-                           wg_file, total_blocks, seed, out);
+#define RSG_LAUNCH(KERNEL, GRID) \
+    hipLaunchKernelGGL(KERNEL, GRID, block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out)
+#define RSG_STAGED(KK, MM)                                                                                      \
+    hipLaunchKernelGGL((block_sums_staged<KK, MM>), dim3((uint32_t)((total_blocks + 256u * KK - 1) / (256u * KK))), \
+                       block, 0, stream, arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out)
+    switch (v) {
+        case 0:
+            if (aligned) RSG_LAUNCH(block_sums_direct<true>, grid);
+            else RSG_LAUNCH(block_sums_direct<false>, grid);
+            break;
+        case 2: RSG_STAGED(4, 0); break;
+        case 3: RSG_LAUNCH(block_sums_regblock<0>, grid); break;
+        case 10: RSG_STAGED(1, 1); break;
+        case 11: RSG_STAGED(1, 2); break;
+        case 15: RSG_STAGED(1, 3); break;
+        case 16: RSG_STAGED(1, 4); break;
+        case 12: RSG_LAUNCH(block_sums_regblock<1>, grid); break;
+        case 13:
+            hipLaunchKernelGGL(diag_linear_read<false>, dim3(2048), dim3(256), 0, stream, arena, arena_bytes,
+                               (uint32_t *)out);
+            break;
+        case 14:
+            hipLaunchKernelGGL(diag_linear_read<true>, dim3(2048), dim3(256), 0, stream, arena, arena_bytes,
+                               (uint32_t *)out);
+            break;
+        default: RSG_STAGED(1, 0); break;
+    }
+#undef RSG_LAUNCH
+#undef RSG_STAGED
     return hipGetLastError();
 }
+
+void set_block_sums_variant(int v) { g_variant = v; }
 
 // ------------------------------------------------------------------ synthetic data
 __global__ void fill_splitmix64_kernel(uint8_t *dst, uint64_t n, uint64_t seed) {

@@ -49,6 +49,7 @@ struct HostPlan {
     uint64_t total_blocks = 0;
     uint32_t nwg = 0;
     bool aligned = true;      // every block start is 4-byte aligned (arena base aside)
+    uint32_t max_blen = 0;    // largest block length (picks blocks per lane)
     uint64_t arena_bytes = 0;
 };
 

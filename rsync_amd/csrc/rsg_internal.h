@@ -21,7 +21,10 @@ static_assert(sizeof(DevFile) == 32, "DevFile layout");
 
 hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const DevFile *files,
                              const uint32_t *wg_file, uint64_t total_blocks, uint32_t nwg, bool aligned,
-                             uint32_t seed, uint8_t *out, hipStream_t stream);
+                             uint32_t max_blen, uint32_t seed, uint8_t *out, hipStream_t stream);
+
+// 0 = direct (per-lane loads), 1 = staged (LDS DMA, default for aligned batches).
+void set_block_sums_variant(int v);
 
 hipError_t launch_fill_splitmix64(uint8_t *dst, uint64_t n, uint64_t seed, hipStream_t stream);
 

@@ -174,3 +174,26 @@ def test_generate_and_send_sums_wire(eng):
     eng.generate_and_send_sums(conn, d, d.size, cases.SEED)
     want = orc.head_bytes(orc.sum_sizes_sqroot(d.size)) + orc.block_sums(d, 0, cases.SEED)
     assert bytes(conn.buf) == want
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("blen", [700, 64, 1773, 4096, 131072])
+def test_kernel_variants_match(eng, variant, blen):
+    """Every kernel variant (direct / staged K=1 / staged K=4 / register-block)
+    gives the oracle's records, including waves that straddle files."""
+    from rsync_amd import _lib
+    lens = [1 << 20, 700 * 64 * 3 + 5, 12345, 64, 1, 0, 300_001]
+    files = [cases.splitmix64_bytes(4000 + i, n) for i, n in enumerate(lens)]
+    want = b"".join(orc.block_sums(f, blen, cases.SEED) for f in files)
+    try:
+        _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))
+        _, rec, _ = eng.block_sums(files, cases.SEED, blen)
+        arena = eng.alloc(sum(lens))
+        offs = np.cumsum([0] + lens[:-1]).tolist()
+        arena.upload(np.concatenate(files))
+        recs, total = eng.block_sums_device(arena, [(o, n, blen) for o, n in zip(offs, lens)], cases.SEED)
+        rec_dev = recs.download(total * 20).tobytes()
+    finally:
+        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+    assert rec == want
+    assert rec_dev == want

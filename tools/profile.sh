@@ -1,0 +1,16 @@
+#!/bin/bash
+# Collects the rocprofv3 evidence for the bench kernel: a kernel-trace + stats
+# pass, then separate PMC passes (never combined with trace domains).
+# Usage: tools/profile.sh <tag> [bench args...]
+set -o pipefail
+TAG=${1:-r01}; shift
+ARGS=${@:---steps 20 --warmup 3 --no-cpu --no-host-path}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || exit 1
+for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY" "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"; do
+  N=$(echo $P | tr ' ' '_' | cut -c1-40)
+  timeout -k 10 300 rocprofv3 --pmc $P --output-format csv -d $OUT/pmc_$N -o pmc -- python3 bench.py $ARGS > $OUT/pmc_$N.log 2>&1 || echo "pmc pass $P failed rc=$?" >> $OUT/errors.txt
+done
+exit 0
