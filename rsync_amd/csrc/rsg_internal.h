@@ -26,6 +26,33 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
 // 0 = direct (per-lane loads), 1 = staged (LDS DMA, default for aligned batches).
 void set_block_sums_variant(int v);
 
+// ---- sender search (rsg_match_kernels.hip)
+constexpr uint32_t kScanTile = 32768;                          // source bytes per tile
+constexpr uint32_t kRollThreads = 1024;                        // lanes per roll workgroup
+constexpr uint32_t kRollPerThread = kScanTile / kRollThreads;  // consecutive offsets per lane
+constexpr uint32_t kFilterBits = 1u << 19;                     // 64 KiB LDS bitmap
+
+struct TileAgg {     // per tile: whole tile and its first r = B % kScanTile bytes
+    uint32_t a1, a2;  // sum x, sum (i - tile_start) * x
+    uint32_t r1, r2;
+};
+struct TilePrefix {  // at a tile start: P = sum_{i<j} x_i, Q = sum_{i<j} i * x_i (mod 2^32)
+    uint32_t p, q;
+};
+
+// Bitmap slot of a 32-bit weak sum (low half s1, high half s2).
+__host__ __device__ inline uint32_t filter_index_host(uint32_t sum) {
+    return ((sum & 0xffffu) ^ ((sum >> 16) << 3)) & (kFilterBits - 1);
+}
+
+hipError_t launch_tile_agg(const uint8_t *src, uint64_t size, uint32_t r, TileAgg *out, uint32_t ntiles,
+                           hipStream_t stream);
+hipError_t launch_tile_scan(const TileAgg *agg, uint32_t ntiles, TilePrefix *pre, hipStream_t stream);
+hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
+                       uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
+                       const uint32_t *bitmap, const uint64_t *table, uint32_t table_bits, uint64_t *cand,
+                       uint32_t cap, uint32_t *count, uint32_t grid, hipStream_t stream);
+
 hipError_t launch_fill_splitmix64(uint8_t *dst, uint64_t n, uint64_t seed, hipStream_t stream);
 
 }  // namespace rsg

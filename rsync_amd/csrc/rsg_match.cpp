@@ -1,24 +1,321 @@
-// rsg_match.cpp -- sender hash search (match.go:21-230) orchestration.
+// rsg_match.cpp -- sender hash search (internal/sender/match.go:21-230) on the GPU.
+//
+// Division of labour:
+//   GPU  weak sum at every offset + exact-equivalent filter against the basis
+//        sums (rsg_match_kernels.hip), and the strong sum (MD4 || seed) plus
+//        Checksum1 of every window the greedy walk needs to confirm
+//        (rsg_blocksums.hip, the same kernel the receiver uses).
+//   host the greedy walk of match.go over the (sorted, sparse) candidate
+//        offsets: O(candidates), no hashing.
+// The result is exactly the (offset, block index) sequence hashSearch passes
+// to matched(): a visited offset q (q = 0, or q < end = size + 1 - lastLen,
+// match.go:70) matches the FIRST block i in `targets` order with
+// Sum1_i == weak(q), Len_i == min(B, size - q) and MD4(window || seed)[:s2len]
+// == Sum2_i[:s2len] (match.go:108-136); after a match the next visited offset
+// is q + Len_i (match.go:158), otherwise q + 1.
+#include <string.h>
+
+#include <algorithm>
+#include <unordered_map>
+#include <vector>
+
 #include "rsg_host.h"
 
 using namespace rsgh;
+using rsg::DevFile;
+using rsg::kRecordBytes;
+using rsg::kScanTile;
+using rsg::TileAgg;
+using rsg::TilePrefix;
+
+namespace {
+
+constexpr uint32_t kCandCap = 1u << 22;      // candidates per roll launch (32 MiB)
+constexpr uint64_t kSparseBatch = 1u << 16;  // windows per verification batch
+
+struct Search {
+    rsg_ctx *ctx;
+    hipStream_t st;
+    const uint8_t *d_src;
+    uint64_t size;
+    rsg_sum_head head;
+    const uint8_t *sum2;
+    int32_t seed;
+    int64_t end;  // visited offsets are q < end (end >= 1: offset 0 is always visited)
+    std::unordered_map<uint32_t, std::vector<int32_t>> groups;  // sum1 -> blocks in targets order
+    std::unordered_map<uint64_t, int32_t> verified;             // offset -> block index or -1
+    std::vector<rsg_match> out;
+
+    int64_t len_of(int32_t i) const {
+        return (i == head.count - 1 && head.rem != 0) ? head.rem : head.block_len;  // sender.go:135-139
+    }
+    uint32_t window(uint64_t q) const {
+        return (uint32_t)std::min<uint64_t>((uint64_t)head.block_len, size - q);  // match.go:114-117
+    }
+};
+
+// Confirm a batch of window offsets: Checksum1 + MD4(window || seed) on the GPU,
+// then the first block in targets order whose sums and length agree.
+rsg_status verify(Search &S, const std::vector<uint64_t> &qs) {
+    if (qs.empty()) return RSG_OK;
+    rsg_ctx *ctx = S.ctx;
+    std::vector<rsg_file> wins(qs.size());
+    for (size_t i = 0; i < qs.size(); i++) {
+        wins[i].data = nullptr;
+        wins[i].offset = qs[i];
+        wins[i].len = S.window(qs[i]);
+        wins[i].block_len = (int32_t)wins[i].len;
+        wins[i].reserved = 0;
+    }
+    HostPlan plan;
+    rsg_status s = build_plan(ctx, wins.data(), wins.size(), S.size, true, plan);
+    if (s != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_files, plan.files.size() * sizeof(DevFile) + 32)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_wg, plan.wg_file.size() * sizeof(uint32_t) + 4)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_out[0], plan.total_blocks * kRecordBytes)) != RSG_OK) return s;
+    RSG_HIP(ctx, hipMemcpyAsync(ctx->d_files.p, plan.files.data(), plan.files.size() * sizeof(DevFile),
+                                hipMemcpyHostToDevice, S.st));
+    RSG_HIP(ctx, hipMemcpyAsync(ctx->d_wg.p, plan.wg_file.data(), plan.wg_file.size() * sizeof(uint32_t),
+                                hipMemcpyHostToDevice, S.st));
+    if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, S.d_src, S.seed, ctx->d_out[0].p, S.st)) != RSG_OK)
+        return s;
+    std::vector<uint8_t> rec(plan.total_blocks * kRecordBytes);
+    RSG_HIP(ctx, hipMemcpyAsync(rec.data(), ctx->d_out[0].p, rec.size(), hipMemcpyDeviceToHost, S.st));
+    RSG_HIP(ctx, hipStreamSynchronize(S.st));
+    for (size_t i = 0; i < qs.size(); i++) {
+        const uint8_t *r = rec.data() + i * kRecordBytes;
+        uint32_t w;
+        memcpy(&w, r, 4);
+        int32_t res = -1;
+        auto it = S.groups.find(w);
+        if (it != S.groups.end()) {
+            const int64_t k = (int64_t)wins[i].len;
+            for (int32_t b : it->second) {  // targets order, match.go:108
+                if (S.len_of(b) != k) continue;  // :118
+                if (memcmp(r + 4, S.sum2 + 16 * (int64_t)b, (size_t)S.head.s2len) != 0) continue;  // :133
+                res = b;
+                break;
+            }
+        }
+        S.verified[qs[i]] = res;
+    }
+    return RSG_OK;
+}
+
+// Greedy walk over one range's sorted candidates (match.go:93-210 reduced to
+// the offsets where the weak sum can hit).
+rsg_status walk(Search &S, const std::vector<uint64_t> &C, uint64_t &pos) {
+    size_t i = std::lower_bound(C.begin(), C.end(), pos) - C.begin();
+    while (i < C.size()) {
+        const uint64_t c = C[i];
+        if ((int64_t)c >= S.end) break;
+        auto it = S.verified.find(c);
+        if (it == S.verified.end()) {
+            // Batch: every pending candidate ahead while they are sparse (the
+            // hashing they cost stays below twice the span they cover); in
+            // dense stretches (repetitive data) follow the chain of offsets the
+            // walk visits if each confirmation succeeds, plus the candidate
+            // after each one in case it fails.
+            std::vector<uint64_t> batch;
+            uint64_t hashed = 0;
+            size_t j = i;
+            for (; j < C.size() && batch.size() < kSparseBatch && (int64_t)C[j] < S.end; j++) {
+                if (!S.verified.count(C[j])) {
+                    batch.push_back(C[j]);
+                    hashed += S.window(C[j]);
+                }
+            }
+            const uint64_t span = (j > i ? C[j - 1] - c : 0) + (uint64_t)S.head.block_len;
+            if (hashed > 2 * span + (1u << 20)) {
+                batch.clear();
+                uint64_t x = c;
+                for (int n = 0; n < 4096; n++) {
+                    size_t a = std::lower_bound(C.begin() + i, C.end(), x) - C.begin();
+                    if (a >= C.size() || (int64_t)C[a] >= S.end) break;
+                    if (!S.verified.count(C[a])) batch.push_back(C[a]);
+                    if (a + 1 < C.size() && (int64_t)C[a + 1] < S.end && !S.verified.count(C[a + 1]))
+                        batch.push_back(C[a + 1]);
+                    x = C[a] + S.window(C[a]);
+                }
+                std::sort(batch.begin(), batch.end());
+                batch.erase(std::unique(batch.begin(), batch.end()), batch.end());
+            }
+            rsg_status s = verify(S, batch);
+            if (s != RSG_OK) return s;
+            it = S.verified.find(c);
+        }
+        const int32_t b = it->second;
+        if (b >= 0) {
+            S.out.push_back(rsg_match{(int64_t)c, b, 0});
+            pos = c + (uint64_t)S.len_of(b);  // match.go:158 + the roll
+            i = std::lower_bound(C.begin() + i, C.end(), pos) - C.begin();
+        } else {
+            pos = c + 1;
+            i++;
+        }
+    }
+    return RSG_OK;
+}
+
+rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_sum_head *head, const uint32_t *sum1,
+                  const uint8_t *sum2, const int32_t *targets, int32_t seed, rsg_match *matches, uint64_t match_cap,
+                  uint64_t *n_matches) {
+    Search S;
+    S.seed = seed;
+    S.ctx = ctx;
+    S.st = ctx->stream;
+    S.d_src = d_src;
+    S.size = size;
+    S.head = *head;
+    S.sum2 = sum2;
+    const int64_t B = head->block_len;
+    const int32_t count = head->count;
+    const int64_t last_len = (head->rem != 0) ? head->rem : B;
+    S.end = std::max<int64_t>((int64_t)size + 1 - last_len, 1);  // match.go:70 (offset 0 always visited)
+
+    // Basis sums grouped by Sum1 in targets order; device filter = bitmap of
+    // every Sum1 + open-addressing table {Sum1, flags: bit1 = a block of
+    // length B, bit2 = the remainder block}.
+    std::unordered_map<uint32_t, uint32_t> flags;
+    S.groups.reserve((size_t)count * 2);
+    for (int32_t k = 0; k < count; k++) {
+        const int32_t i = targets[k];
+        S.groups[sum1[i]].push_back(i);
+        uint32_t &f = flags[sum1[i]];
+        f |= 1u;
+        f |= (S.len_of(i) == B) ? 2u : 4u;
+    }
+    uint32_t tbits = 10;
+    while ((1ull << tbits) < 2ull * flags.size()) tbits++;
+    std::vector<uint64_t> table(1ull << tbits, 0);
+    std::vector<uint32_t> bitmap(rsg::kFilterBits / 32, 0);
+    for (auto &kv : flags) {
+        const uint32_t key = kv.first;
+        uint32_t h = (key * 0x9E3779B1u) >> (32 - tbits);
+        while ((uint32_t)table[h] != 0) h = (h + 1) & ((1u << tbits) - 1);
+        table[h] = ((uint64_t)key << 32) | kv.second;
+        const uint32_t fi = rsg::filter_index_host(key);
+        bitmap[fi >> 5] |= 1u << (fi & 31);
+    }
+    const uint64_t ntiles64 = (size + kScanTile - 1) / kScanTile;
+    if (ntiles64 >= 0xFFFFFFF0ull) return fail(ctx, RSG_ERR_INVALID, "source too large");
+    const uint32_t ntiles = (uint32_t)ntiles64;
+    rsg_status s;
+    if ((s = ensure_dev(ctx, ctx->d_filter, bitmap.size() * 4)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_table, table.size() * 8)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_agg, (uint64_t)ntiles * sizeof(TileAgg) + 64)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_prefix, ((uint64_t)ntiles + 1) * sizeof(TilePrefix) + 64)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_list, (uint64_t)kCandCap * 8)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_counts, 64)) != RSG_OK) return s;
+    RSG_HIP(ctx, hipMemcpyAsync(ctx->d_filter.p, bitmap.data(), bitmap.size() * 4, hipMemcpyHostToDevice, S.st));
+    RSG_HIP(ctx, hipMemcpyAsync(ctx->d_table.p, table.data(), table.size() * 8, hipMemcpyHostToDevice, S.st));
+    const uint32_t r = (uint32_t)(B % kScanTile);
+    RSG_HIP(ctx, rsg::launch_tile_agg(d_src, size, r, (TileAgg *)ctx->d_agg.p, ntiles, S.st));
+    RSG_HIP(ctx, rsg::launch_tile_scan((const TileAgg *)ctx->d_agg.p, ntiles, (TilePrefix *)ctx->d_prefix.p, S.st));
+
+    int dev_cus = 256;
+    hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    const uint64_t scan_end = std::min<uint64_t>((uint64_t)S.end, size);
+    const uint32_t tile_end = (uint32_t)((scan_end + kScanTile - 1) / kScanTile);
+    uint32_t lo = 0, span = tile_end;
+    uint64_t pos = 0;
+    std::vector<uint64_t> C;
+    while (lo < tile_end) {
+        const uint32_t hi = std::min(tile_end, lo + span);
+        if ((uint64_t)hi * kScanTile <= pos) {  // the walk already jumped past this range
+            lo = hi;
+            continue;
+        }
+        RSG_HIP(ctx, hipMemsetAsync(ctx->d_counts.p, 0, 4, S.st));
+        RSG_HIP(ctx, rsg::launch_roll(d_src, size, (uint32_t)B, (uint32_t)head->rem, (uint64_t)S.end, lo, hi,
+                                      (const TileAgg *)ctx->d_agg.p, (const TilePrefix *)ctx->d_prefix.p, ntiles,
+                                      (const uint32_t *)ctx->d_filter.p, (const uint64_t *)ctx->d_table.p, tbits,
+                                      (uint64_t *)ctx->d_list.p, kCandCap, (uint32_t *)ctx->d_counts.p,
+                                      (uint32_t)dev_cus, S.st));
+        uint32_t n = 0;
+        RSG_HIP(ctx, hipMemcpyAsync(&n, ctx->d_counts.p, 4, hipMemcpyDeviceToHost, S.st));
+        RSG_HIP(ctx, hipStreamSynchronize(S.st));
+        if (n > kCandCap) {  // dense range (repetitive data): halve it and retry
+            if (hi - lo == 1) return fail(ctx, RSG_ERR_INVALID, "internal: candidate overflow in one tile");
+            span = std::max<uint32_t>(1, (hi - lo) / 2);
+            continue;
+        }
+        C.resize(n);
+        if (n) RSG_HIP(ctx, hipMemcpy(C.data(), ctx->d_list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost));
+        std::sort(C.begin(), C.end());
+        if ((s = walk(S, C, pos)) != RSG_OK) return s;
+        lo = hi;
+    }
+    *n_matches = S.out.size();
+    const uint64_t ncopy = std::min<uint64_t>(S.out.size(), match_cap);
+    if (ncopy) memcpy(matches, S.out.data(), ncopy * sizeof(rsg_match));
+    if (S.out.size() > match_cap)
+        return fail(ctx, RSG_ERR_TRUNCATED, "%llu matches, capacity %llu", (unsigned long long)S.out.size(),
+                    (unsigned long long)match_cap);
+    return RSG_OK;
+}
+
+// SumHead.ReadFrom validation (types.go:38-77) plus the arrays' consistency.
+rsg_status check_args(rsg_ctx *ctx, const rsg_sum_head *head, const uint32_t *sum1, const uint8_t *sum2,
+                      const int32_t *targets, rsg_match *matches, uint64_t match_cap, uint64_t *n_matches) {
+    if (!head || !n_matches) return fail(ctx, RSG_ERR_INVALID, "NULL head or n_matches");
+    if (head->count < 0) return fail(ctx, RSG_ERR_INVALID, "invalid checksum count %d", head->count);
+    if (head->block_len < 0 || head->block_len > RSG_MAX_BLOCK_LEN)
+        return fail(ctx, RSG_ERR_INVALID, "invalid block length %d", head->block_len);
+    if (head->s2len < 0 || head->s2len > 16) return fail(ctx, RSG_ERR_INVALID, "invalid checksum length %d", head->s2len);
+    if (head->rem < 0 || head->rem > head->block_len)
+        return fail(ctx, RSG_ERR_INVALID, "invalid remainder length %d", head->rem);
+    if (head->count > 0 && head->block_len == 0) return fail(ctx, RSG_ERR_INVALID, "zero block length");
+    if (head->count > 0 && (!sum1 || !sum2 || !targets)) return fail(ctx, RSG_ERR_INVALID, "NULL sums or targets");
+    if (match_cap && !matches) return fail(ctx, RSG_ERR_INVALID, "NULL matches");
+    std::vector<uint8_t> seen((size_t)head->count, 0);
+    for (int32_t k = 0; k < head->count; k++) {
+        const int32_t i = targets[k];
+        if (i < 0 || i >= head->count || seen[(size_t)i]) return fail(ctx, RSG_ERR_INVALID, "targets is not a permutation");
+        seen[(size_t)i] = 1;
+    }
+    return RSG_OK;
+}
+
+}  // namespace
 
 extern "C" {
-
-rsg_status rsg_hash_search_host(rsg_ctx *ctx, const uint8_t *src, uint64_t src_len, const rsg_sum_head *head,
-                                const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets, int32_t seed,
-                                rsg_match *matches, uint64_t match_cap, uint64_t *n_matches) {
-    (void)src; (void)src_len; (void)head; (void)sum1; (void)sum2; (void)targets; (void)seed;
-    (void)matches; (void)match_cap; (void)n_matches;
-    return fail(ctx, RSG_ERR_INVALID, "hash search not built yet");
-}
 
 rsg_status rsg_hash_search_device(rsg_ctx *ctx, const void *d_src, uint64_t src_len, const rsg_sum_head *head,
                                   const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets, int32_t seed,
                                   rsg_match *matches, uint64_t match_cap, uint64_t *n_matches) {
-    (void)d_src; (void)src_len; (void)head; (void)sum1; (void)sum2; (void)targets; (void)seed;
-    (void)matches; (void)match_cap; (void)n_matches;
-    return fail(ctx, RSG_ERR_INVALID, "hash search not built yet");
+    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    RSG_HIP(ctx, hipSetDevice(ctx->device));
+    rsg_status s = check_args(ctx, head, sum1, sum2, targets, matches, match_cap, n_matches);
+    if (s != RSG_OK) return s;
+    *n_matches = 0;
+    if (head->count == 0 || src_len == 0) return RSG_OK;  // sendFile path / empty source: no matches
+    if (!d_src) return fail(ctx, RSG_ERR_INVALID, "NULL source");
+    const uint8_t *src = (const uint8_t *)d_src;
+    if ((uintptr_t)src & 15u) {  // the scan kernels read 16-byte vectors at 16-byte strides
+        if ((s = ensure_dev(ctx, ctx->d_misc, src_len + 64)) != RSG_OK) return s;
+        RSG_HIP(ctx, hipMemcpyAsync(ctx->d_misc.p, src, src_len, hipMemcpyDeviceToDevice, ctx->stream));
+        src = (const uint8_t *)ctx->d_misc.p;
+    }
+    return search(ctx, src, src_len, head, sum1, sum2, targets, seed, matches, match_cap, n_matches);
+}
+
+rsg_status rsg_hash_search_host(rsg_ctx *ctx, const uint8_t *src, uint64_t src_len, const rsg_sum_head *head,
+                                const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets, int32_t seed,
+                                rsg_match *matches, uint64_t match_cap, uint64_t *n_matches) {
+    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    RSG_HIP(ctx, hipSetDevice(ctx->device));
+    rsg_status s = check_args(ctx, head, sum1, sum2, targets, matches, match_cap, n_matches);
+    if (s != RSG_OK) return s;
+    *n_matches = 0;
+    if (head->count == 0 || src_len == 0) return RSG_OK;
+    if (!src) return fail(ctx, RSG_ERR_INVALID, "NULL source");
+    if ((s = ensure_dev(ctx, ctx->d_misc, src_len + 64)) != RSG_OK) return s;
+    RSG_HIP(ctx, hipMemcpyAsync(ctx->d_misc.p, src, src_len, hipMemcpyHostToDevice, ctx->stream));
+    return search(ctx, (const uint8_t *)ctx->d_misc.p, src_len, head, sum1, sum2, targets, seed, matches,
+                  match_cap, n_matches);
 }
 
 }  // extern "C"

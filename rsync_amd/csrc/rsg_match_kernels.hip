@@ -1,2 +1,305 @@
-// rsg_match_kernels.hip -- sender kernels (filled in next).
+// rsg_match_kernels.hip -- sender search kernels (internal/sender/match.go:21-230).
+//
+// The reference slides a block-length window one byte at a time over the
+// source, rolling the weak sum (match.go:171-196) and looking every offset up
+// in a 16-bit tag table (match.go:95-108).  Here every offset is independent:
+// the weak sum of the window [q, e), e = min(q + B, size), is
+//     S1 = P[e] - P[q],  S2 = e*(P[e] - P[q]) - (Q[e] - Q[q])   (mod 2^16)
+// with P[j] = sum_{i<j} x_i and Q[j] = sum_{i<j} i*x_i over sign-extended
+// bytes (SignExtend, rsyncchecksum.go:24-27).  Three kernels:
+//   tile_agg   one pass over the source: per 32 KiB tile, (sum x, sum i*x) of
+//              the whole tile and of its first r = B mod 32768 bytes;
+//   tile_scan  exclusive prefix of the tile sums (P, Q at every tile start);
+//   roll       per tile, 1024 lanes x 32 consecutive offsets: initial window
+//              from the prefixes plus a workgroup scan, then the reference's
+//              own rolling update; each offset is tested against an exact-
+//              equivalent filter (64 KiB LDS bitmap keyed on the full 32-bit
+//              sum, then an L2-resident hash table of the basis sums with the
+//              block lengths present) and survivors are appended as
+//              candidates.  Candidates are confirmed on the host side of the
+//              C-ABI with the strong-sum kernel (rsg_blocksums.hip) in the
+//              greedy order of match.go (rsg_match.cpp).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
 #include "rsg_internal.h"
+
+namespace rsg {
+
+typedef uint32_t u32x4a4m __attribute__((ext_vector_type(4), aligned(4)));
+
+__device__ __forceinline__ int32_t sx8(uint32_t w, int b) {
+    return (int32_t)(w << (24 - 8 * b)) >> 24;  // SignExtend of byte b of w
+}
+
+// Four little-endian words of src[pos, pos+16); bytes at or past `size` read 0.
+// The fast path needs pos 4-byte aligned (the caller guarantees it).
+__device__ __forceinline__ void load_vec(const uint8_t *src, uint64_t size, uint64_t pos, uint32_t w[4]) {
+    if (pos + 16 <= size) {
+        const u32x4a4m v = *reinterpret_cast<const u32x4a4m *>(src + pos);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const uint64_t p = pos + 4 * q + b;
+                if (p < size) x |= (uint32_t)src[p] << (8 * b);
+            }
+            w[q] = x;
+        }
+    }
+}
+
+// sum x and sum k*x (k = 0..15) of one 16-byte vector, signed bytes.
+__device__ __forceinline__ void vec_sums(const uint32_t w[4], int32_t &v1, int32_t &v2) {
+    v1 = 0;
+    v2 = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int wt = (4 * q) | ((4 * q + 1) << 8) | ((4 * q + 2) << 16) | ((4 * q + 3) << 24);
+        v1 = __builtin_amdgcn_sdot4((int)w[q], 0x01010101, v1, false);
+        v2 = __builtin_amdgcn_sdot4((int)w[q], wt, v2, false);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ T block_reduce_add(T v, T *scratch) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) scratch[wave] = v;
+    __syncthreads();
+    T tot = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); i++) tot += scratch[i];
+    __syncthreads();
+    return tot;
+}
+
+// --------------------------------------------------------------- tile_agg
+__global__ __launch_bounds__(256) void tile_agg_kernel(const uint8_t *__restrict__ src, uint64_t size, uint32_t r,
+                                                       TileAgg *__restrict__ out) {
+    __shared__ uint32_t scratch[4][4];
+    const uint64_t t0 = (uint64_t)blockIdx.x * kScanTile;
+    uint32_t a1 = 0, a2 = 0, r1 = 0, r2 = 0;
+#pragma unroll 2
+    for (uint32_t j = 0; j < kScanTile / (256 * 16); j++) {
+        const uint32_t loc = 16u * (256u * j + threadIdx.x);
+        uint32_t w[4];
+        load_vec(src, size, t0 + loc, w);
+        int32_t v1, v2;
+        vec_sums(w, v1, v2);
+        a1 += (uint32_t)v1;
+        a2 += (uint32_t)v2 + loc * (uint32_t)v1;
+        if (loc + 16 <= r) {
+            r1 += (uint32_t)v1;
+            r2 += (uint32_t)v2 + loc * (uint32_t)v1;
+        } else if (loc < r) {  // the vector holding byte r: keep bytes < r only
+            const uint32_t keep = r - loc;  // 1..15
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const uint32_t k = 4 * q + b;
+                    if (k < keep) {
+                        const int32_t x = sx8(w[q], b);
+                        r1 += (uint32_t)x;
+                        r2 += (loc + k) * (uint32_t)x;
+                    }
+                }
+        }
+    }
+    uint32_t (*s)[4] = scratch;
+    a1 = block_reduce_add(a1, &s[0][0]);
+    a2 = block_reduce_add(a2, &s[1][0]);
+    r1 = block_reduce_add(r1, &s[2][0]);
+    r2 = block_reduce_add(r2, &s[3][0]);
+    if (threadIdx.x == 0) out[blockIdx.x] = TileAgg{a1, a2, r1, r2};
+}
+
+// --------------------------------------------------------------- tile_scan
+// One workgroup: pre[t] = (P, Q) at the start of tile t (global byte index in
+// Q), pre[ntiles] = totals.  Tile t contributes (a1, a2 + t*T*a1).
+__global__ __launch_bounds__(1024) void tile_scan_kernel(const TileAgg *__restrict__ agg, uint32_t ntiles,
+                                                         TilePrefix *__restrict__ pre) {
+    __shared__ uint32_t sp[1024], sq[1024];
+    const uint32_t per = (ntiles + 1023) / 1024;
+    const uint32_t b = threadIdx.x * per, e = min(b + per, ntiles);
+    uint32_t p = 0, q = 0;
+    for (uint32_t t = b; t < e; t++) {
+        p += agg[t].a1;
+        q += agg[t].a2 + t * kScanTile * agg[t].a1;
+    }
+    sp[threadIdx.x] = p;
+    sq[threadIdx.x] = q;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
+        uint32_t vp = 0, vq = 0;
+        if (threadIdx.x >= d) { vp = sp[threadIdx.x - d]; vq = sq[threadIdx.x - d]; }
+        __syncthreads();
+        sp[threadIdx.x] += vp;
+        sq[threadIdx.x] += vq;
+        __syncthreads();
+    }
+    p = threadIdx.x ? sp[threadIdx.x - 1] : 0;
+    q = threadIdx.x ? sq[threadIdx.x - 1] : 0;
+    for (uint32_t t = b; t < e; t++) {
+        pre[t] = TilePrefix{p, q};
+        p += agg[t].a1;
+        q += agg[t].a2 + t * kScanTile * agg[t].a1;
+    }
+    if (threadIdx.x == 1023) pre[ntiles] = TilePrefix{sp[1023], sq[1023]};
+}
+
+// --------------------------------------------------------------- roll
+__device__ __forceinline__ uint32_t filter_index(uint32_t sum) { return filter_index_host(sum); }
+
+// Inclusive scan of v over the 1024-thread workgroup (wave scans + LDS).
+__device__ __forceinline__ uint32_t wg_inclusive_scan(uint32_t v, uint32_t *wsum) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    if (lane == 63) wsum[wave] = v;
+    __syncthreads();
+    uint32_t add = 0;
+    for (int i = 0; i < wave; i++) add += wsum[i];
+    __syncthreads();
+    return v + add;
+}
+
+__global__ __launch_bounds__(kRollThreads) void roll_kernel(
+    const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
+    uint32_t tile_hi, const TileAgg *__restrict__ agg, const TilePrefix *__restrict__ pre, uint32_t ntiles,
+    const uint32_t *__restrict__ bitmap_g, const uint64_t *__restrict__ table, uint32_t table_bits,
+    uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count) {
+    __shared__ uint32_t bitmap[kFilterBits / 32];
+    __shared__ uint32_t wsum[4][kRollThreads / 64];
+    for (uint32_t i = threadIdx.x; i < kFilterBits / 32; i += kRollThreads) bitmap[i] = bitmap_g[i];
+    __syncthreads();
+    const uint32_t Bt = B / kScanTile, Br = B % kScanTile;
+    const TilePrefix tot = pre[ntiles];
+    const uint32_t need_rem_flag = (rem != 0 && rem != B) ? 4u : 2u;
+
+    for (uint32_t t = tile_lo + blockIdx.x; t < tile_hi; t += gridDim.x) {
+        const uint64_t q0 = (uint64_t)t * kScanTile;
+        if (q0 >= end) break;  // uniform
+        const uint64_t qt = q0 + (uint64_t)threadIdx.x * kRollPerThread;
+        // own bytes [qt, qt+32) and shifted bytes [qt+B, qt+B+32)
+        uint32_t O[8], S[8];
+        load_vec(src, size, qt, O);
+        load_vec(src, size, qt + 16, O + 4);
+        {
+            const uint64_t ps = qt + B;
+            const uint32_t sh = (uint32_t)(ps & 3u);  // uniform across the workgroup
+            const uint64_t pa = ps - sh;
+            uint32_t A[12];
+            load_vec(src, size, pa, A);
+            load_vec(src, size, pa + 16, A + 4);
+            load_vec(src, size, pa + 32, A + 8);
+#pragma unroll
+            for (int k = 0; k < 8; k++) S[k] = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sh);
+        }
+        int32_t o1, o2, s1, s2, v1, v2;
+        vec_sums(O, o1, o2);
+        vec_sums(O + 4, v1, v2);
+        o2 += v2 + 16 * v1;
+        o1 += v1;
+        vec_sums(S, s1, s2);
+        vec_sums(S + 4, v1, v2);
+        s2 += v2 + 16 * v1;
+        s1 += v1;
+        const uint32_t lo = threadIdx.x * kRollPerThread;  // local offset of qt in the tile
+        // inclusive scans -> exclusive prefixes within the tile
+        const uint32_t i_o1 = wg_inclusive_scan((uint32_t)o1, wsum[0]);
+        const uint32_t i_o2 = wg_inclusive_scan((uint32_t)o2 + lo * (uint32_t)o1, wsum[1]);
+        const uint32_t i_s1 = wg_inclusive_scan((uint32_t)s1, wsum[2]);
+        const uint32_t i_s2 = wg_inclusive_scan((uint32_t)s2 + lo * (uint32_t)s1, wsum[3]);
+        const uint32_t e_o1 = i_o1 - (uint32_t)o1, e_o2 = i_o2 - ((uint32_t)o2 + lo * (uint32_t)o1);
+        const uint32_t e_s1 = i_s1 - (uint32_t)s1, e_s2 = i_s2 - ((uint32_t)s2 + lo * (uint32_t)s1);
+        if (qt >= end) continue;
+        // P, Q at qt
+        const uint32_t Pq = pre[t].p + e_o1;
+        const uint32_t Qq = pre[t].q + e_o2 + (uint32_t)q0 * e_o1;
+        uint32_t W1, W2, k;
+        if (qt + B <= size) {
+            // P, Q at qt + B via the tile holding q0 + B
+            const uint32_t u = t + Bt;
+            const uint32_t ur1 = u < ntiles ? agg[u].r1 : 0u, ur2 = u < ntiles ? agg[u].r2 : 0u;
+            const uint32_t Pb = pre[u].p + ur1;                                   // P[q0 + B]
+            const uint32_t Qb = pre[u].q + ur2 + (uint32_t)((uint64_t)u * kScanTile) * ur1;  // Q[q0 + B]
+            const uint32_t Pe = Pb + e_s1;
+            const uint32_t Qe = Qb + e_s2 + (uint32_t)(q0 + B) * e_s1;
+            W1 = Pe - Pq;
+            W2 = (uint32_t)(qt + B) * W1 - (Qe - Qq);
+            k = B;
+        } else {
+            W1 = tot.p - Pq;
+            W2 = (uint32_t)size * W1 - (tot.q - Qq);
+            k = (uint32_t)(size - qt);
+        }
+        (void)Br;
+#pragma unroll
+        for (int j = 0; j < (int)kRollPerThread; j++) {
+            const uint64_t q = qt + j;
+            if (q < end) {
+                const uint32_t sum = (W1 & 0xffffu) | (W2 << 16);  // match.go:106
+                const uint32_t fi = filter_index(sum);
+                if ((bitmap[fi >> 5] >> (fi & 31)) & 1u) {
+                    // exact probe: flags bit1 = a block of length B, bit2 = the remainder block
+                    uint32_t hsh = (sum * 0x9E3779B1u) >> (32 - table_bits);
+                    const uint32_t mask = (1u << table_bits) - 1;
+                    for (;;) {
+                        const uint64_t slot = table[hsh];
+                        const uint32_t fl = (uint32_t)slot;
+                        if (fl == 0) break;
+                        if ((uint32_t)(slot >> 32) == sum) {
+                            const uint32_t need = (k == B) ? 2u : ((k == rem) ? need_rem_flag : 0u);
+                            if (fl & need) {
+                                const uint32_t at = atomicAdd(count, 1u);
+                                if (at < cap) cand[at] = q;
+                            }
+                            break;
+                        }
+                        hsh = (hsh + 1) & mask;
+                    }
+                }
+            }
+            // rolling update, match.go:171-196
+            const int32_t xo = sx8(O[j >> 2], j & 3);
+            const bool more = q + k < size;
+            const int32_t xi = more ? sx8(S[j >> 2], j & 3) : 0;
+            W1 = W1 - (uint32_t)xo + (uint32_t)xi;
+            W2 = W2 - k * (uint32_t)xo + (more ? W1 : 0u);
+            if (!more) k--;
+        }
+    }
+}
+
+hipError_t launch_tile_agg(const uint8_t *src, uint64_t size, uint32_t r, TileAgg *out, uint32_t ntiles,
+                           hipStream_t stream) {
+    if (ntiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(tile_agg_kernel, dim3(ntiles), dim3(256), 0, stream, src, size, r, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_scan(const TileAgg *agg, uint32_t ntiles, TilePrefix *pre, hipStream_t stream) {
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, stream, agg, ntiles, pre);
+    return hipGetLastError();
+}
+
+hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
+                       uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
+                       const uint32_t *bitmap, const uint64_t *table, uint32_t table_bits, uint64_t *cand,
+                       uint32_t cap, uint32_t *count, uint32_t grid, hipStream_t stream) {
+    if (tile_hi <= tile_lo) return hipSuccess;
+    const uint32_t g = min(grid, tile_hi - tile_lo);
+    hipLaunchKernelGGL(roll_kernel, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, tile_hi,
+                       agg, pre, ntiles, bitmap, table, table_bits, cand, cap, count);
+    return hipGetLastError();
+}
+
+}  // namespace rsg

@@ -1,0 +1,112 @@
+"""GPU parity of the sender search (match.go:21-230) against the golden
+fixtures and the C oracle.  Everything goes through the C-ABI."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import cases
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import rsync_amd
+    e = rsync_amd.Engine(0)
+    yield e
+    e.close()
+
+
+def basis_sums(basis, blen, seed):
+    head = orc.sum_head(basis.size, blen)
+    if head[0]:
+        s1, s2 = orc.parse_records(orc.block_sums(basis, blen, seed))
+    else:
+        s1, s2 = np.zeros(0, np.uint32), np.zeros((0, 16), np.uint8)
+    return head, s1, s2
+
+
+@pytest.mark.parametrize("name", sorted(cases.match_cases()))
+def test_golden_cases(eng, name):
+    import rsync_amd
+    g = json.load(open(os.path.join(GOLD, "match_cases.json")))[name]
+    src, basis, blen, seed = cases.match_cases()[name]
+    head, s1, s2 = basis_sums(basis, blen, seed)
+    got = eng.hash_search(src, head, s1, s2, orc.stable_targets(s1), seed)
+    assert [list(m) for m in got] == g["matches"]
+    tokens = rsync_amd.encode_tokens(src, head, got)
+    assert len(tokens) == g["tokens_len"]
+    assert hashlib.sha256(tokens).hexdigest() == g["tokens_sha256"]
+
+
+@pytest.mark.parametrize("seed_case", range(8))
+def test_random_vs_oracle(eng, seed_case):
+    rng = np.random.default_rng(100 + seed_case)
+    n = int(rng.integers(1, 300_000))
+    basis = cases.splitmix64_bytes(700 + seed_case, n)
+    src = cases.mutate(basis, 800 + seed_case, float(rng.uniform(0, 0.6)), 1, 3000,
+                       n_ins=int(rng.integers(0, 5)), n_del=int(rng.integers(0, 5)))
+    blen = int(rng.choice([0, 1, 7, 64, 333, 700, 1024, 4096, 40000]))
+    seed = int(rng.integers(-2**31, 2**31))
+    head, s1, s2 = basis_sums(basis, blen, seed)
+    s2len = int(rng.choice([16, 16, 2, 0]))
+    head = (head[0], head[1], s2len, head[3])
+    tg = orc.stable_targets(s1)
+    want, _, _ = orc.hash_search(src, head, s1, s2, tg, seed)
+    assert eng.hash_search(src, head, s1, s2, tg, seed) == want
+
+
+def test_device_unaligned_source(eng):
+    src, basis, blen, seed = cases.match_cases()["shifted_700"]
+    head, s1, s2 = basis_sums(basis, blen, seed)
+    tg = orc.stable_targets(s1)
+    want, _, _ = orc.hash_search(src, head, s1, s2, tg, seed)
+    buf = eng.alloc(src.size + 3)
+    buf.upload(np.concatenate([np.zeros(3, np.uint8), src]))
+
+    class View:  # the same buffer seen 3 bytes in: a misaligned device pointer
+        ptr = buf.ptr + 3
+    assert eng.hash_search_device(View, src.size, head, s1, s2, tg, seed) == want
+
+
+def test_periodic_dense(eng):
+    """Every offset is a weak and strong hit (the dense path of the walk)."""
+    src = np.full(3 << 20, 0xBB, np.uint8)
+    basis = np.full(1 << 20, 0xBB, np.uint8)
+    head, s1, s2 = basis_sums(basis, 0, 7)
+    tg = orc.stable_targets(s1)
+    want, _, _ = orc.hash_search(src, head, s1, s2, tg, 7)
+    assert eng.hash_search(src, head, s1, s2, tg, 7) == want
+
+
+def test_cfg3_shape_vs_oracle(eng):
+    """cfg3 recipe at 64 MiB: a ~50%-modified basis with
+    long runs plus shifts, reference block sizing (B = sqrt(len))."""
+    basis = cases.splitmix64_bytes(3, 64 << 20)
+    head, s1, s2 = basis_sums(basis, 0, cases.SEED)
+    src = cases.mutate(basis, 33, 0.5, 1, 2 * head[1], n_ins=5, n_del=5)
+    tg = orc.stable_targets(s1)
+    want, _, _ = orc.hash_search(src, head, s1, s2, tg, cases.SEED)
+    got = eng.hash_search(src, head, s1, s2, tg, cases.SEED)
+    assert len(want) > 100
+    assert got == want
+
+
+def test_identical_large_property(eng):
+    """1 GiB source identical to its basis (B = 32768): every block matches at
+    its own offset, in order (size-independent property at full cfg3 file size)."""
+    size = 1 << 30
+    dev = eng.alloc(size)
+    eng.fill_splitmix64(dev, size, 11)
+    recs, total = eng.block_sums_device(dev, [(0, size, 0)], cases.SEED)
+    rec = recs.download(total * 20).tobytes()
+    s1, s2 = orc.parse_records(rec)
+    head = orc.sum_head(size, 0)
+    assert head[0] == total == 32768
+    got = eng.hash_search_device(dev, size, head, s1, s2, orc.stable_targets(s1), cases.SEED)
+    assert got == [(i * head[1], i) for i in range(total)]
