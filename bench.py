@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--ab", action="store_true", help="A/B the block-sum kernel variants (interleaved rounds)")
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3"],
+                    help="cfg2 = receiver block sums (the metric); cfg3 = sender match, reported separately")
+    ap.add_argument("--cfg3-files", type=int, default=10)
     return ap.parse_args()
 
 
@@ -65,6 +68,8 @@ def main():
         dist.init_process_group("gloo")  # control plane only; data moves over RCCL
     torch.cuda.set_device(local)
     import rsync_amd
+    if args.workload == "cfg3":
+        return bench_sender(args, rank, world, local)
 
     eng = rsync_amd.Engine(local)
     stream = torch.cuda.Stream(device=local)
@@ -239,6 +244,90 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def make_cfg3_file(eng, basis, src, size, seed, B, rng):
+    """Source = the basis with random runs (1 B .. 2B long) overwritten until
+    ~50% of the bytes differ, plus a few insertions/deletions so matches fall at
+    offsets that are not multiples of B.  Built on the
+    device with splitmix64 fills and device copies; returns the source length."""
+    import rsync_amd
+    from rsync_amd import _lib
+    eng.fill_splitmix64(basis, size, seed)
+    # shifts: copy basis pieces with small gaps/overlaps into src
+    cuts = sorted(rng.choice(np.arange(1, size - 1), 8, replace=False).tolist())
+    pos_src, prev = 0, 0
+    for i, c in enumerate(cuts + [size]):
+        n = max(0, c - prev)
+        _lib.check(_lib.lib.rsg_memcpy_d2d(eng.ctx, rsync_amd.engine.ctypes.c_void_p(src.ptr + pos_src),
+                                            rsync_amd.engine.ctypes.c_void_p(basis.ptr + prev), n), eng.ctx)
+        pos_src += n
+        if i % 2 == 0 and c < size:  # insertion of random bytes
+            k = int(rng.integers(1, 64))
+            eng.fill_splitmix64(src, k, seed * 7919 + i, offset=pos_src)
+            pos_src += k
+        elif c < size:  # deletion
+            prev = c + int(rng.integers(1, 64))
+            continue
+        prev = c
+    total = pos_src
+    touched, run_seed = 0, 1
+    while touched < total // 2:
+        ln = int(rng.integers(1, 2 * B))
+        at = int(rng.integers(0, total - ln))
+        eng.fill_splitmix64(src, ln, seed * 104729 + run_seed, offset=at)
+        run_seed += 1
+        touched += ln
+    return total
+
+
+def bench_sender(args, rank, world, local):
+    """cfg3: sender byte-rolling match, 10 x 1 GiB sources vs 50%-modified bases
+    on one GPU (the files shard across GPUs with no exchange).  Metric: source
+    GiB scanned per second, device-resident, end to end through the C-ABI."""
+    import torch
+    import rsync_amd
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    eng = rsync_amd.Engine(local)
+    size = 1 << 30
+    rng = np.random.default_rng(3 + rank)
+    basis = eng.alloc(size)
+    srcs, metas = [], []
+    for f in range(args.cfg3_files):
+        src = eng.alloc(size + 4096)
+        seed = 1000 * rank + f + 3
+        n = make_cfg3_file(eng, basis, src, size, seed, 32768, rng)
+        recs, total = eng.block_sums_device(basis, [(0, size, 0)], SEED)
+        rec = recs.download(total * 20).reshape(-1, 20)
+        recs.free()
+        s1 = rec[:, :4].copy().view("<u4").reshape(-1)
+        s2 = rec[:, 4:].copy()
+        tags = ((s1 & 0xFFFF) + (s1 >> 16)) & 0xFFFF
+        tg = np.argsort(tags, kind="stable").astype(np.int32)
+        head = rsync_amd.sum_sizes_sqroot(size)
+        srcs.append(src)
+        metas.append((n, head, s1, s2, tg))
+    eng.synchronize()
+    # warm up once per file, then time K passes over the file set
+    for (n, head, s1, s2, tg), src in zip(metas, srcs):
+        eng.hash_search_device(src, n, head, s1, s2, tg, SEED)
+    steps = max(1, min(args.steps, 5))
+    t0 = time.perf_counter()
+    nm = 0
+    for _ in range(steps):
+        for (n, head, s1, s2, tg), src in zip(metas, srcs):
+            nm += len(eng.hash_search_device(src, n, head, s1, s2, tg, SEED))
+    dt = time.perf_counter() - t0
+    scanned = sum(m[0] for m in metas) * steps
+    if rank == 0:
+        print(json.dumps({"metric": "GiB/s source scanned (sender rolling match), device-resident",
+                          "value": round(scanned / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
+                          "steps": steps, "higher_is_better": True, "dtype": "u32",
+                          "data": "synthetic (splitmix64 bases; sources 50% overwritten + shifts)",
+                          "config": {"workload": "cfg3: 10 x 1 GiB sources vs 50%-modified bases, B=32768",
+                                     "files": args.cfg3_files, "matches_per_pass": nm // steps},
+                          "ms_per_file": round(dt * 1e3 / (steps * len(metas)), 3)}), flush=True)
+    eng.close()
 
 
 if __name__ == "__main__":

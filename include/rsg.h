@@ -108,6 +108,7 @@ rsg_status rsg_alloc_device(rsg_ctx *ctx, uint64_t bytes, void **out);
 rsg_status rsg_free_device(rsg_ctx *ctx, void *p);
 rsg_status rsg_memcpy_h2d(rsg_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 rsg_status rsg_memcpy_d2h(rsg_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+rsg_status rsg_memcpy_d2d(rsg_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 rsg_status rsg_synchronize(rsg_ctx *ctx, void *stream);
 /* Synthetic data: dst[0..n) = splitmix64(seed) little-endian byte stream
  * (SURVEY.md appendix), generated on the device. */

@@ -69,6 +69,7 @@ _PROTOS = {
     "rsg_free_device": (_st, [_vp, _vp]),
     "rsg_memcpy_h2d": (_st, [_vp, _vp, _vp, _u64]),
     "rsg_memcpy_d2h": (_st, [_vp, _vp, _vp, _u64]),
+    "rsg_memcpy_d2d": (_st, [_vp, _vp, _vp, _u64]),
     "rsg_synchronize": (_st, [_vp, _vp]),
     "rsg_fill_splitmix64": (_st, [_vp, _vp, _u64, _u64, _vp]),
     "rsg_plan_block_sums": (_st, [ctypes.POINTER(File), _u64, ctypes.POINTER(SumHead),

@@ -271,13 +271,28 @@ rsg_status rsg_free_device(rsg_ctx *ctx, void *p) {
 
 rsg_status rsg_memcpy_h2d(rsg_ctx *ctx, void *dst, const void *src, uint64_t bytes) {
     RSG_ENTER(ctx);
-    if (bytes) RSG_HIP(ctx, hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    if (bytes) {  // on the context's stream: ordered after its kernels (it is non-blocking)
+        RSG_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+        RSG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
     return RSG_OK;
 }
 
 rsg_status rsg_memcpy_d2h(rsg_ctx *ctx, void *dst, const void *src, uint64_t bytes) {
     RSG_ENTER(ctx);
-    if (bytes) RSG_HIP(ctx, hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    if (bytes) {  // on the context's stream: ordered after its kernels (it is non-blocking)
+        RSG_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        RSG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return RSG_OK;
+}
+
+rsg_status rsg_memcpy_d2d(rsg_ctx *ctx, void *dst, const void *src, uint64_t bytes) {
+    RSG_ENTER(ctx);
+    if (bytes) {  // on the context's stream: ordered after its kernels (it is non-blocking)
+        RSG_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+        RSG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
     return RSG_OK;
 }
 

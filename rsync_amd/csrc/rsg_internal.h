@@ -45,12 +45,18 @@ __host__ __device__ inline uint32_t filter_index_host(uint32_t sum) {
     return ((sum & 0xffffu) ^ ((sum >> 16) << 3)) & (kFilterBits - 1);
 }
 
+// Exact table of basis weak sums: buckets of kBucketWays u64 entries
+// {sum1 << 32 | flags}; a sum lives in bucket hash1 or hash2.
+constexpr uint32_t kBucketWays = 4;
+__host__ __device__ inline uint32_t bucket_hash1(uint32_t s) { return (s * 0x9E3779B1u) >> 7; }
+__host__ __device__ inline uint32_t bucket_hash2(uint32_t s) { return ((s ^ (s >> 15)) * 0x85EBCA77u) >> 9; }
+
 hipError_t launch_tile_agg(const uint8_t *src, uint64_t size, uint32_t r, TileAgg *out, uint32_t ntiles,
                            hipStream_t stream);
 hipError_t launch_tile_scan(const TileAgg *agg, uint32_t ntiles, TilePrefix *pre, hipStream_t stream);
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
-                       const uint32_t *bitmap, const uint64_t *table, uint32_t table_bits, uint64_t *cand,
+                       const uint32_t *bitmap, const uint64_t *table, uint32_t bmask, uint64_t *cand,
                        uint32_t cap, uint32_t *count, uint32_t grid, hipStream_t stream);
 
 hipError_t launch_fill_splitmix64(uint8_t *dst, uint64_t n, uint64_t seed, hipStream_t stream);

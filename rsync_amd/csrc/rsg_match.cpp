@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <climits>
 #include <unordered_map>
 #include <vector>
 
@@ -42,8 +43,10 @@ struct Search {
     const uint8_t *sum2;
     int32_t seed;
     int64_t end;  // visited offsets are q < end (end >= 1: offset 0 is always visited)
-    std::unordered_map<uint32_t, std::vector<int32_t>> groups;  // sum1 -> blocks in targets order
-    std::unordered_map<uint64_t, int32_t> verified;             // offset -> block index or -1
+    // (sum1, block) in targets order, stably sorted by sum1: each sum's blocks
+    // are one run, in targets order (match.go:108 walks targets in that order)
+    std::vector<std::pair<uint32_t, int32_t>> groups;
+    std::unordered_map<uint64_t, int32_t> verified;  // offset -> block index or -1
     std::vector<rsg_match> out;
 
     int64_t len_of(int32_t i) const {
@@ -87,15 +90,14 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &qs) {
         uint32_t w;
         memcpy(&w, r, 4);
         int32_t res = -1;
-        auto it = S.groups.find(w);
-        if (it != S.groups.end()) {
-            const int64_t k = (int64_t)wins[i].len;
-            for (int32_t b : it->second) {  // targets order, match.go:108
-                if (S.len_of(b) != k) continue;  // :118
-                if (memcmp(r + 4, S.sum2 + 16 * (int64_t)b, (size_t)S.head.s2len) != 0) continue;  // :133
-                res = b;
-                break;
-            }
+        auto it = std::lower_bound(S.groups.begin(), S.groups.end(), std::make_pair(w, INT32_MIN));
+        const int64_t k = (int64_t)wins[i].len;
+        for (; it != S.groups.end() && it->first == w; ++it) {  // targets order, match.go:108
+            const int32_t b = it->second;
+            if (S.len_of(b) != k) continue;                                                        // :118
+            if (memcmp(r + 4, S.sum2 + 16 * (int64_t)b, (size_t)S.head.s2len) != 0) continue;  // :133
+            res = b;
+            break;
         }
         S.verified[qs[i]] = res;
     }
@@ -174,28 +176,40 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
     S.end = std::max<int64_t>((int64_t)size + 1 - last_len, 1);  // match.go:70 (offset 0 always visited)
 
     // Basis sums grouped by Sum1 in targets order; device filter = bitmap of
-    // every Sum1 + open-addressing table {Sum1, flags: bit1 = a block of
+    // every Sum1 + a 2-choice bucketed table {Sum1, flags: bit1 = a block of
     // length B, bit2 = the remainder block}.
-    std::unordered_map<uint32_t, uint32_t> flags;
-    S.groups.reserve((size_t)count * 2);
-    for (int32_t k = 0; k < count; k++) {
-        const int32_t i = targets[k];
-        S.groups[sum1[i]].push_back(i);
-        uint32_t &f = flags[sum1[i]];
-        f |= 1u;
-        f |= (S.len_of(i) == B) ? 2u : 4u;
+    S.groups.resize((size_t)count);
+    for (int32_t k = 0; k < count; k++) S.groups[(size_t)k] = {sum1[targets[k]], targets[k]};
+    std::stable_sort(S.groups.begin(), S.groups.end(),
+                     [](const std::pair<uint32_t, int32_t> &a, const std::pair<uint32_t, int32_t> &b) {
+                         return a.first < b.first;
+                     });
+    std::vector<std::pair<uint32_t, uint32_t>> keys;  // distinct sum1 -> flags
+    for (size_t i = 0; i < S.groups.size(); i++) {
+        const uint32_t f = 1u | ((S.len_of(S.groups[i].second) == B) ? 2u : 4u);
+        if (!keys.empty() && keys.back().first == S.groups[i].first) keys.back().second |= f;
+        else keys.push_back({S.groups[i].first, f});
     }
-    uint32_t tbits = 10;
-    while ((1ull << tbits) < 2ull * flags.size()) tbits++;
-    std::vector<uint64_t> table(1ull << tbits, 0);
     std::vector<uint32_t> bitmap(rsg::kFilterBits / 32, 0);
-    for (auto &kv : flags) {
-        const uint32_t key = kv.first;
-        uint32_t h = (key * 0x9E3779B1u) >> (32 - tbits);
-        while ((uint32_t)table[h] != 0) h = (h + 1) & ((1u << tbits) - 1);
-        table[h] = ((uint64_t)key << 32) | kv.second;
-        const uint32_t fi = rsg::filter_index_host(key);
+    for (auto &kv : keys) {
+        const uint32_t fi = rsg::filter_index_host(kv.first);
         bitmap[fi >> 5] |= 1u << (fi & 31);
+    }
+    uint32_t nb = 16;
+    while (nb < keys.size() / 2) nb <<= 1;
+    std::vector<uint64_t> table;
+    for (;;) {
+        table.assign((size_t)nb * rsg::kBucketWays, 0);
+        std::vector<uint8_t> fill(nb, 0);
+        bool ok = true;
+        for (auto &kv : keys) {
+            const uint32_t h1 = rsg::bucket_hash1(kv.first) & (nb - 1), h2 = rsg::bucket_hash2(kv.first) & (nb - 1);
+            const uint32_t h = fill[h2] < fill[h1] ? h2 : h1;
+            if (fill[h] == rsg::kBucketWays) { ok = false; break; }
+            table[(size_t)h * rsg::kBucketWays + fill[h]++] = ((uint64_t)kv.first << 32) | kv.second;
+        }
+        if (ok) break;
+        nb <<= 1;
     }
     const uint64_t ntiles64 = (size + kScanTile - 1) / kScanTile;
     if (ntiles64 >= 0xFFFFFFF0ull) return fail(ctx, RSG_ERR_INVALID, "source too large");
@@ -203,6 +217,7 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
     rsg_status s;
     if ((s = ensure_dev(ctx, ctx->d_filter, bitmap.size() * 4)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, ctx->d_table, table.size() * 8)) != RSG_OK) return s;
+    const uint32_t bmask = nb - 1;
     if ((s = ensure_dev(ctx, ctx->d_agg, (uint64_t)ntiles * sizeof(TileAgg) + 64)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, ctx->d_prefix, ((uint64_t)ntiles + 1) * sizeof(TilePrefix) + 64)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, ctx->d_list, (uint64_t)kCandCap * 8)) != RSG_OK) return s;
@@ -229,7 +244,7 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
         RSG_HIP(ctx, hipMemsetAsync(ctx->d_counts.p, 0, 4, S.st));
         RSG_HIP(ctx, rsg::launch_roll(d_src, size, (uint32_t)B, (uint32_t)head->rem, (uint64_t)S.end, lo, hi,
                                       (const TileAgg *)ctx->d_agg.p, (const TilePrefix *)ctx->d_prefix.p, ntiles,
-                                      (const uint32_t *)ctx->d_filter.p, (const uint64_t *)ctx->d_table.p, tbits,
+                                      (const uint32_t *)ctx->d_filter.p, (const uint64_t *)ctx->d_table.p, bmask,
                                       (uint64_t *)ctx->d_list.p, kCandCap, (uint32_t *)ctx->d_counts.p,
                                       (uint32_t)dev_cus, S.st));
         uint32_t n = 0;
@@ -241,7 +256,10 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
             continue;
         }
         C.resize(n);
-        if (n) RSG_HIP(ctx, hipMemcpy(C.data(), ctx->d_list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost));
+        if (n) {
+            RSG_HIP(ctx, hipMemcpyAsync(C.data(), ctx->d_list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, S.st));
+            RSG_HIP(ctx, hipStreamSynchronize(S.st));
+        }
         std::sort(C.begin(), C.end());
         if ((s = walk(S, C, pos)) != RSG_OK) return s;
         lo = hi;

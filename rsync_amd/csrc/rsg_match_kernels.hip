@@ -155,39 +155,63 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(const TileAgg *__restri
 // --------------------------------------------------------------- roll
 __device__ __forceinline__ uint32_t filter_index(uint32_t sum) { return filter_index_host(sum); }
 
-// Inclusive scan of v over the 1024-thread workgroup (wave scans + LDS).
-__device__ __forceinline__ uint32_t wg_inclusive_scan(uint32_t v, uint32_t *wsum) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// Exact membership of a weak sum in the basis: 2-choice table of buckets of
+// kBucketWays entries {sum1 << 32 | flags} (flags: bit0 used, bit1 = a block
+// of length B has this sum, bit2 = the remainder block has it).  Two 32-byte
+// bucket loads, no probe chains.
+__device__ __forceinline__ uint32_t table_flags(const uint64_t *__restrict__ table, uint32_t bmask, uint32_t sum) {
+    const uint32_t h1 = bucket_hash1(sum) & bmask, h2 = bucket_hash2(sum) & bmask;
+    const uint64_t *b1 = table + (uint64_t)h1 * kBucketWays;
+    const uint64_t *b2 = table + (uint64_t)h2 * kBucketWays;
+    uint64_t e[2 * kBucketWays];
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(v, d, 64);
-        if (lane >= d) v += o;
-    }
-    if (lane == 63) wsum[wave] = v;
-    __syncthreads();
-    uint32_t add = 0;
-    for (int i = 0; i < wave; i++) add += wsum[i];
-    __syncthreads();
-    return v + add;
+    for (uint32_t i = 0; i < kBucketWays; i++) { e[i] = b1[i]; e[kBucketWays + i] = b2[i]; }
+    uint32_t fl = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 2 * kBucketWays; i++)
+        if ((uint32_t)(e[i] >> 32) == sum && (uint32_t)e[i] != 0) fl |= (uint32_t)e[i];
+    return fl;
 }
+
+constexpr uint32_t kQueueCap = 192;  // bitmap hits parked per wave before the exact probes
 
 __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
     uint32_t tile_hi, const TileAgg *__restrict__ agg, const TilePrefix *__restrict__ pre, uint32_t ntiles,
-    const uint32_t *__restrict__ bitmap_g, const uint64_t *__restrict__ table, uint32_t table_bits,
+    const uint32_t *__restrict__ bitmap_g, const uint64_t *__restrict__ table, uint32_t bmask,
     uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count) {
-    __shared__ uint32_t bitmap[kFilterBits / 32];
-    __shared__ uint32_t wsum[4][kRollThreads / 64];
+    constexpr uint32_t kWaves = kRollThreads / 64;
+    __shared__ uint32_t bitmap[kFilterBits / 32];       // 64 KiB
+    __shared__ uint2 queue[kWaves][kQueueCap];           // (tile-local offset, sum)
+    __shared__ uint32_t wsum[2][kWaves][4];              // scan partials, double-buffered per tile
     for (uint32_t i = threadIdx.x; i < kFilterBits / 32; i += kRollThreads) bitmap[i] = bitmap_g[i];
     __syncthreads();
-    const uint32_t Bt = B / kScanTile, Br = B % kScanTile;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t Bt = B / kScanTile;
     const TilePrefix tot = pre[ntiles];
-    const uint32_t need_rem_flag = (rem != 0 && rem != B) ? 4u : 2u;
+    const uint32_t rem_flag = (rem != 0 && rem != B) ? 4u : 2u;
+    uint32_t parity = 0;
+
+    // exact probes of this wave's parked hits; true candidates go to `cand`
+    auto drain = [&](uint64_t q0, uint32_t n) {
+        for (uint32_t i = lane; i < n; i += 64) {
+            const uint2 e = queue[wave][i];
+            const uint64_t q = q0 + e.x;
+            const uint32_t k = (uint32_t)min<uint64_t>((uint64_t)B, size - q);
+            const uint32_t need = (k == B) ? 2u : ((k == rem) ? rem_flag : 0u);
+            if (table_flags(table, bmask, e.y) & need) {
+                const uint32_t at = atomicAdd(count, 1u);
+                if (at < cap) cand[at] = q;
+            }
+        }
+    };
 
     for (uint32_t t = tile_lo + blockIdx.x; t < tile_hi; t += gridDim.x) {
         const uint64_t q0 = (uint64_t)t * kScanTile;
         if (q0 >= end) break;  // uniform
-        const uint64_t qt = q0 + (uint64_t)threadIdx.x * kRollPerThread;
+        const uint32_t lo = threadIdx.x * kRollPerThread;  // local offset of this lane's first offset
+        const uint64_t qt = q0 + lo;
         // own bytes [qt, qt+32) and shifted bytes [qt+B, qt+B+32)
         uint32_t O[8], S[8];
         load_vec(src, size, qt, O);
@@ -212,61 +236,73 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         vec_sums(S + 4, v1, v2);
         s2 += v2 + 16 * v1;
         s1 += v1;
-        const uint32_t lo = threadIdx.x * kRollPerThread;  // local offset of qt in the tile
-        // inclusive scans -> exclusive prefixes within the tile
-        const uint32_t i_o1 = wg_inclusive_scan((uint32_t)o1, wsum[0]);
-        const uint32_t i_o2 = wg_inclusive_scan((uint32_t)o2 + lo * (uint32_t)o1, wsum[1]);
-        const uint32_t i_s1 = wg_inclusive_scan((uint32_t)s1, wsum[2]);
-        const uint32_t i_s2 = wg_inclusive_scan((uint32_t)s2 + lo * (uint32_t)s1, wsum[3]);
-        const uint32_t e_o1 = i_o1 - (uint32_t)o1, e_o2 = i_o2 - ((uint32_t)o2 + lo * (uint32_t)o1);
-        const uint32_t e_s1 = i_s1 - (uint32_t)s1, e_s2 = i_s2 - ((uint32_t)s2 + lo * (uint32_t)s1);
-        if (qt >= end) continue;
+        // one workgroup scan of four values: prefixes (within the tile) of the
+        // own and shifted byte sums, sum x and sum (local index) * x
+        uint32_t v[4] = {(uint32_t)o1, (uint32_t)o2 + lo * (uint32_t)o1, (uint32_t)s1,
+                         (uint32_t)s2 + lo * (uint32_t)s1};
+        uint32_t incl[4] = {v[0], v[1], v[2], v[3]};
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t o = __shfl_up(incl[c], d, 64);
+                if (lane >= (uint32_t)d) incl[c] += o;
+            }
+        }
+        if (lane == 63) {
+#pragma unroll
+            for (int c = 0; c < 4; c++) wsum[parity][wave][c] = incl[c];
+        }
+        __syncthreads();
+        uint32_t ex[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            uint32_t add = 0;
+            for (uint32_t w = 0; w < wave; w++) add += wsum[parity][w][c];
+            ex[c] = incl[c] - v[c] + add;
+        }
+        parity ^= 1u;
+        // Lanes past `end` stay in the loop (they never hit): drain() spreads the
+        // wave's parked hits over all 64 lanes.
         // P, Q at qt
-        const uint32_t Pq = pre[t].p + e_o1;
-        const uint32_t Qq = pre[t].q + e_o2 + (uint32_t)q0 * e_o1;
+        const uint32_t Pq = pre[t].p + ex[0];
+        const uint32_t Qq = pre[t].q + ex[1] + (uint32_t)q0 * ex[0];
         uint32_t W1, W2, k;
         if (qt + B <= size) {
-            // P, Q at qt + B via the tile holding q0 + B
-            const uint32_t u = t + Bt;
+            const uint32_t u = min(t + Bt, ntiles);  // tile holding q0 + B
             const uint32_t ur1 = u < ntiles ? agg[u].r1 : 0u, ur2 = u < ntiles ? agg[u].r2 : 0u;
-            const uint32_t Pb = pre[u].p + ur1;                                   // P[q0 + B]
+            const uint32_t Pb = pre[u].p + ur1;                                              // P[q0 + B]
             const uint32_t Qb = pre[u].q + ur2 + (uint32_t)((uint64_t)u * kScanTile) * ur1;  // Q[q0 + B]
-            const uint32_t Pe = Pb + e_s1;
-            const uint32_t Qe = Qb + e_s2 + (uint32_t)(q0 + B) * e_s1;
+            const uint32_t Pe = Pb + ex[2];
+            const uint32_t Qe = Qb + ex[3] + (uint32_t)(q0 + B) * ex[2];
             W1 = Pe - Pq;
             W2 = (uint32_t)(qt + B) * W1 - (Qe - Qq);
             k = B;
         } else {
             W1 = tot.p - Pq;
             W2 = (uint32_t)size * W1 - (tot.q - Qq);
-            k = (uint32_t)(size - qt);
+            k = qt < size ? (uint32_t)(size - qt) : 0u;
         }
-        (void)Br;
+        uint32_t nq = 0;  // wave-uniform queue fill
 #pragma unroll
         for (int j = 0; j < (int)kRollPerThread; j++) {
             const uint64_t q = qt + j;
-            if (q < end) {
-                const uint32_t sum = (W1 & 0xffffu) | (W2 << 16);  // match.go:106
-                const uint32_t fi = filter_index(sum);
-                if ((bitmap[fi >> 5] >> (fi & 31)) & 1u) {
-                    // exact probe: flags bit1 = a block of length B, bit2 = the remainder block
-                    uint32_t hsh = (sum * 0x9E3779B1u) >> (32 - table_bits);
-                    const uint32_t mask = (1u << table_bits) - 1;
-                    for (;;) {
-                        const uint64_t slot = table[hsh];
-                        const uint32_t fl = (uint32_t)slot;
-                        if (fl == 0) break;
-                        if ((uint32_t)(slot >> 32) == sum) {
-                            const uint32_t need = (k == B) ? 2u : ((k == rem) ? need_rem_flag : 0u);
-                            if (fl & need) {
-                                const uint32_t at = atomicAdd(count, 1u);
-                                if (at < cap) cand[at] = q;
-                            }
-                            break;
-                        }
-                        hsh = (hsh + 1) & mask;
-                    }
+            const uint32_t sum = (W1 & 0xffffu) | (W2 << 16);  // match.go:106
+            const uint32_t fi = filter_index(sum);
+            const bool hit = q < end && ((bitmap[fi >> 5] >> (fi & 31)) & 1u);
+            const uint64_t bal = __ballot(hit);
+            if (bal) {
+                const uint32_t nb = __popcll(bal);
+                if (nq + nb > kQueueCap) {
+                    drain(q0, nq);
+                    nq = 0;
                 }
+                if (hit) {
+                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    queue[wave][nq + below] = make_uint2(lo + j, sum);
+                }
+                nq += nb;
             }
             // rolling update, match.go:171-196
             const int32_t xo = sx8(O[j >> 2], j & 3);
@@ -276,6 +312,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
             W2 = W2 - k * (uint32_t)xo + (more ? W1 : 0u);
             if (!more) k--;
         }
+        drain(q0, nq);
     }
 }
 
@@ -293,12 +330,12 @@ hipError_t launch_tile_scan(const TileAgg *agg, uint32_t ntiles, TilePrefix *pre
 
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
-                       const uint32_t *bitmap, const uint64_t *table, uint32_t table_bits, uint64_t *cand,
+                       const uint32_t *bitmap, const uint64_t *table, uint32_t bmask, uint64_t *cand,
                        uint32_t cap, uint32_t *count, uint32_t grid, hipStream_t stream) {
     if (tile_hi <= tile_lo) return hipSuccess;
     const uint32_t g = min(grid, tile_hi - tile_lo);
     hipLaunchKernelGGL(roll_kernel, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, tile_hi,
-                       agg, pre, ntiles, bitmap, table, table_bits, cand, cap, count);
+                       agg, pre, ntiles, bitmap, table, bmask, cand, cap, count);
     return hipGetLastError();
 }
 
