@@ -13,9 +13,12 @@
 // Sum1_i == weak(q), Len_i == min(B, size - q) and MD4(window || seed)[:s2len]
 // == Sum2_i[:s2len] (match.go:108-136); after a match the next visited offset
 // is q + Len_i (match.go:158), otherwise q + 1.
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <unordered_map>
 #include <vector>
@@ -34,7 +37,21 @@ namespace {
 constexpr uint32_t kCandCap = 1u << 22;      // candidates per roll launch (32 MiB)
 constexpr uint64_t kSparseBatch = 1u << 16;  // windows per verification batch
 
+// RSG_TIMING=1 prints the host-side phase times of each search to stderr.
+struct PhaseTimer {
+    bool on;
+    std::chrono::steady_clock::time_point t0, t;
+    PhaseTimer() : on(getenv("RSG_TIMING") != nullptr), t0(std::chrono::steady_clock::now()), t(t0) {}
+    void mark(const char *what) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        fprintf(stderr, "[rsg] %-10s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+};
+
 struct Search {
+    PhaseTimer *pt;
     rsg_ctx *ctx;
     hipStream_t st;
     const uint8_t *d_src;
@@ -46,7 +63,7 @@ struct Search {
     // (sum1, block) in targets order, stably sorted by sum1: each sum's blocks
     // are one run, in targets order (match.go:108 walks targets in that order)
     std::vector<std::pair<uint32_t, int32_t>> groups;
-    std::unordered_map<uint64_t, int32_t> verified;  // offset -> block index or -1
+    std::vector<uint32_t> hi16;  // groups index of the first sum with a given high half (65537 entries)
     std::vector<rsg_match> out;
 
     int64_t len_of(int32_t i) const {
@@ -57,22 +74,34 @@ struct Search {
     }
 };
 
-// Confirm a batch of window offsets: Checksum1 + MD4(window || seed) on the GPU,
-// then the first block in targets order whose sums and length agree.
-rsg_status verify(Search &S, const std::vector<uint64_t> &qs) {
-    if (qs.empty()) return RSG_OK;
+// Confirm a batch of candidates (indices into C): Checksum1 + MD4(window ||
+// seed) on the GPU, then the first block in targets order whose sums and
+// length agree.  res[i]: -2 unknown, -1 no match, else the block index.
+rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t> &res,
+                  const std::vector<uint32_t> &idx) {
+    if (idx.empty()) return RSG_OK;
     rsg_ctx *ctx = S.ctx;
-    std::vector<rsg_file> wins(qs.size());
-    for (size_t i = 0; i < qs.size(); i++) {
-        wins[i].data = nullptr;
-        wins[i].offset = qs[i];
-        wins[i].len = S.window(qs[i]);
-        wins[i].block_len = (int32_t)wins[i].len;
-        wins[i].reserved = 0;
-    }
+    // One block per window: the plan is direct (record i = window i).
     HostPlan plan;
-    rsg_status s = build_plan(ctx, wins.data(), wins.size(), S.size, true, plan);
-    if (s != RSG_OK) return s;
+    plan.files.resize(idx.size());
+    plan.total_blocks = idx.size();
+    plan.aligned = false;
+    plan.arena_bytes = S.size;
+    plan.max_blen = 0;
+    std::vector<uint32_t> wlen(idx.size());
+    for (size_t i = 0; i < idx.size(); i++) {
+        const uint64_t q = C[idx[i]];
+        const uint32_t k = S.window(q);
+        wlen[i] = k;
+        plan.files[i] = DevFile{q, k, i, k, 1};
+        plan.max_blen = std::max(plan.max_blen, k);
+    }
+    plan.nwg = (uint32_t)((idx.size() + rsg::kBlockSumThreads - 1) / rsg::kBlockSumThreads);
+    plan.wg_file.resize(plan.nwg + 1);
+    for (uint32_t w = 0; w <= plan.nwg; w++)
+        plan.wg_file[w] = (uint32_t)std::min<uint64_t>((uint64_t)w * rsg::kBlockSumThreads, idx.size() - 1);
+    rsg_status s;
+    S.pt->mark("v.plan");
     if ((s = ensure_dev(ctx, ctx->d_files, plan.files.size() * sizeof(DevFile) + 32)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, ctx->d_wg, plan.wg_file.size() * sizeof(uint32_t) + 4)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, ctx->d_out[0], plan.total_blocks * kRecordBytes)) != RSG_OK) return s;
@@ -82,48 +111,55 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &qs) {
                                 hipMemcpyHostToDevice, S.st));
     if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, S.d_src, S.seed, ctx->d_out[0].p, S.st)) != RSG_OK)
         return s;
-    std::vector<uint8_t> rec(plan.total_blocks * kRecordBytes);
-    RSG_HIP(ctx, hipMemcpyAsync(rec.data(), ctx->d_out[0].p, rec.size(), hipMemcpyDeviceToHost, S.st));
+    if ((s = ensure_pin(ctx, ctx->h_out[0], plan.total_blocks * kRecordBytes)) != RSG_OK) return s;
+    const uint8_t *rec = (const uint8_t *)ctx->h_out[0].p;
+    RSG_HIP(ctx, hipMemcpyAsync(ctx->h_out[0].p, ctx->d_out[0].p, plan.total_blocks * kRecordBytes,
+                                hipMemcpyDeviceToHost, S.st));
     RSG_HIP(ctx, hipStreamSynchronize(S.st));
-    for (size_t i = 0; i < qs.size(); i++) {
-        const uint8_t *r = rec.data() + i * kRecordBytes;
+    S.pt->mark("v.kernel");
+    for (size_t i = 0; i < idx.size(); i++) {
+        const uint8_t *r = rec + i * kRecordBytes;
         uint32_t w;
         memcpy(&w, r, 4);
-        int32_t res = -1;
-        auto it = std::lower_bound(S.groups.begin(), S.groups.end(), std::make_pair(w, INT32_MIN));
-        const int64_t k = (int64_t)wins[i].len;
-        for (; it != S.groups.end() && it->first == w; ++it) {  // targets order, match.go:108
+        int32_t found = -1;
+        const int64_t k = (int64_t)wlen[i];
+        auto it = S.groups.begin() + S.hi16[w >> 16];
+        const auto stop = S.groups.begin() + S.hi16[(w >> 16) + 1];
+        while (it != stop && it->first < w) ++it;
+        for (; it != stop && it->first == w; ++it) {  // targets order, match.go:108
             const int32_t b = it->second;
             if (S.len_of(b) != k) continue;                                                        // :118
             if (memcmp(r + 4, S.sum2 + 16 * (int64_t)b, (size_t)S.head.s2len) != 0) continue;  // :133
-            res = b;
+            found = b;
             break;
         }
-        S.verified[qs[i]] = res;
+        res[idx[i]] = found;
     }
+    S.pt->mark("v.resolve");
     return RSG_OK;
 }
 
 // Greedy walk over one range's sorted candidates (match.go:93-210 reduced to
 // the offsets where the weak sum can hit).
 rsg_status walk(Search &S, const std::vector<uint64_t> &C, uint64_t &pos) {
+    std::vector<int32_t> res(C.size(), -2);
     size_t i = std::lower_bound(C.begin(), C.end(), pos) - C.begin();
+    std::vector<uint32_t> batch;
     while (i < C.size()) {
         const uint64_t c = C[i];
         if ((int64_t)c >= S.end) break;
-        auto it = S.verified.find(c);
-        if (it == S.verified.end()) {
+        if (res[i] == -2) {
             // Batch: every pending candidate ahead while they are sparse (the
             // hashing they cost stays below twice the span they cover); in
             // dense stretches (repetitive data) follow the chain of offsets the
             // walk visits if each confirmation succeeds, plus the candidate
             // after each one in case it fails.
-            std::vector<uint64_t> batch;
+            batch.clear();
             uint64_t hashed = 0;
             size_t j = i;
             for (; j < C.size() && batch.size() < kSparseBatch && (int64_t)C[j] < S.end; j++) {
-                if (!S.verified.count(C[j])) {
-                    batch.push_back(C[j]);
+                if (res[j] == -2) {
+                    batch.push_back((uint32_t)j);
                     hashed += S.window(C[j]);
                 }
             }
@@ -134,19 +170,18 @@ rsg_status walk(Search &S, const std::vector<uint64_t> &C, uint64_t &pos) {
                 for (int n = 0; n < 4096; n++) {
                     size_t a = std::lower_bound(C.begin() + i, C.end(), x) - C.begin();
                     if (a >= C.size() || (int64_t)C[a] >= S.end) break;
-                    if (!S.verified.count(C[a])) batch.push_back(C[a]);
-                    if (a + 1 < C.size() && (int64_t)C[a + 1] < S.end && !S.verified.count(C[a + 1]))
-                        batch.push_back(C[a + 1]);
+                    if (res[a] == -2) batch.push_back((uint32_t)a);
+                    if (a + 1 < C.size() && (int64_t)C[a + 1] < S.end && res[a + 1] == -2)
+                        batch.push_back((uint32_t)(a + 1));
                     x = C[a] + S.window(C[a]);
                 }
                 std::sort(batch.begin(), batch.end());
                 batch.erase(std::unique(batch.begin(), batch.end()), batch.end());
             }
-            rsg_status s = verify(S, batch);
+            rsg_status s = verify(S, C, res, batch);
             if (s != RSG_OK) return s;
-            it = S.verified.find(c);
         }
-        const int32_t b = it->second;
+        const int32_t b = res[i];
         if (b >= 0) {
             S.out.push_back(rsg_match{(int64_t)c, b, 0});
             pos = c + (uint64_t)S.len_of(b);  // match.go:158 + the roll
@@ -162,7 +197,9 @@ rsg_status walk(Search &S, const std::vector<uint64_t> &C, uint64_t &pos) {
 rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_sum_head *head, const uint32_t *sum1,
                   const uint8_t *sum2, const int32_t *targets, int32_t seed, rsg_match *matches, uint64_t match_cap,
                   uint64_t *n_matches) {
+    PhaseTimer pt;
     Search S;
+    S.pt = &pt;
     S.seed = seed;
     S.ctx = ctx;
     S.st = ctx->stream;
@@ -178,12 +215,28 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
     // Basis sums grouped by Sum1 in targets order; device filter = bitmap of
     // every Sum1 + a 2-choice bucketed table {Sum1, flags: bit1 = a block of
     // length B, bit2 = the remainder block}.
-    S.groups.resize((size_t)count);
-    for (int32_t k = 0; k < count; k++) S.groups[(size_t)k] = {sum1[targets[k]], targets[k]};
-    std::stable_sort(S.groups.begin(), S.groups.end(),
-                     [](const std::pair<uint32_t, int32_t> &a, const std::pair<uint32_t, int32_t> &b) {
-                         return a.first < b.first;
-                     });
+    {
+        // Stable LSD radix sort (two 16-bit passes) of the targets-ordered
+        // (sum1, block) list: equal sums keep their targets order.
+        std::vector<std::pair<uint32_t, int32_t>> tmp((size_t)count);
+        S.groups.resize((size_t)count);
+        for (int32_t k = 0; k < count; k++) tmp[(size_t)k] = {sum1[targets[k]], targets[k]};
+        std::vector<uint32_t> cnt(65537);
+        for (int pass = 0; pass < 2; pass++) {
+            auto &from = pass == 0 ? tmp : S.groups;
+            auto &to = pass == 0 ? S.groups : tmp;
+            const int shift = 16 * pass;
+            std::fill(cnt.begin(), cnt.end(), 0u);
+            for (auto &e : from) cnt[((e.first >> shift) & 0xffffu) + 1]++;
+            for (size_t h = 1; h < cnt.size(); h++) cnt[h] += cnt[h - 1];
+            for (auto &e : from) to[cnt[(e.first >> shift) & 0xffffu]++] = e;
+        }
+        S.groups.swap(tmp);
+        S.hi16.assign(65537, 0);
+        for (auto &e : S.groups) S.hi16[(e.first >> 16) + 1]++;
+        for (size_t h = 1; h < S.hi16.size(); h++) S.hi16[h] += S.hi16[h - 1];
+    }
+    pt.mark("groups");
     std::vector<std::pair<uint32_t, uint32_t>> keys;  // distinct sum1 -> flags
     for (size_t i = 0; i < S.groups.size(); i++) {
         const uint32_t f = 1u | ((S.len_of(S.groups[i].second) == B) ? 2u : 4u);
@@ -211,6 +264,7 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
         if (ok) break;
         nb <<= 1;
     }
+    pt.mark("tables");
     const uint64_t ntiles64 = (size + kScanTile - 1) / kScanTile;
     if (ntiles64 >= 0xFFFFFFF0ull) return fail(ctx, RSG_ERR_INVALID, "source too large");
     const uint32_t ntiles = (uint32_t)ntiles64;
@@ -228,6 +282,10 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
     RSG_HIP(ctx, rsg::launch_tile_agg(d_src, size, r, (TileAgg *)ctx->d_agg.p, ntiles, S.st));
     RSG_HIP(ctx, rsg::launch_tile_scan((const TileAgg *)ctx->d_agg.p, ntiles, (TilePrefix *)ctx->d_prefix.p, S.st));
 
+    if (pt.on) {
+        RSG_HIP(ctx, hipStreamSynchronize(S.st));
+        pt.mark("agg+scan");
+    }
     int dev_cus = 256;
     hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
     const uint64_t scan_end = std::min<uint64_t>((uint64_t)S.end, size);
@@ -260,8 +318,11 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
             RSG_HIP(ctx, hipMemcpyAsync(C.data(), ctx->d_list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, S.st));
             RSG_HIP(ctx, hipStreamSynchronize(S.st));
         }
+        pt.mark("roll");
         std::sort(C.begin(), C.end());
+        C.erase(std::unique(C.begin(), C.end()), C.end());
         if ((s = walk(S, C, pos)) != RSG_OK) return s;
+        pt.mark("walk");
         lo = hi;
     }
     *n_matches = S.out.size();

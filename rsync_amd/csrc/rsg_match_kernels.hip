@@ -183,7 +183,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     constexpr uint32_t kWaves = kRollThreads / 64;
     __shared__ uint32_t bitmap[kFilterBits / 32];       // 64 KiB
     __shared__ uint2 queue[kWaves][kQueueCap];           // (tile-local offset, sum)
-    __shared__ uint32_t wsum[2][kWaves][4];              // scan partials, double-buffered per tile
+    __shared__ uint4 wsum[2][kWaves];                     // scan partials, double-buffered per tile
     for (uint32_t i = threadIdx.x; i < kFilterBits / 32; i += kRollThreads) bitmap[i] = bitmap_g[i];
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
@@ -249,18 +249,15 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                 if (lane >= (uint32_t)d) incl[c] += o;
             }
         }
-        if (lane == 63) {
-#pragma unroll
-            for (int c = 0; c < 4; c++) wsum[parity][wave][c] = incl[c];
-        }
+        if (lane == 63) wsum[parity][wave] = make_uint4(incl[0], incl[1], incl[2], incl[3]);
         __syncthreads();
-        uint32_t ex[4];
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            uint32_t add = 0;
-            for (uint32_t w = 0; w < wave; w++) add += wsum[parity][w][c];
-            ex[c] = incl[c] - v[c] + add;
+        uint4 add = make_uint4(0, 0, 0, 0);
+        for (uint32_t w = 0; w < wave; w++) {
+            const uint4 p = wsum[parity][w];
+            add.x += p.x; add.y += p.y; add.z += p.z; add.w += p.w;
         }
+        const uint32_t ex[4] = {incl[0] - v[0] + add.x, incl[1] - v[1] + add.y, incl[2] - v[2] + add.z,
+                                incl[3] - v[3] + add.w};
         parity ^= 1u;
         // Lanes past `end` stay in the loop (they never hit): drain() spreads the
         // wave's parked hits over all 64 lanes.
@@ -284,33 +281,82 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
             k = qt < size ? (uint32_t)(size - qt) : 0u;
         }
         uint32_t nq = 0;  // wave-uniform queue fill
-#pragma unroll
-        for (int j = 0; j < (int)kRollPerThread; j++) {
-            const uint64_t q = qt + j;
-            const uint32_t sum = (W1 & 0xffffu) | (W2 << 16);  // match.go:106
-            const uint32_t fi = filter_index(sum);
-            const bool hit = q < end && ((bitmap[fi >> 5] >> (fi & 31)) & 1u);
+        // Park one offset's filter hit in the wave's LDS queue (wave-uniform
+        // branch on the ballot).  When the queue is full (repetitive data: most
+        // offsets hit) the hit goes straight to the candidate list unprobed;
+        // the host-side confirmation re-checks Checksum1 exactly anyway.
+        auto park = [&](bool hit, uint32_t j, uint32_t sum) {
             const uint64_t bal = __ballot(hit);
             if (bal) {
                 const uint32_t nb = __popcll(bal);
-                if (nq + nb > kQueueCap) {
-                    drain(q0, nq);
-                    nq = 0;
+                if (nq + nb <= kQueueCap) {
+                    if (hit) {
+                        const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                            (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                        queue[wave][nq + below] = make_uint2(lo + j, sum);
+                    }
+                    nq += nb;
+                } else if (hit) {
+                    const uint32_t at = atomicAdd(count, 1u);
+                    if (at < cap) cand[at] = q0 + lo + j;
                 }
-                if (hit) {
-                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    queue[wave][nq + below] = make_uint2(lo + j, sum);
-                }
-                nq += nb;
             }
-            // rolling update, match.go:171-196
-            const int32_t xo = sx8(O[j >> 2], j & 3);
-            const bool more = q + k < size;
-            const int32_t xi = more ? sx8(S[j >> 2], j & 3) : 0;
-            W1 = W1 - (uint32_t)xo + (uint32_t)xi;
-            W2 = W2 - k * (uint32_t)xo + (more ? W1 : 0u);
-            if (!more) k--;
+        };
+        // Offsets go in groups of 8: the 8 sums and their bitmap words are
+        // computed and fetched first (one LDS wait per group, not per offset),
+        // then the hits are parked.
+        constexpr int G = 8;
+        if (q0 + kScanTile <= end && q0 + kScanTile + B <= size) {
+            // Interior tile: every offset is visited and every window has its
+            // full length B and a byte entering (match.go:175-191 "more").
+            // S2 only matters mod 2^16, so B*x uses B mod 2^16 (24-bit mul).
+            const int32_t B16 = (int32_t)(B & 0xffffu);
+#pragma unroll
+            for (int g0 = 0; g0 < (int)kRollPerThread; g0 += G) {
+                uint32_t sum[G], word[G];
+#pragma unroll
+                for (int jj = 0; jj < G; jj++) {
+                    const int j = g0 + jj;
+                    sum[jj] = __builtin_amdgcn_perm(W2, W1, 0x05040100u);  // (W1 & 0xffff) | W2 << 16, match.go:106
+                    word[jj] = bitmap[filter_index(sum[jj]) >> 5];
+                    const int32_t xo = sx8(O[j >> 2], j & 3);
+                    const int32_t xi = sx8(S[j >> 2], j & 3);
+                    W1 += (uint32_t)(xi - xo);
+                    W2 = W2 + (uint32_t)__mul24(-B16, xo) + W1;
+                }
+#pragma unroll
+                for (int jj = 0; jj < G; jj++) {
+                    const bool hit = (word[jj] >> (filter_index(sum[jj]) & 31)) & 1u;
+                    park(hit, (uint32_t)(g0 + jj), sum[jj]);
+                }
+            }
+        } else {
+            // Edge tile (the file's end is near): 32-bit offsets relative to q0.
+            const uint32_t end_rel = (uint32_t)min<uint64_t>(end - q0, 0xFFFFFFFFull);
+            const uint32_t size_rel = (uint32_t)min<uint64_t>(size > q0 ? size - q0 : 0, 0xFFFFFFFFull);
+#pragma unroll
+            for (int g0 = 0; g0 < (int)kRollPerThread; g0 += G) {
+                uint32_t sum[G], word[G];
+#pragma unroll
+                for (int jj = 0; jj < G; jj++) {
+                    const int j = g0 + jj;
+                    const uint32_t qr = lo + j;
+                    sum[jj] = __builtin_amdgcn_perm(W2, W1, 0x05040100u);
+                    word[jj] = bitmap[filter_index(sum[jj]) >> 5];
+                    // rolling update, match.go:171-196
+                    const int32_t xo = sx8(O[j >> 2], j & 3);
+                    const bool more = qr + k < size_rel;
+                    const int32_t xi = more ? sx8(S[j >> 2], j & 3) : 0;
+                    W1 = W1 - (uint32_t)xo + (uint32_t)xi;
+                    W2 = W2 - k * (uint32_t)xo + (more ? W1 : 0u);
+                    if (!more) k--;
+                }
+#pragma unroll
+                for (int jj = 0; jj < G; jj++) {
+                    const bool hit = ((word[jj] >> (filter_index(sum[jj]) & 31)) & 1u) && (lo + g0 + jj < end_rel);
+                    park(hit, (uint32_t)(g0 + jj), sum[jj]);
+                }
+            }
         }
         drain(q0, nq);
     }
