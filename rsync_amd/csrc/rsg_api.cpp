@@ -136,13 +136,14 @@ rsg_status build_plan(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, uint
 }
 
 rsg_status launch_plan(rsg_ctx *ctx, const HostPlan &plan, const void *d_files, const void *d_wg,
-                       const void *d_arena, int32_t seed, void *d_records, hipStream_t stream) {
+                       const void *d_arena, int32_t seed, void *d_records, void *d_scratch, hipStream_t stream) {
     if (plan.total_blocks == 0) return RSG_OK;
     if (!d_arena || !d_records) return fail(ctx, RSG_ERR_INVALID, "NULL device pointer");
     const bool aligned = plan.aligned && (((uintptr_t)d_arena & 3u) == 0);
     RSG_HIP(ctx, rsg::launch_block_sums((const uint8_t *)d_arena, plan.arena_bytes, (const DevFile *)d_files,
                                         (const uint32_t *)d_wg, plan.total_blocks, plan.nwg, aligned,
-                                        plan.max_blen, (uint32_t)seed, (uint8_t *)d_records, stream));
+                                        plan.max_blen, (uint32_t)seed, (uint8_t *)d_records,
+                                        (uint32_t *)d_scratch, stream));
     return RSG_OK;
 }
 
@@ -225,7 +226,7 @@ void rsg_ctx_destroy(rsg_ctx *c) {
     for (int i = 0; i < 2; i++)
         if (c->side[i]) hipStreamSynchronize(c->side[i]);
     DevBuf *dbs[] = {&c->d_files, &c->d_wg, &c->d_in[0], &c->d_in[1], &c->d_out[0], &c->d_out[1],
-                     &c->d_desc[0], &c->d_desc[1], &c->d_agg, &c->d_prefix, &c->d_bits, &c->d_counts,
+                     &c->d_desc[0], &c->d_desc[1], &c->d_fb[0], &c->d_fb[1], &c->d_agg, &c->d_prefix, &c->d_bits, &c->d_counts,
                      &c->d_list, &c->d_table, &c->d_filter, &c->d_misc};
     for (DevBuf *b : dbs)
         if (b->p) hipFree(b->p);
@@ -342,6 +343,7 @@ rsg_status rsg_plan_create(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles,
     hipError_t e;
     if ((e = hipMalloc(&p->d_files, std::max<uint64_t>(p->host.files.size(), 1) * sizeof(DevFile))) != hipSuccess ||
         (e = hipMalloc(&p->d_wg, p->host.wg_file.size() * sizeof(uint32_t) + 4)) != hipSuccess ||
+        (e = hipMalloc(&p->d_scratch, rsg::block_sums_scratch_bytes(p->host.total_blocks))) != hipSuccess ||
         (e = hipMemcpy(p->d_files, p->host.files.data(), p->host.files.size() * sizeof(DevFile),
                        hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(p->d_wg, p->host.wg_file.data(), p->host.wg_file.size() * sizeof(uint32_t),
@@ -358,6 +360,7 @@ void rsg_plan_destroy(rsg_plan *p) {
     if (p->ctx) hipSetDevice(p->ctx->device);
     if (p->d_files) hipFree(p->d_files);
     if (p->d_wg) hipFree(p->d_wg);
+    if (p->d_scratch) hipFree(p->d_scratch);
     delete p;
 }
 
@@ -367,13 +370,13 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
                                   void *d_records, void *stream) {
     RSG_ENTER(ctx);
     if (!plan || plan->ctx != ctx) return fail(ctx, RSG_ERR_INVALID, "plan belongs to another context");
-    return launch_plan(ctx, plan->host, plan->d_files, plan->d_wg, d_arena, seed, d_records,
+    return launch_plan(ctx, plan->host, plan->d_files, plan->d_wg, d_arena, seed, d_records, plan->d_scratch,
                        pick_stream(ctx, stream));
 }
 
 rsg_status rsg_set_block_sums_kernel(int32_t variant) {
-    if (variant < -1 || (variant > 3 && variant < 10) || variant > 16)
-        return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..3 or 10..16");
+    if (variant < -1 || (variant > 4 && variant < 10) || variant > 17)
+        return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..4 or 10..17");
     rsg::set_block_sums_variant(variant);
     return RSG_OK;
 }
@@ -393,7 +396,9 @@ rsg_status rsg_block_sums_device(rsg_ctx *ctx, const void *d_arena, uint64_t are
                                 hipMemcpyHostToDevice, ctx->stream));
     RSG_HIP(ctx, hipMemcpyAsync(ctx->d_wg.p, plan.wg_file.data(), plan.wg_file.size() * sizeof(uint32_t),
                                 hipMemcpyHostToDevice, ctx->stream));
-    if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, d_arena, seed, d_records, ctx->stream)) != RSG_OK)
+    if ((s = ensure_dev(ctx, ctx->d_fb[0], rsg::block_sums_scratch_bytes(plan.total_blocks))) != RSG_OK) return s;
+    if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, d_arena, seed, d_records, ctx->d_fb[0].p,
+                         ctx->stream)) != RSG_OK)
         return s;
     RSG_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return RSG_OK;
@@ -461,6 +466,7 @@ rsg_status rsg_block_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfi
         if ((s = ensure_dev(ctx, ctx->d_in[k], max_bytes)) != RSG_OK) return s;
         if ((s = ensure_dev(ctx, ctx->d_out[k], max_recs * kRecordBytes)) != RSG_OK) return s;
         if ((s = ensure_dev(ctx, ctx->d_desc[k], desc_bytes)) != RSG_OK) return s;
+        if ((s = ensure_dev(ctx, ctx->d_fb[k], rsg::block_sums_scratch_bytes(max_recs))) != RSG_OK) return s;
         if ((s = ensure_pin(ctx, ctx->h_in[k], max_bytes)) != RSG_OK) return s;
         if ((s = ensure_pin(ctx, ctx->h_out[k], max_recs * kRecordBytes)) != RSG_OK) return s;
         if ((s = ensure_pin(ctx, ctx->h_desc[k], desc_bytes)) != RSG_OK) return s;
@@ -505,7 +511,8 @@ rsg_status rsg_block_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfi
         uint8_t *dd = (uint8_t *)ctx->d_desc[slot].p;
         RSG_HIP(ctx, hipMemcpyAsync(dd, hd, wg_off + plan.wg_file.size() * 4, hipMemcpyHostToDevice, st));
         RSG_HIP(ctx, hipMemcpyAsync(ctx->d_in[slot].p, stage, off, hipMemcpyHostToDevice, st));
-        if ((s = launch_plan(ctx, plan, dd, dd + wg_off, ctx->d_in[slot].p, seed, ctx->d_out[slot].p, st)) != RSG_OK)
+        if ((s = launch_plan(ctx, plan, dd, dd + wg_off, ctx->d_in[slot].p, seed, ctx->d_out[slot].p,
+                             ctx->d_fb[slot].p, st)) != RSG_OK)
             return s;
         RSG_HIP(ctx, hipMemcpyAsync(ctx->h_out[slot].p, ctx->d_out[slot].p, b.recs * kRecordBytes,
                                     hipMemcpyDeviceToHost, st));

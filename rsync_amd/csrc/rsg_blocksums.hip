@@ -21,6 +21,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include "rsg_internal.h"
 #include "rsg_md4.h"
 
@@ -533,6 +535,163 @@ __global__ __launch_bounds__(256) void diag_linear_read(const uint8_t *__restric
     if (acc == 0x12345678u) sink[0] = acc;  // keep the loads alive
 }
 
+// ---------------------------------------------------------------- register-tile variant
+// For blocks of at most kRegMaxBytes (the reference's default 700-byte blocks):
+// a wave's 64 consecutive blocks are fetched as ONE near-linear stream of
+// 1 KiB LDS-DMA instructions (block j lands at j*720 in an LDS tile, so each
+// instruction covers ~1.4 contiguous blocks: full cache lines, DRAM rows read
+// once), then every lane copies its block into VGPRs with 16-byte-aligned
+// ds_read_b128 (stride 720 B = 180 dwords: conflict-free) and hashes it from
+// registers.  A persistent 8-wave workgroup per CU shares kRtBufs LDS tiles:
+// the waves of one tile buffer take turns in a fixed order (an LDS ticket),
+// so while some waves hash, others keep the HBM stream busy.
+constexpr uint32_t kRtPiece = 720;                 // LDS bytes per block (45 x 16 B)
+constexpr uint32_t kRtTile = 64 * kRtPiece;        // 46080 B per wave tile
+constexpr uint32_t kRtDma = kRtTile / 1024;        // 45 DMA instructions per tile
+constexpr uint32_t kRtBufs = 3;
+constexpr uint32_t kRtWaves = 8;
+constexpr uint32_t kRtThreads = 64 * kRtWaves;
+static_assert(kRtTile % 1024 == 0, "tile must be whole DMA instructions");
+
+// Follow-up to the register-tile kernel: the tiles (64 blocks) it could not
+// stage (the arena's last partial tile, a tile whose 720-byte reads would run
+// past the arena, giant spans) are hashed here with per-lane loads.
+// fb[0] = count, fb[1..] = tile indices.
+__global__ __launch_bounds__(64) void block_sums_tile_fallback(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out, const uint32_t *__restrict__ fb) {
+    const uint32_t count = fb[0];
+    const uintptr_t aend = (uintptr_t)(arena + arena_bytes);
+    for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
+        const uint64_t t = fb[1 + i];
+        const uint64_t g = t * 64 + threadIdx.x;
+        if (g >= total_blocks) continue;
+        const uint64_t wlo = t * 64 / 256, whi = (t * 64 + 63) / 256 + 1;
+        uint32_t lo = wg_file[wlo < nwg256 ? wlo : nwg256];
+        uint32_t hi = wg_file[whi < nwg256 ? whi : nwg256];
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (files[mid].first_block <= g) lo = mid; else hi = mid - 1;
+        }
+        const DevFile F = files[lo];
+        const uint64_t boff = (g - F.first_block) * F.blen;
+        const uint64_t left = F.len - boff;
+        const uint32_t n = left < F.blen ? (uint32_t)left : F.blen;
+        const uint64_t off = F.offset + boff;
+        uint32_t h[4];
+        md4_init(h);
+        int32_t s1 = 0;
+        uint32_t tw = 0;
+        if (((uintptr_t)(arena + off) & 3u) == 0) hash_block_direct<true>(arena, aend, off, n, seed, h, s1, tw);
+        else hash_block_direct<false>(arena, aend, off, n, seed, h, s1, tw);
+        store_record(out, g, n, s1, tw, h);
+    }
+}
+
+template <int MODE>  // 0 = product, 1 = memory only (diagnostic)
+__global__ __launch_bounds__(kRtThreads) void block_sums_regtile(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out, uint32_t *__restrict__ fb) {
+    __shared__ __attribute__((aligned(16))) uint8_t tiles[kRtBufs][kRtTile];
+    __shared__ uint32_t turn[kRtBufs];
+    if (threadIdx.x < kRtBufs) turn[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t buf = wave % kRtBufs;
+    const uint32_t users = (kRtWaves - buf + kRtBufs - 1) / kRtBufs;  // waves sharing this buffer
+    const uint32_t order = wave / kRtBufs;                             // this wave's turn within a round
+    uint8_t *tile = &tiles[buf][0];
+    const uint64_t ntile = (total_blocks + 63) / 64;
+    const uint64_t per_round = (uint64_t)gridDim.x * kRtWaves;
+    const uint32_t rounds = (uint32_t)((ntile + per_round - 1) / per_round);
+
+    for (uint32_t r = 0; r < rounds; r++) {
+        const uint64_t t = (uint64_t)r * per_round + (uint64_t)blockIdx.x * kRtWaves + wave;
+        const uint64_t g = t * 64 + lane;
+        const bool valid = g < total_blocks;
+        uint64_t off = 0;
+        uint32_t n = 0;
+        if (valid) {
+            const uint64_t gq = g;
+            const uint64_t wlo = t * 64 / 256, whi = (t * 64 + 63) / 256 + 1;
+            uint32_t lo = wg_file[wlo < nwg256 ? wlo : nwg256];
+            uint32_t hi = wg_file[whi < nwg256 ? whi : nwg256];
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (files[mid].first_block <= gq) lo = mid; else hi = mid - 1;
+            }
+            const DevFile F = files[lo];
+            const uint64_t boff = (g - F.first_block) * F.blen;
+            const uint64_t left = F.len - boff;
+            n = left < F.blen ? (uint32_t)left : F.blen;
+            off = F.offset + boff;
+        }
+        // wave-uniform: staged through the LDS tile, or per-lane fallback
+        const uint64_t base_v = wave_min_u64(valid ? off : ~0ull);
+        const uint64_t base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(base_v >> 32)) << 32) |
+                              __builtin_amdgcn_readfirstlane((uint32_t)base_v);
+        const uint64_t top = wave_max_u64(valid ? off + kRtPiece : 0);
+        const uint32_t nmax = (uint32_t)wave_max_u64(n);
+        const bool fast = (t * 64 + 63 < total_blocks) && nmax <= kRegMaxBytes && top <= arena_bytes &&
+                          (top - base) <= 0x7FFFFFFFull;
+
+        // take this wave's turn on its tile buffer
+        const uint32_t ticket = r * users + order;
+        while (__hip_atomic_load(&turn[buf], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != ticket)
+            __builtin_amdgcn_s_sleep(1);
+        uint32_t R[16 * kRegChunks];
+        if (fast) {
+            const __amdgpu_buffer_rsrc_t rsrc =
+                __builtin_amdgcn_make_buffer_rsrc((void *)(arena + base), (short)0, 0x7FFFFFFF, 0x00020000);
+            const uint32_t rel = (uint32_t)(off - base);
+#pragma unroll 5
+            for (uint32_t i = 0; i < kRtDma; i++) {
+                const uint32_t idx = 64u * i + lane;
+                const uint32_t j = idx / 45u, u = idx - 45u * j;
+                const uint32_t voff = __shfl(rel, (int)j, 64) + 16u * u;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rsrc, (__attribute__((address_space(3))) void *)(tile + 1024u * i), 16, voff, 0, 0, 0);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint8_t *mine = tile + lane * kRtPiece;
+#pragma unroll
+            for (uint32_t q = 0; q < 4 * kRegChunks; q++) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
+                R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        // release the buffer to the next wave in line
+        if (lane == 0) __hip_atomic_fetch_add(&turn[buf], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+
+        if (fast) {
+            uint32_t h[4];
+            md4_init(h);
+            int32_t s1 = 0;
+            uint32_t tw = 0;
+            const uint32_t nfull = n >> 6;
+            if (MODE == 1) {
+#pragma unroll
+                for (int q = 0; q < 16 * (int)kRegChunks; q++) h[q & 3] ^= R[q];
+            } else {
+#pragma unroll
+                for (uint32_t c = 0; c < kRegChunks; c++) {
+                    if (c < nfull) hash_chunk<true>(R + 16 * c, 0u, 0u, c, h, s1, tw);
+                    else if (c == nfull) hash_tail<true>(R + 16 * c, 0u, 0u, n, seed, h, s1, tw);
+                }
+            }
+            store_record(out, g, n, s1, tw, h);
+        } else if (valid && lane == 0 && MODE == 0) {
+            // irregular wave: the follow-up kernel hashes its blocks per lane
+            const uint32_t at = atomicAdd(&fb[0], 1u);
+            fb[1 + at] = (uint32_t)t;
+        }
+    }
+}
+
 // Kernel variants (rsg_set_block_sums_kernel): -1 = automatic, 0 = direct,
 // 1 = staged K=1, 2 = staged K=4, 3 = register-block.  Timing diagnostics with
 // meaningless outputs: 10 = staged K=1 memory only, 11 = staged K=1 hashing
@@ -542,7 +701,7 @@ static int g_variant = -2;  // -2 = not yet read from RSG_BLOCKSUMS_KERNEL
 
 hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const DevFile *files,
                              const uint32_t *wg_file, uint64_t total_blocks, uint32_t nwg, bool aligned,
-                             uint32_t max_blen, uint32_t seed, uint8_t *out, hipStream_t stream) {
+                             uint32_t max_blen, uint32_t seed, uint8_t *out, uint32_t *scratch, hipStream_t stream) {
     if (total_blocks == 0) return hipSuccess;
     if (g_variant == -2) {
         const char *e = getenv("RSG_BLOCKSUMS_KERNEL");
@@ -551,7 +710,8 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     int v = g_variant;
     if (v == -1) v = 1;  // automatic choice
     if (!aligned && v < 13) v = 0;
-    if ((v == 3 || v == 12) && max_blen > kRegMaxBytes) v = 1;
+    if ((v == 3 || v == 4 || v == 12 || v == 17) && max_blen > kRegMaxBytes) v = 1;
+    if ((v == 4 || v == 17) && !scratch) v = 1;
     dim3 grid(nwg), block(kBlockSumThreads);
 #define RSG_LAUNCH(KERNEL, GRID) \
     hipLaunchKernelGGL(KERNEL, GRID, block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out)
@@ -565,6 +725,24 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             break;
         case 2: RSG_STAGED(4, 0); break;
         case 3: RSG_LAUNCH(block_sums_regblock<0>, grid); break;
+        case 4:
+        case 17: {
+            int cus = 256;
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+            const uint64_t ntile = (total_blocks + 63) / 64;
+            const uint32_t g = (uint32_t)std::min<uint64_t>((uint64_t)cus, (ntile + kRtWaves - 1) / kRtWaves);
+            hipError_t e = hipMemsetAsync(scratch, 0, 4, stream);
+            if (e != hipSuccess) return e;
+            if (v == 4)
+                hipLaunchKernelGGL(block_sums_regtile<0>, dim3(g), dim3(kRtThreads), 0, stream, arena, arena_bytes,
+                                   files, wg_file, nwg, total_blocks, seed, out, scratch);
+            else
+                hipLaunchKernelGGL(block_sums_regtile<1>, dim3(g), dim3(kRtThreads), 0, stream, arena, arena_bytes,
+                                   files, wg_file, nwg, total_blocks, seed, out, scratch);
+            hipLaunchKernelGGL(block_sums_tile_fallback, dim3(256), dim3(64), 0, stream, arena, arena_bytes, files,
+                               wg_file, nwg, total_blocks, seed, out, (const uint32_t *)scratch);
+            break;
+        }
         case 10: RSG_STAGED(1, 1); break;
         case 11: RSG_STAGED(1, 2); break;
         case 15: RSG_STAGED(1, 3); break;

@@ -32,7 +32,7 @@ struct rsg_ctx {
     std::string err;
     // scratch reused by one-shot calls
     DevBuf d_files, d_wg;
-    DevBuf d_in[2], d_out[2], d_desc[2];
+    DevBuf d_in[2], d_out[2], d_desc[2], d_fb[2];
     PinBuf h_in[2], h_out[2], h_desc[2];
     // sender scratch
     DevBuf d_agg, d_prefix, d_bits, d_counts, d_list, d_table, d_filter, d_misc;
@@ -58,6 +58,7 @@ struct rsg_plan {
     HostPlan host;
     void *d_files = nullptr;
     void *d_wg = nullptr;
+    void *d_scratch = nullptr;
 };
 
 namespace rsgh {
@@ -78,7 +79,7 @@ rsg_status build_plan(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, uint
 
 // Upload plan descriptors to (grown) device buffers and launch the kernel.
 rsg_status launch_plan(rsg_ctx *ctx, const HostPlan &plan, const void *d_files, const void *d_wg,
-                       const void *d_arena, int32_t seed, void *d_records, hipStream_t stream);
+                       const void *d_arena, int32_t seed, void *d_records, void *d_scratch, hipStream_t stream);
 
 }  // namespace rsgh
 

@@ -109,7 +109,9 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
                                 hipMemcpyHostToDevice, S.st));
     RSG_HIP(ctx, hipMemcpyAsync(ctx->d_wg.p, plan.wg_file.data(), plan.wg_file.size() * sizeof(uint32_t),
                                 hipMemcpyHostToDevice, S.st));
-    if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, S.d_src, S.seed, ctx->d_out[0].p, S.st)) != RSG_OK)
+    if ((s = ensure_dev(ctx, ctx->d_fb[0], rsg::block_sums_scratch_bytes(plan.total_blocks))) != RSG_OK) return s;
+    if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, S.d_src, S.seed, ctx->d_out[0].p, ctx->d_fb[0].p,
+                         S.st)) != RSG_OK)
         return s;
     if ((s = ensure_pin(ctx, ctx->h_out[0], plan.total_blocks * kRecordBytes)) != RSG_OK) return s;
     const uint8_t *rec = (const uint8_t *)ctx->h_out[0].p;

@@ -176,7 +176,7 @@ def test_generate_and_send_sums_wire(eng):
     assert bytes(conn.buf) == want
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("blen", [700, 64, 1773, 4096, 131072])
 def test_kernel_variants_match(eng, variant, blen):
     """Every kernel variant (direct / staged K=1 / staged K=4 / register-block)
@@ -197,3 +197,34 @@ def test_kernel_variants_match(eng, variant, blen):
         _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
     assert rec == want
     assert rec_dev == want
+
+
+@pytest.mark.parametrize("variant", [1, 4])
+def test_variants_device_aligned_arena(eng, variant):
+    """Aligned device arena (the staged / register-tile fast paths), files
+    straddling waves, a file ending exactly at the arena end, blocks of
+    700/64/703 bytes."""
+    from rsync_amd import _lib
+    lens = [1 << 20, 700 * 64 * 3 + 5, 12344, 64, 4, 0, 300_000, 70_000 * 3]
+    offs, o = [], 0
+    for n in lens:
+        offs.append(o)
+        o += (n + 15) & ~15
+    arena_bytes = offs[-1] + lens[-1]
+    host = np.zeros(arena_bytes, np.uint8)
+    datas = []
+    for i, (off, n) in enumerate(zip(offs, lens)):
+        d = cases.splitmix64_bytes(5000 + i, n)
+        host[off:off + n] = d
+        datas.append(d)
+    arena = eng.alloc(arena_bytes)
+    arena.upload(host)
+    for blen in (700, 64, 703):
+        want = b"".join(orc.block_sums(d, blen, cases.SEED) for d in datas)
+        try:
+            _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))
+            recs, total = eng.block_sums_device(arena, [(o, n, blen) for o, n in zip(offs, lens)], cases.SEED)
+            got = recs.download(total * 20).tobytes()
+        finally:
+            _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+        assert got == want, blen
