@@ -4,7 +4,7 @@
 # Usage: tools/profile.sh <tag> [bench args...]
 set -o pipefail
 TAG=${1:-r01}; shift
-ARGS=${@:---steps 20 --warmup 3 --no-cpu --no-host-path}
+ARGS=${@:---steps 30 --warmup 100 --no-cpu --no-host-path}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
