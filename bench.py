@@ -122,7 +122,7 @@ def main():
     extra = {}
     if args.ab:
         from rsync_amd import _lib
-        names = {1: "staged_k1", 6: "lring", 10: "diag_staged_memory_only", 20: "diag_lring_memory_only", 21: "diag_lring_loads_only",
+        names = {1: "staged_k1", 6: "lring", 7: "lring_share", 22: "diag_lring_share_memory_only", 10: "diag_staged_memory_only", 20: "diag_lring_memory_only", 21: "diag_lring_loads_only",
                  11: "diag_staged_hash_only", 14: "diag_linear_read_ldsdma", 13: "diag_linear_read"}
         res = {v: [] for v in names}
         for _ in range(5):

@@ -594,7 +594,14 @@ constexpr uint32_t kLrWave = kLrSlots * kRingSlot;   // 18432 B per wave
 constexpr uint32_t kLrLoads = 8;                     // load instructions per line step
 
 // 0 = product; timing diagnostics (outputs meaningless): 1 = loads + LDS round trip, 2 = loads only
-template <int MODE>
+// SHARE: block j's last line is usually block j+1's first line (blocks are
+// contiguous and rarely end on a line boundary).  Without sharing, lane j+1
+// fetches it at step 0 and lane j again ~6 steps later, long evicted from L2:
+// ~1 extra line per block (6.5 instead of 5.5 for 700-byte blocks).  With
+// SHARE, lane j copies that line out of lane j+1's slot right after step 0's
+// store into 32 VGPRs and writes it into its own slot when its stream reaches
+// it, so the line is requested once.
+template <int MODE, bool SHARE = false>
 __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
@@ -629,6 +636,14 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
     const uint32_t rel = (uint32_t)(abs - base);
     const uint32_t d = rel & 127u;
     const uint32_t nl = (d + n + 127u) >> 7;
+    const uint32_t l0 = rel >> 7;  // first line, relative to base
+    const uint32_t next_l0 = __shfl(l0, (int)((lane + 1) & 63u), 64);
+    const bool share0 = SHARE && lane < 63u && next_l0 == l0 + nl - 1u;
+    // lane j+1 must load its first line itself (not when that line is also
+    // its last and shared onward: a one-line block between two neighbours)
+    const uint32_t next_self = __shfl((uint32_t)(!share0 || nl > 1u), (int)((lane + 1) & 63u), 64);
+    const bool share = share0 && next_self;
+    const uint32_t nl_load = nl - (share ? 1u : 0u);  // lines this lane's stream loads itself
     const uint32_t nfull = n >> 6;
     const uint32_t steps = (nfull + 2u) >> 1;
     const uint32_t T = __builtin_amdgcn_readfirstlane((uint32_t)wave_max_u64(steps));
@@ -640,7 +655,7 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
     for (uint32_t q = 0; q < kLrLoads; q++) {
         const uint32_t j = 8u * q + (lane >> 3), u = lane & 7u;
         voff[q] = __shfl(rel & ~127u, (int)j, 64) + 16u * u;
-        vnl[q] = __shfl(nl, (int)j, 64);
+        vnl[q] = __shfl(nl_load, (int)j, 64);
         wpos[q] = j * kRingLane + 16u * u;
     }
     uint8_t *ring = ring_all + 128 + wave * kLrWave;
@@ -660,6 +675,21 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
             else *reinterpret_cast<u32x4v *>(ring + slot * kRingSlot + wpos[q]) = buf[q];
         }
     };
+    u32x4v tail[SHARE ? 8 : 1];
+    auto fetch_tail = [&]() {  // lane j+1's first line, now in slot 0
+        if (SHARE) {
+#pragma unroll
+            for (uint32_t u = 0; u < 8; u++)
+                tail[u] = *reinterpret_cast<const u32x4v *>(ring + (lane + 1u) * kRingLane + 16u * u);
+        }
+    };
+    auto put_tail = [&](uint32_t t, uint32_t slot) {  // line t just stored into slot
+        if (SHARE && share && t == nl - 1u) {
+#pragma unroll
+            for (uint32_t u = 0; u < 8; u++)
+                *reinterpret_cast<u32x4v *>(ring + slot * kRingSlot + lane * kRingLane + 16u * u) = tail[u];
+        }
+    };
     const uint8_t *mine = ring + lane * kRingLane + d;
     const uint32_t split = (128u - d) >> 2;  // words 0..split-1 from line i, the rest from line i+1
 
@@ -668,8 +698,12 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
     int32_t s1 = 0;
     uint32_t tw = 0;
     auto step = [&](uint32_t i, uint32_t sa) {  // chunks 2i, 2i+1; line i in slot sa
-        const uint8_t *pA = mine + sa * kRingSlot;
-        const uint8_t *pB = mine + (sa ^ 1u) * kRingSlot - 128;
+        // opaque slot index: the 64 per-word addresses are recomputed each
+        // step (one select per word) instead of being held in 64 VGPRs
+        uint32_t so = sa;
+        asm volatile("" : "+s"(so));
+        const uint8_t *pA = mine + so * kRingSlot;
+        const uint8_t *pB = mine + (so ^ 1u) * kRingSlot - 128;
         uint32_t X[32];
 #pragma unroll
         for (uint32_t k = 0; k < 32; k++)
@@ -696,7 +730,10 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
     load_line(0, bufA);
     load_line(1, bufB);
     store_line(0, bufA);
+    fetch_tail();
+    put_tail(0, 0);
     store_line(1, bufB);
+    put_tail(1, 1);
     // The scheduler must not interleave these two groups: the loop below
     // relies on line 2's loads being older than line 3's (vmcnt is in order).
     load_line(2, bufA);
@@ -710,12 +747,14 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
         {
             auto hash = step(i, 0);  // lines i (slot 0), i+1 (slot 1)
             store_line(0, bufA);     // line i+2 -> slot 0
+            put_tail(i + 2, 0);
             load_line(i + 4, bufA);
             hash();
         }
         {
             auto hash = step(i + 1, 1);  // lines i+1 (slot 1), i+2 (slot 0)
             store_line(1, bufB);         // line i+3 -> slot 1
+            put_tail(i + 3, 1);
             load_line(i + 5, bufB);
             hash();
         }
@@ -1033,6 +1072,8 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 6: RSG_LAUNCH(block_sums_lring<0>, grid); break;
         case 20: RSG_LAUNCH(block_sums_lring<1>, grid); break;
         case 21: RSG_LAUNCH(block_sums_lring<2>, grid); break;
+        case 7: RSG_LAUNCH((block_sums_lring<0, true>), grid); break;
+        case 22: RSG_LAUNCH((block_sums_lring<1, true>), grid); break;
         case 19: RSG_LAUNCH(block_sums_ring<2>, grid); break;
         case 10: RSG_STAGED(1, 1); break;
         case 11: RSG_STAGED(1, 2); break;
