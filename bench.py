@@ -122,8 +122,9 @@ def main():
     extra = {}
     if args.ab:
         from rsync_amd import _lib
-        names = {1: "staged_k1", 6: "lring", 7: "lring_share", 22: "diag_lring_share_memory_only", 10: "diag_staged_memory_only", 20: "diag_lring_memory_only", 21: "diag_lring_loads_only",
-                 11: "diag_staged_hash_only", 14: "diag_linear_read_ldsdma", 13: "diag_linear_read"}
+        names = {1: "staged_k1", 6: "lring", 8: "lring_depth3", 9: "lring_share_depth3",
+                 10: "diag_staged_memory_only", 20: "diag_lring_memory_only", 21: "diag_lring_loads_only",
+                 11: "diag_staged_hash_only", 13: "diag_linear_read", 14: "diag_linear_read_ldsdma"}
         res = {v: [] for v in names}
         for _ in range(5):
             for v in names:
@@ -208,6 +209,34 @@ def main():
                          f"oracle/rsg_oracle.c orc_block_sums (scalar C restatement of generator.go:325-350), "
                          f"1 thread, {t_cpu:.1f} s",
                "gpu_parity_on_sample": sample_parity}
+        # the same restatement on T host threads, files partitioned;
+        # ctypes drops the GIL for the foreign call, so the threads run in parallel
+        import threading
+        T = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16
+        wall_s = max(2.0, args.cpu_seconds / 2)
+        counts = [0] * T
+
+        def cpu_worker(k):
+            o = np.empty(1498 * 20, np.uint8)
+            t_end = time.perf_counter() + wall_s
+            j = k
+            while time.perf_counter() < t_end:
+                d = sample_files[j % len(sample_files)]
+                lib.orc_block_sums(orc._ptr(d), d.size, BLOCK_LEN, orc._i32(SEED), orc._ptr(o))
+                counts[k] += d.size
+                j += T
+
+        w0 = time.perf_counter()
+        ths = [threading.Thread(target=cpu_worker, args=(k,)) for k in range(T)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        wdt = time.perf_counter() - w0
+        extra["cpu_baseline_all_cores"] = {
+            "value": round(sum(counts) / wdt / GIB, 4), "unit": "GiB/s", "cores": T, "kind": "port",
+            "sample": f"{sum(counts) // FILE_BYTES} x 1 MiB files on {T} threads (files partitioned), "
+                      f"same orc_block_sums, {wdt:.1f} s wall"}
 
     if rank == 0:
         traffic = None

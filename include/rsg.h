@@ -189,6 +189,27 @@ rsg_status rsg_encode_tokens(const uint8_t *src, uint64_t src_len, const rsg_sum
                              const rsg_match *matches, uint64_t n_matches, uint8_t *out,
                              uint64_t out_cap, uint64_t *out_len);
 
+/* ------------------------------------------ whole-file sums
+ * MD4 of whole files, one GPU lane per file (MD4 is serial within a message,
+ * so this pays off for many files per call, e.g. a --checksum file list):
+ *   RSG_FILESUM_PLAIN  = MD4(file): rsyncchecksum.ReaderChecksum
+ *                        (rsyncchecksum.go:60-66), called per file by the
+ *                        sender's file list (sender/flist.go:276-293) and the
+ *                        receiver's quick check (receiver/generator.go:82-88);
+ *   RSG_FILESUM_SEEDED = MD4(int32_LE(seed) || file): the transfer's whole-file
+ *                        sum, seeded before the data (match.go:52-53,
+ *                        sender.go:184-206, receiver.go:117-120).
+ * out receives nfiles * 16 bytes, digest i at out + 16 i. */
+#define RSG_FILESUM_PLAIN 0
+#define RSG_FILESUM_SEEDED 1
+/* files[i].data / len (offset and block_len ignored). */
+rsg_status rsg_file_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, int32_t mode,
+                              int32_t seed, uint8_t *out);
+/* files[i].offset / len inside the device arena; d_out on the device. */
+rsg_status rsg_file_sums_device(rsg_ctx *ctx, const void *d_arena, uint64_t arena_bytes,
+                                const rsg_file *files, uint64_t nfiles, int32_t mode, int32_t seed,
+                                void *d_out);
+
 /* ------------------------------------------ multi-GPU sums gather
  * Files shard across the GPUs of one node with no data-path collective; the
  * only exchange is the final gather of each rank's records to the root over

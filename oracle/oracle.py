@@ -43,6 +43,8 @@ def lib():
         L.orc_tag.restype = ctypes.c_uint16
         L.orc_md4.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
         L.orc_checksum2.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        L.orc_file_sum.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_uint64,
+                                   ctypes.c_void_p]
         L.orc_sum_sizes_sqroot.argtypes = [ctypes.c_int64, ctypes.c_void_p]
         L.orc_block_sums.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
                                      ctypes.c_void_p]
@@ -102,6 +104,15 @@ def checksum2(seed: int, buf) -> bytes:
     a = _as_u8(buf)
     out = np.zeros(16, dtype=np.uint8)
     lib().orc_checksum2(ctypes.c_int32(_i32(seed)), _ptr(a), a.size, _ptr(out))
+    return out.tobytes()
+
+
+def file_sum(mode: int, seed: int, buf) -> bytes:
+    """Whole-file MD4: mode 0 = MD4(file) (rsyncchecksum.go:60-66), mode 1 =
+    MD4(int32_LE(seed) || file) (match.go:52-53, receiver.go:117-120)."""
+    a = _as_u8(buf)
+    out = np.zeros(16, dtype=np.uint8)
+    lib().orc_file_sum(ctypes.c_int32(mode), ctypes.c_int32(_i32(seed)), _ptr(a), a.size, _ptr(out))
     return out.tobytes()
 
 

@@ -177,6 +177,27 @@ void orc_checksum2(int32_t seed, const uint8_t *buf, uint64_t n, uint8_t out[16]
     md4_final(&c, out);
 }
 
+/* Whole-file sums.
+ * mode 0: MD4(file)                  rsyncchecksum.ReaderChecksum, rsyncchecksum.go:60-66
+ *                                    (the --checksum file-list sums, sender/flist.go:276-293,
+ *                                    receiver/generator.go:82-88)
+ * mode 1: MD4(int32_LE(seed) || file) the transfer's whole-file sum: h = md4.New();
+ *                                    binary.Write(h, seed) before any data (match.go:52-53,
+ *                                    sender.go:184-206, receiver.go:117-120)
+ * The seed is PREPENDED here, unlike Checksum2 where it is appended. */
+void orc_file_sum(int32_t mode, int32_t seed, const uint8_t *buf, uint64_t n, uint8_t out[16]) {
+    md4_ctx c;
+    md4_init(&c);
+    if (mode == 1) {
+        uint8_t s[4];
+        uint32_t u = (uint32_t)seed;
+        s[0] = (uint8_t)u; s[1] = (uint8_t)(u >> 8); s[2] = (uint8_t)(u >> 16); s[3] = (uint8_t)(u >> 24);
+        md4_update(&c, s, 4);
+    }
+    md4_update(&c, buf, n);
+    md4_final(&c, out);
+}
+
 /* ------------------------------------------------------------------------- */
 /* Block sizing: rsynccommon.SumSizesSqroot, internal/rsynccommon/rsynccommon.go:14-37 */
 /* out = {ChecksumCount, BlockLength, ChecksumLength, RemainderLength}        */

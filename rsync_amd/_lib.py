@@ -19,6 +19,8 @@ if not os.path.exists(LIB_PATH):
 lib = ctypes.CDLL(LIB_PATH)
 
 RECORD_BYTES = 20
+FILESUM_PLAIN = 0   # MD4(file), rsyncchecksum.go:60-66
+FILESUM_SEEDED = 1  # MD4(int32_LE(seed) || file), match.go:52-53
 CHUNK_SIZE = 256 * 1024
 ABI_VERSION = 1
 
@@ -87,6 +89,8 @@ _PROTOS = {
                                      ctypes.POINTER(Match), _u64, ctypes.POINTER(_u64)]),
     "rsg_encode_tokens": (_st, [_vp, _u64, ctypes.POINTER(SumHead), ctypes.POINTER(Match), _u64,
                                 _vp, _u64, ctypes.POINTER(_u64)]),
+    "rsg_file_sums_host": (_st, [_vp, ctypes.POINTER(File), _u64, _i32, _i32, _vp]),
+    "rsg_file_sums_device": (_st, [_vp, _vp, _u64, ctypes.POINTER(File), _u64, _i32, _i32, _vp]),
     "rsg_comm_unique_id": (_st, [_vp]),
     "rsg_comm_init": (_st, [_vp, _i32, _i32, _vp]),
     "rsg_gather_bytes": (_st, [_vp, _vp, ctypes.POINTER(_u64), _vp, _i32, _vp]),

@@ -8,7 +8,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <new>
+#include <thread>
 
 #include "rsg_host.h"
 
@@ -145,6 +147,37 @@ rsg_status launch_plan(rsg_ctx *ctx, const HostPlan &plan, const void *d_files, 
                                         plan.max_blen, (uint32_t)seed, (uint8_t *)d_records,
                                         (uint32_t *)d_scratch, stream));
     return RSG_OK;
+}
+
+void parallel_copy(const std::vector<CopyJob> &jobs) {
+    const uint64_t kPiece = 2ull << 20;
+    std::vector<CopyJob> pieces;
+    uint64_t total = 0;
+    for (const CopyJob &j : jobs) {
+        for (uint64_t o = 0; o < j.n; o += kPiece) {
+            const uint64_t n = std::min(kPiece, j.n - o);
+            pieces.push_back({(uint8_t *)j.dst + o, (const uint8_t *)j.src + o, n});
+        }
+        total += j.n;
+    }
+    static const int threads = [] {
+        const char *e = getenv("RSG_COPY_THREADS");
+        const int t = e ? atoi(e) : 8;
+        return std::max(1, std::min(t, 64));
+    }();
+    const int nt = (int)std::min<uint64_t>((uint64_t)threads, std::max<uint64_t>(1, total / (4ull << 20)));
+    if (nt <= 1) {
+        for (const CopyJob &p : pieces) memcpy(p.dst, p.src, p.n);
+        return;
+    }
+    std::atomic<size_t> next{0};
+    auto worker = [&] {
+        for (size_t k; (k = next.fetch_add(1)) < pieces.size();) memcpy(pieces[k].dst, pieces[k].src, pieces[k].n);
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; t++) pool.emplace_back(worker);
+    worker();
+    for (auto &t : pool) t.join();
 }
 
 }  // namespace rsgh
@@ -375,8 +408,8 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
 }
 
 rsg_status rsg_set_block_sums_kernel(int32_t variant) {
-    if (variant < -1 || (variant > 7 && variant < 10) || variant > 22)
-        return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..7 or 10..22");
+    if (variant < -1 || variant > 23)
+        return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..23");
     rsg::set_block_sums_variant(variant);
     return RSG_OK;
 }
@@ -487,19 +520,21 @@ rsg_status rsg_block_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfi
         if ((s = drain(slot)) != RSG_OK) return s;
         // stage pieces as virtual files in the pinned arena
         std::vector<rsg_file> vf(b.pieces.size());
+        std::vector<CopyJob> copies(b.pieces.size());
         uint8_t *stage = (uint8_t *)ctx->h_in[slot].p;
         uint64_t off = 0;
         for (size_t j = 0; j < b.pieces.size(); j++) {
             const Piece &pc = b.pieces[j];
             const uint64_t B = (uint64_t)heads[pc.file].block_len;
             const uint64_t start = pc.b0 * B, end = std::min<uint64_t>(pc.b1 * B, files[pc.file].len);
-            memcpy(stage + off, files[pc.file].data + start, end - start);
+            copies[j] = {stage + off, files[pc.file].data + start, end - start};
             vf[j].data = nullptr;
             vf[j].offset = off;
             vf[j].len = end - start;
             vf[j].block_len = (int32_t)B;
             off += ((end - start) + 15) & ~15ull;
         }
+        parallel_copy(copies);
         HostPlan plan;
         if ((s = build_plan(ctx, vf.data(), vf.size(), off, true, plan)) != RSG_OK) return s;
         uint8_t *hd = (uint8_t *)ctx->h_desc[slot].p;

@@ -601,7 +601,7 @@ constexpr uint32_t kLrLoads = 8;                     // load instructions per li
 // SHARE, lane j copies that line out of lane j+1's slot right after step 0's
 // store into 32 VGPRs and writes it into its own slot when its stream reaches
 // it, so the line is requested once.
-template <int MODE, bool SHARE = false>
+template <int MODE, bool SHARE = false, int DEPTH = 2>
 __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
@@ -698,10 +698,11 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
     int32_t s1 = 0;
     uint32_t tw = 0;
     auto step = [&](uint32_t i, uint32_t sa) {  // chunks 2i, 2i+1; line i in slot sa
-        // opaque slot index: the 64 per-word addresses are recomputed each
-        // step (one select per word) instead of being held in 64 VGPRs
+        // DEPTH 3 makes the slot index opaque: the 64 per-word addresses are
+        // recomputed each step (one select per word) instead of being held in
+        // 64 VGPRs, which the third line buffer needs
         uint32_t so = sa;
-        asm volatile("" : "+s"(so));
+        if (DEPTH == 3 || SHARE) asm volatile("" : "+s"(so));
         const uint8_t *pA = mine + so * kRingSlot;
         const uint8_t *pB = mine + (so ^ 1u) * kRingSlot - 128;
         uint32_t X[32];
@@ -724,38 +725,40 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
             }
         };
     };
-    u32x4v bufA[kLrLoads], bufB[kLrLoads];
+    // DEPTH line steps in flight in VGPR buffers; buffer (t % DEPTH) carries line t.
+    u32x4v buf[DEPTH][kLrLoads];
 #pragma unroll
-    for (uint32_t q = 0; q < kLrLoads; q++) bufA[q] = bufB[q] = (u32x4v){0u, 0u, 0u, 0u};
-    load_line(0, bufA);
-    load_line(1, bufB);
-    store_line(0, bufA);
+    for (int b = 0; b < DEPTH; b++)
+#pragma unroll
+        for (uint32_t q = 0; q < kLrLoads; q++) buf[b][q] = (u32x4v){0u, 0u, 0u, 0u};
+    load_line(0, buf[0]);
+    load_line(1, buf[1]);
+    store_line(0, buf[0]);
     fetch_tail();
     put_tail(0, 0);
-    store_line(1, bufB);
+    store_line(1, buf[1]);
     put_tail(1, 1);
-    // The scheduler must not interleave these two groups: the loop below
-    // relies on line 2's loads being older than line 3's (vmcnt is in order).
-    load_line(2, bufA);
-    __builtin_amdgcn_sched_barrier(0);
-    load_line(3, bufB);
-    __builtin_amdgcn_sched_barrier(0);
-    // Two steps per trip (the slots and buffers alternate); an odd T runs one
-    // extra step whose chunks are past every block (it hashes nothing).
+    // The scheduler must not interleave these groups: the loop relies on the
+    // loads of line t being older than those of line t+1 (vmcnt is in order).
+#pragma unroll
+    for (uint32_t t = 2; t < 2 + DEPTH; t++) {
+        load_line(t, buf[t % DEPTH]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // U steps per trip (slots alternate, buffers rotate); the trip may run
+    // past T by a step (DEPTH 2: its chunks are past every block, it hashes
+    // nothing); with DEPTH 3 the steps past T are skipped.
+    constexpr uint32_t U = DEPTH == 3 ? 6 : 2;
 #pragma unroll 1
-    for (uint32_t i = 0; i < T; i += 2) {
-        {
-            auto hash = step(i, 0);  // lines i (slot 0), i+1 (slot 1)
-            store_line(0, bufA);     // line i+2 -> slot 0
-            put_tail(i + 2, 0);
-            load_line(i + 4, bufA);
-            hash();
-        }
-        {
-            auto hash = step(i + 1, 1);  // lines i+1 (slot 1), i+2 (slot 0)
-            store_line(1, bufB);         // line i+3 -> slot 1
-            put_tail(i + 3, 1);
-            load_line(i + 5, bufB);
+    for (uint32_t i0 = 0; i0 < T; i0 += U) {
+#pragma unroll
+        for (uint32_t st = 0; st < U; st++) {
+            const uint32_t i = i0 + st;
+            if (DEPTH == 3 && st > 0 && i >= T) break;
+            auto hash = step(i, st & 1u);              // lines i (slot st&1), i+1 (other slot)
+            store_line(st & 1u, buf[(st + 2) % DEPTH]);  // line i+2 -> slot st&1
+            put_tail(i + 2, st & 1u);
+            load_line(i + 2 + DEPTH, buf[(st + 2) % DEPTH]);
             hash();
         }
     }
@@ -1074,6 +1077,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 21: RSG_LAUNCH(block_sums_lring<2>, grid); break;
         case 7: RSG_LAUNCH((block_sums_lring<0, true>), grid); break;
         case 22: RSG_LAUNCH((block_sums_lring<1, true>), grid); break;
+        case 8: RSG_LAUNCH((block_sums_lring<0, false, 3>), grid); break;
+        case 9: RSG_LAUNCH((block_sums_lring<0, true, 3>), grid); break;
+        case 23: RSG_LAUNCH((block_sums_lring<1, false, 3>), grid); break;
         case 19: RSG_LAUNCH(block_sums_ring<2>, grid); break;
         case 10: RSG_STAGED(1, 1); break;
         case 11: RSG_STAGED(1, 2); break;

@@ -77,6 +77,17 @@ bool head_for(int64_t len, int32_t block_len, rsg_sum_head *out);
 rsg_status build_plan(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, uint64_t arena_bytes,
                       bool use_offsets, HostPlan &plan);
 
+// Host memcpy of many (dst, src, n) jobs on a few threads (staging files into
+// pinned memory is the host path's limiter on one core).  Jobs are cut into
+// pieces of at most 2 MiB and handed out dynamically; small totals stay on
+// the calling thread.  Threads: RSG_COPY_THREADS, default 8.
+struct CopyJob {
+    void *dst;
+    const void *src;
+    uint64_t n;
+};
+void parallel_copy(const std::vector<CopyJob> &jobs);
+
 // Upload plan descriptors to (grown) device buffers and launch the kernel.
 rsg_status launch_plan(rsg_ctx *ctx, const HostPlan &plan, const void *d_files, const void *d_wg,
                        const void *d_arena, int32_t seed, void *d_records, void *d_scratch, hipStream_t stream);

@@ -62,6 +62,16 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                        const uint32_t *bitmap, const uint64_t *table, uint32_t bmask, uint64_t *cand,
                        uint32_t cap, uint32_t *count, uint32_t grid, hipStream_t stream);
 
+// ---- whole-file sums (rsg_filesums.hip)
+struct FileSpan {
+    uint64_t offset;  // byte offset of the file in the arena
+    uint64_t len;
+};
+// out[16 * i] = MD4 of file i: mode 0 MD4(file), mode 1 MD4(int32_LE(seed) || file).
+// order = a permutation of the files (lane k hashes file order[k]).
+hipError_t launch_file_sums(const uint8_t *arena, uint64_t arena_bytes, const FileSpan *files, const uint32_t *order,
+                            uint32_t nfiles, uint32_t mode, uint32_t seed, uint8_t *out, hipStream_t stream);
+
 hipError_t launch_fill_splitmix64(uint8_t *dst, uint64_t n, uint64_t seed, hipStream_t stream);
 
 }  // namespace rsg

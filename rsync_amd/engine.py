@@ -233,6 +233,38 @@ class Engine:
         conn.write(rec)
         return h
 
+    # ------------------------------------------------------------ whole-file sums
+    def file_sums(self, files: Sequence, mode: int = _lib.FILESUM_PLAIN, seed: int = 0) -> List[bytes]:
+        """Whole-file MD4 of each host buffer, one GPU lane per file:
+        FILESUM_PLAIN = rsyncchecksum.ReaderChecksum (rsyncchecksum.go:60-66),
+        FILESUM_SEEDED = the transfer's MD4(int32_LE(seed) || file)
+        (match.go:52-53, receiver.go:117-120)."""
+        n = len(files)
+        if n == 0:
+            return []
+        arrs = [_u8(f) for f in files]
+        desc = (File * n)()
+        for i, a in enumerate(arrs):
+            desc[i].data = a.ctypes.data if a.size else None
+            desc[i].len = a.size
+        out = np.empty(16 * n, dtype=np.uint8)
+        check(lib.rsg_file_sums_host(self.ctx, desc, n, mode, _i32(seed), _ptr(out)), self.ctx)
+        return [out[16 * i: 16 * i + 16].tobytes() for i in range(n)]
+
+    def file_sums_device(self, arena: DeviceBuffer, files: Sequence[Tuple[int, int]], mode: int = _lib.FILESUM_PLAIN,
+                         seed: int = 0, out: Optional[DeviceBuffer] = None) -> DeviceBuffer:
+        """Same for files already in device memory: files = [(offset, len)];
+        returns a device buffer of len(files) * 16 digest bytes."""
+        n = len(files)
+        desc = (File * max(n, 1))()
+        for i, (off, ln) in enumerate(files):
+            desc[i].offset, desc[i].len = off, ln
+        if out is None:
+            out = self.alloc(max(n, 1) * 16)
+        check(lib.rsg_file_sums_device(self.ctx, ctypes.c_void_p(arena.ptr), arena.nbytes, desc, n, mode, _i32(seed),
+                                       ctypes.c_void_p(out.ptr)), self.ctx)
+        return out
+
     # ------------------------------------------------------------ sender
     def hash_search(self, src, head, sum1, sum2, targets, seed: int) -> List[Tuple[int, int]]:
         """(*sender.Transfer).hashSearch (match.go:21-230): the greedy match
@@ -318,7 +350,13 @@ def checksum1(buf) -> int:
 def checksum2(seed: int, buf) -> bytes:
     """rsyncchecksum.Checksum2 = MD4(buf || int32_LE(seed)), computed on the GPU."""
     a = _u8(buf)
-    if a.size == 0:
-        raise RsgError(_lib.ERR_INVALID, "checksum2 of an empty buffer: the block kernel needs >= 1 byte")
+    if a.size == 0:  # MD4(seed_LE): the whole-file kernel's seeded form of an empty file
+        return default_engine().file_sums([a], _lib.FILESUM_SEEDED, seed)[0]
     _, rec, _ = default_engine().block_sums([a], seed, a.size)
     return rec[4:20]
+
+
+def reader_checksum(buf) -> bytes:
+    """rsyncchecksum.ReaderChecksum (rsyncchecksum.go:60-66): MD4 of the whole
+    buffer, on the GPU."""
+    return default_engine().file_sums([_u8(buf)], _lib.FILESUM_PLAIN)[0]

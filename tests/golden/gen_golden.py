@@ -181,6 +181,20 @@ def gen_match():
     return res
 
 
+def gen_file_sums():
+    """Whole-file sums: MD4(file) and MD4(int32_LE(seed) || file), by OpenSSL."""
+    data = cases.splitmix64_bytes(11, 300_001)
+    out = []
+    for n in [0, 1, 3, 4, 5, 55, 56, 59, 60, 61, 63, 64, 65, 119, 120, 123, 124, 127, 128, 700, 4096,
+              65_537, 300_001]:
+        m = data[:n].tobytes()
+        e = {"len": n, "plain": ssl_md4(m).hex(), "seeded": {}}
+        for seed in [cases.SEED, 0, -1]:
+            e["seeded"][str(seed)] = ssl_md4(struct.pack("<i", seed) + m).hex()
+        out.append(e)
+    return {"data": "splitmix64(seed=11)", "cases": out}
+
+
 def main():
     w = lambda name, obj: json.dump(obj, open(os.path.join(HERE, name), "w"), indent=1)
     w("md4_vectors.json", gen_md4())
@@ -191,6 +205,8 @@ def main():
     print("block sums ok")
     w("match_cases.json", gen_match())
     print("match ok")
+    w("file_sums.json", gen_file_sums())
+    print("file sums ok")
 
 
 if __name__ == "__main__":

@@ -39,6 +39,18 @@ def test_checksum2_edge_lengths():
     assert orc.checksum2(g["spot"]["seed"], spot).hex() == g["spot"]["sum2"]
 
 
+def test_file_sums_golden():
+    """Whole-file sums (rsyncchecksum.go:60-66 plain; match.go:52-53 /
+    receiver.go:117-120 seed-prefixed) against OpenSSL MD4 fixtures."""
+    g = load("file_sums.json")
+    data = cases.splitmix64_bytes(11, 300_001)
+    for c in g["cases"]:
+        m = data[: c["len"]]
+        assert orc.file_sum(0, 0, m).hex() == c["plain"], c["len"]
+        for seed, want in c["seeded"].items():
+            assert orc.file_sum(1, int(seed), m).hex() == want, (c["len"], seed)
+
+
 def test_weak_kat_reference():
     """internal/rsyncchecksum/checksum_test.go:32-73: all 1780 values."""
     g = load("weak_kat.json")
