@@ -122,8 +122,8 @@ def main():
     extra = {}
     if args.ab:
         from rsync_amd import _lib
-        names = {1: "staged_k1", 6: "lring", 8: "lring_depth3", 9: "lring_share_depth3",
-                 10: "diag_staged_memory_only", 20: "diag_lring_memory_only", 21: "diag_lring_loads_only",
+        names = {1: "staged_k1", 5: "line_ring", 6: "line_ring_shared", 4: "regtile",
+                 10: "diag_staged_memory_only", 18: "diag_line_ring_memory_only", 15: "diag_staged_line_aligned_memory",
                  11: "diag_staged_hash_only", 13: "diag_linear_read", 14: "diag_linear_read_ldsdma"}
         res = {v: [] for v in names}
         for _ in range(5):

@@ -140,11 +140,15 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
                                   int32_t seed, void *d_records, void *stream);
 
 /* Tuning knob (process-wide): block-sum kernel variant.  -1 = automatic
- * (default), 0 = direct per-lane loads, 1 = staged LDS-DMA slabs, 2 = staged
- * with 4 blocks per lane, 3 = whole block in registers (blocks <= 703 bytes).
- * These give identical results; only speed differs.  10..12 are timing
- * diagnostics whose outputs are meaningless (memory-only / hashing-only).
- * Unaligned batches always use variant 0. */
+ * (default: 1), 0 = direct per-lane loads, 1 = staged LDS-DMA slabs, 2 = staged
+ * with 4 blocks per lane, 3 = whole block in registers (blocks <= 703 bytes),
+ * 4 = register tiles (blocks <= 703 bytes), 5 = aligned line ring (each line
+ * loaded once, realigned through LDS), 6 = line ring with each block's last
+ * line taken from the next lane.  These give identical results; only speed
+ * differs.  10..18 are timing diagnostics whose outputs are meaningless
+ * (memory-only / hashing-only / plain reads).  Unaligned batches always use
+ * variant 0.  The environment variable RSG_BLOCKSUMS_KERNEL sets the initial
+ * value. */
 rsg_status rsg_set_block_sums_kernel(int32_t variant);
 
 /* One-shot device call: plan + launch + wait. */

@@ -262,25 +262,24 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 // is an L2 hit, whereas across lanes they are a whole block apart and the line
 // is often refetched from HBM.  K = 4 cuts those refetches by 4x.
 template <int K, int MODE>
-__global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
-    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
-    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
-    uint8_t *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * kWaveSlab];
+__device__ __forceinline__ void staged_tile(
+    uint32_t tile, uint8_t *slab_all, const uint8_t *__restrict__ arena, uint64_t arena_bytes,
+    const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file, uint32_t nwg256,
+    uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
     const uint32_t lane = threadIdx.x & 63u;
     // readfirstlane: provably wave-uniform values keep the LDS base (M0) and
     // the buffer descriptor in SGPRs (no waterfall loops around the DMA).
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint8_t *slab = slab_all + wave * kWaveSlab;
-    const uint64_t wave_first = ((uint64_t)blockIdx.x * (kBlockSumThreads / 64) + wave) * 64u * K;
+    const uint64_t wave_first = ((uint64_t)tile * (kBlockSumThreads / 64) + wave) * 64u * K;
     const uint64_t g0 = wave_first + (uint64_t)lane * K;
 
     // Locate the lane's K blocks: binary search for the first, then walk.
     uint64_t off[K];
     uint32_t n[K];
     {
-        uint32_t lo = wg_file[blockIdx.x * K];
-        uint32_t hi = wg_file[min((blockIdx.x + 1) * K, nwg256)];
+        uint32_t lo = wg_file[tile * K];
+        uint32_t hi = wg_file[min((tile + 1) * K, nwg256)];
         const uint64_t gq = g0 < total_blocks ? g0 : total_blocks - 1;
         while (lo < hi) {
             const uint32_t mid = (lo + hi + 1) >> 1;
@@ -438,145 +437,21 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     }
 }
 
-// ---------------------------------------------------------------- line-ring variant
-// Every 128-byte line a wave needs is requested from L2 exactly once.  The
-// staged variant above fetches each lane's 256-byte windows at the block's own
-// (unaligned) offsets, so a window touches 3 lines and the line it shares with
-// the next window is requested again one window later -- by then often
-// evicted from L2, so ~25 % of the HBM traffic is refetch (profiles/).  Here
-// the DMA moves whole aligned lines: lane j's stream is the lines
-// l_j, l_j+1, ... that hold its block (l_j = its first line), fetched one line
-// per step into a 4-slot ring in LDS:
-//     ring[slot][lane] = 128-byte line + 16-byte pad (bank spread)
-// so one 1 KiB DMA instruction carries the same line step of 8 lanes and a
-// line step is 9 instructions (the pad unit is out of range: no request).
-// Step i hashes chunks 2i, 2i+1 = block bytes [128 i, 128 i + 128), which
-// start d_j = (block offset mod 128) bytes into line i and end in line i+1;
-// each lane reads its 32 words from the two slots (the split point is per
-// lane and constant, so the choice of base is a per-word select).  Lines
-// i+2, i+3 are in flight while step i hashes.  4 waves x 36 KiB of LDS per
-// CU: one wave per SIMD.
-constexpr uint32_t kRingSlots = 4;
+
+template <int K, int MODE>
+__global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * kWaveSlab];
+    staged_tile<K, MODE>(blockIdx.x, slab_all, arena, arena_bytes, files, wg_file, nwg256, total_blocks, seed, out);
+}
+
+// ---------------------------------------------------------------- line-ring layout
+// A line step of a wave in LDS: 64 lanes x (128-byte line + 16-byte pad); the
+// pad spreads the lanes' realigned reads over the banks.
 constexpr uint32_t kRingLane = 144;                    // 128-byte line + 16-byte pad
 constexpr uint32_t kRingSlot = 64 * kRingLane;         // 9216 B: one line step of the wave
-constexpr uint32_t kRingDma = kRingSlot / 1024;        // 9 DMA instructions per line step
-constexpr uint32_t kRingWave = kRingSlots * kRingSlot; // 36864 B per wave
-static_assert(kRingSlot % 1024 == 0, "a line step must be whole DMA instructions");
-
-__device__ __forceinline__ void lds_read_b32(uint32_t &v, uint32_t addr, int off) {
-    // Not visible to the compiler as an LDS access, so it does not serialise
-    // it behind every pending LDS-DMA (the caller waits for exactly the lines
-    // it reads with vmcnt and drains lgkmcnt itself).
-    asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
-}
-
-// MODE 0 = product.  Timing diagnostics (outputs meaningless): 1 = DMA + LDS
-// reads only, 2 = LDS reads + hashing only (no DMA).
-template <int MODE>
-__global__ __launch_bounds__(kBlockSumThreads) void block_sums_ring(
-    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
-    const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
-    // 128-byte guard in front: a lane's line-(i+1) base is formed 128 bytes
-    // below its slot (see pB), which must not wrap below LDS address 0.
-    __shared__ __attribute__((aligned(16))) uint8_t ring_all[128 + (kBlockSumThreads / 64) * kRingWave];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t wave_first = (uint64_t)blockIdx.x * kBlockSumThreads + wave * 64u;
-    const uint64_t g = wave_first + lane;
-    uint64_t off = 0;
-    uint32_t n = 0;
-    locate_block(files, wg_file, g < total_blocks ? g : total_blocks - 1, off, n);
-
-    // Wave-uniform path choice: all 64 blocks present and the wave's lines
-    // addressable by a 32-bit buffer offset; otherwise per-lane loads.
-    const uintptr_t abs = (uintptr_t)(arena + off);
-    const uint64_t lo = wave_min_u64(abs);
-    const uint64_t hi = wave_max_u64(abs + n);
-    const uint64_t base = (((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo >> 32)) << 32) |
-                           __builtin_amdgcn_readfirstlane((uint32_t)lo)) & ~127ull;
-    if (!(wave_first + 63 < total_blocks) || hi - base > 0x7FFFFF00ull) {
-        if (g >= total_blocks) return;
-        uint32_t h[4];
-        md4_init(h);
-        int32_t s1 = 0;
-        uint32_t t = 0;
-        hash_block_direct<true>(arena, (uintptr_t)(arena + arena_bytes), off, n, seed, h, s1, t);
-        store_record(out, g, n, s1, t, h);
-        return;
-    }
-    // Bytes past the arena's end (the last line may overhang it) read as 0.
-    const uint64_t avail = (uint64_t)(uintptr_t)(arena + arena_bytes) - base;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)base, (short)0, (int)(avail < 0x7FFFFFFFull ? avail : 0x7FFFFFFFull), 0x00020000);
-    const uint32_t rel = (uint32_t)(abs - base);
-    const uint32_t d = rel & 127u;                   // block start within its first line
-    const uint32_t nl = (d + n + 127u) >> 7;         // lines holding the block
-    const uint32_t nfull = n >> 6;
-    const uint32_t steps = (nfull + 2u) >> 1;        // chunk pairs through the tail chunk
-    const uint32_t T = __builtin_amdgcn_readfirstlane((uint32_t)wave_max_u64(steps));
-    const uint32_t NL = __builtin_amdgcn_readfirstlane((uint32_t)wave_max_u64(nl));
-
-    // DMA instruction q, lane t fills slot bytes [16 (64 q + t), +16): lane
-    // j = (64 q + t) / 9's line, unit u = (64 q + t) % 9 (u == 8: pad).
-    uint32_t voff[kRingDma], vnl[kRingDma];
-#pragma unroll
-    for (uint32_t q = 0; q < kRingDma; q++) {
-        const uint32_t idx = 64u * q + lane;
-        const uint32_t j = idx / 9u, u = idx - 9u * j;
-        // shuffles outside the select: every lane must take part as a source
-        const uint32_t lj = __shfl(rel & ~127u, (int)j, 64);
-        const uint32_t nj = __shfl(nl, (int)j, 64);
-        voff[q] = u < 8u ? lj + 16u * u : 0x80000000u;
-        vnl[q] = u < 8u ? nj : 0u;
-    }
-    uint8_t *ring = ring_all + 128 + wave * kRingWave;
-    const uint32_t ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t *)ring;
-    auto fetch_line = [&](uint32_t t) {  // line step t of every lane -> slot t % 4
-        uint8_t *dst = ring + (t & (kRingSlots - 1)) * kRingSlot;
-#pragma unroll
-        for (uint32_t q = 0; q < kRingDma; q++)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * q),
-                                                     16, t < vnl[q] ? voff[q] : 0x80000000u, 128u * t, 0, 0);
-    };
-    const uint32_t lane_lds = ring_lds + lane * kRingLane + d;
-    const uint32_t split = (128u - d) >> 2;  // words 0..split-1 come from line i, the rest from line i+1
-
-    uint32_t h[4];
-    md4_init(h);
-    int32_t s1 = 0;
-    uint32_t tw = 0;
-    if (MODE != 2) {
-        fetch_line(0);
-        if (1 < NL) fetch_line(1);
-        if (2 < NL) fetch_line(2);
-    }
-#pragma unroll 1
-    for (uint32_t i = 0; i < T; i++) {
-        if (MODE != 2) {
-            if (i + 2 < NL) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        const uint32_t pA = lane_lds + (i & (kRingSlots - 1)) * kRingSlot;
-        const uint32_t pB = lane_lds + ((i + 1) & (kRingSlots - 1)) * kRingSlot - 128u;
-        uint32_t X[32];
-#pragma unroll
-        for (uint32_t k = 0; k < 32; k++) lds_read_b32(X[k], k < split ? pA : pB, (int)(4 * k));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (MODE != 2 && i + 3 < NL) fetch_line(i + 3);
-        if (MODE == 1) {
-#pragma unroll
-            for (int k = 0; k < 32; k++) h[k & 3] ^= X[k];
-        } else {
-#pragma unroll
-            for (uint32_t c2 = 0; c2 < 2; c2++) {
-                const uint32_t c = 2u * i + c2;
-                if (c < nfull) hash_chunk<true>(X + 16 * c2, 0u, 0u, c, h, s1, tw);
-                else if (c == nfull) hash_tail<true>(X + 16 * c2, 0u, 0u, n, seed, h, s1, tw);
-            }
-        }
-    }
-    store_record(out, g, n, s1, tw, h);
-}
 
 // ---------------------------------------------------------------- loaded-line-ring variant
 // Same line stream as the ring above (every line requested once, whole
@@ -601,7 +476,7 @@ constexpr uint32_t kLrLoads = 8;                     // load instructions per li
 // SHARE, lane j copies that line out of lane j+1's slot right after step 0's
 // store into 32 VGPRs and writes it into its own slot when its stream reaches
 // it, so the line is requested once.
-template <int MODE, bool SHARE = false, int DEPTH = 2>
+template <int MODE, bool SHARE = false>
 __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
@@ -667,13 +542,10 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
         for (uint32_t q = 0; q < kLrLoads; q++)
             buf[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, t < vnl[q] ? voff[q] : 0x80000000u, 128u * t, 0);
     };
-    uint32_t sink = 0;
     auto store_line = [&](uint32_t slot, const u32x4v buf[kLrLoads]) {
 #pragma unroll
-        for (uint32_t q = 0; q < kLrLoads; q++) {
-            if (MODE == 2) sink ^= buf[q].x ^ buf[q].y ^ buf[q].z ^ buf[q].w;
-            else *reinterpret_cast<u32x4v *>(ring + slot * kRingSlot + wpos[q]) = buf[q];
-        }
+        for (uint32_t q = 0; q < kLrLoads; q++)
+            *reinterpret_cast<u32x4v *>(ring + slot * kRingSlot + wpos[q]) = buf[q];
     };
     u32x4v tail[SHARE ? 8 : 1];
     auto fetch_tail = [&]() {  // lane j+1's first line, now in slot 0
@@ -698,21 +570,19 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
     int32_t s1 = 0;
     uint32_t tw = 0;
     auto step = [&](uint32_t i, uint32_t sa) {  // chunks 2i, 2i+1; line i in slot sa
-        // DEPTH 3 makes the slot index opaque: the 64 per-word addresses are
+        // SHARE makes the slot index opaque: the 64 per-word addresses are
         // recomputed each step (one select per word) instead of being held in
-        // 64 VGPRs, which the third line buffer needs
+        // 64 VGPRs, which the tail line needs
         uint32_t so = sa;
-        if (DEPTH == 3 || SHARE) asm volatile("" : "+s"(so));
+        if (SHARE) asm volatile("" : "+s"(so));
         const uint8_t *pA = mine + so * kRingSlot;
         const uint8_t *pB = mine + (so ^ 1u) * kRingSlot - 128;
         uint32_t X[32];
 #pragma unroll
         for (uint32_t k = 0; k < 32; k++)
-            X[k] = MODE == 2 ? k : *reinterpret_cast<const uint32_t *>((k < split ? pA : pB) + 4 * k);
+            X[k] = *reinterpret_cast<const uint32_t *>((k < split ? pA : pB) + 4 * k);
         return [=, &h, &s1, &tw]() mutable {
-            if (MODE == 2) {
-                h[0] ^= sink;
-            } else if (MODE == 1) {
+            if (MODE == 1) {
 #pragma unroll
                 for (int k = 0; k < 32; k++) h[k & 3] ^= X[k];
             } else {
@@ -725,10 +595,10 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
             }
         };
     };
-    // DEPTH line steps in flight in VGPR buffers; buffer (t % DEPTH) carries line t.
-    u32x4v buf[DEPTH][kLrLoads];
+    // Two line steps in flight in VGPR buffers; buffer (t % 2) carries line t.
+    u32x4v buf[2][kLrLoads];
 #pragma unroll
-    for (int b = 0; b < DEPTH; b++)
+    for (int b = 0; b < 2; b++)
 #pragma unroll
         for (uint32_t q = 0; q < kLrLoads; q++) buf[b][q] = (u32x4v){0u, 0u, 0u, 0u};
     load_line(0, buf[0]);
@@ -739,26 +609,22 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_lring(
     store_line(1, buf[1]);
     put_tail(1, 1);
     // The scheduler must not interleave these groups: the loop relies on the
-    // loads of line t being older than those of line t+1 (vmcnt is in order).
-#pragma unroll
-    for (uint32_t t = 2; t < 2 + DEPTH; t++) {
-        load_line(t, buf[t % DEPTH]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    // U steps per trip (slots alternate, buffers rotate); the trip may run
-    // past T by a step (DEPTH 2: its chunks are past every block, it hashes
-    // nothing); with DEPTH 3 the steps past T are skipped.
-    constexpr uint32_t U = DEPTH == 3 ? 6 : 2;
+    // loads of line 2 being older than those of line 3 (vmcnt is in order).
+    load_line(2, buf[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    load_line(3, buf[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    // Two steps per trip (slots and buffers alternate); an odd T runs one
+    // extra step whose chunks are past every block (it hashes nothing).
 #pragma unroll 1
-    for (uint32_t i0 = 0; i0 < T; i0 += U) {
+    for (uint32_t i0 = 0; i0 < T; i0 += 2) {
 #pragma unroll
-        for (uint32_t st = 0; st < U; st++) {
+        for (uint32_t st = 0; st < 2; st++) {
             const uint32_t i = i0 + st;
-            if (DEPTH == 3 && st > 0 && i >= T) break;
-            auto hash = step(i, st & 1u);              // lines i (slot st&1), i+1 (other slot)
-            store_line(st & 1u, buf[(st + 2) % DEPTH]);  // line i+2 -> slot st&1
-            put_tail(i + 2, st & 1u);
-            load_line(i + 2 + DEPTH, buf[(st + 2) % DEPTH]);
+            auto hash = step(i, st);      // lines i (slot st), i+1 (the other slot)
+            store_line(st, buf[st]);      // line i+2 -> slot st
+            put_tail(i + 2, st);
+            load_line(i + 4, buf[st]);
             hash();
         }
     }
@@ -1020,10 +886,13 @@ __global__ __launch_bounds__(kRtThreads) void block_sums_regtile(
 }
 
 // Kernel variants (rsg_set_block_sums_kernel): -1 = automatic, 0 = direct,
-// 1 = staged K=1, 2 = staged K=4, 3 = register-block.  Timing diagnostics with
-// meaningless outputs: 10 = staged K=1 memory only, 11 = staged K=1 hashing
-// only, 12 = register-block memory only, 13/14 = linear read of the arena
-// (plain loads / LDS DMA).
+// 1 = staged K=1, 2 = staged K=4, 3 = register-block, 4 = register-tile,
+// 5 = loaded line ring, 6 = line ring with shared boundary lines.  Timing
+// diagnostics with meaningless outputs: 10 = staged K=1 memory only, 11 =
+// staged K=1 hashing only, 12 = register-block memory only, 13/14 = linear
+// read of the arena (plain loads / LDS DMA), 15 = staged with line-aligned
+// pieces (memory only), 16 = staged with packed pieces (memory only), 17 =
+// register-tile memory only, 18 = line ring memory only.
 static int g_variant = -2;  // -2 = not yet read from RSG_BLOCKSUMS_KERNEL
 
 hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const DevFile *files,
@@ -1070,17 +939,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                                wg_file, nwg, total_blocks, seed, out, (const uint32_t *)scratch);
             break;
         }
-        case 5: RSG_LAUNCH(block_sums_ring<0>, grid); break;
-        case 18: RSG_LAUNCH(block_sums_ring<1>, grid); break;
-        case 6: RSG_LAUNCH(block_sums_lring<0>, grid); break;
-        case 20: RSG_LAUNCH(block_sums_lring<1>, grid); break;
-        case 21: RSG_LAUNCH(block_sums_lring<2>, grid); break;
-        case 7: RSG_LAUNCH((block_sums_lring<0, true>), grid); break;
-        case 22: RSG_LAUNCH((block_sums_lring<1, true>), grid); break;
-        case 8: RSG_LAUNCH((block_sums_lring<0, false, 3>), grid); break;
-        case 9: RSG_LAUNCH((block_sums_lring<0, true, 3>), grid); break;
-        case 23: RSG_LAUNCH((block_sums_lring<1, false, 3>), grid); break;
-        case 19: RSG_LAUNCH(block_sums_ring<2>, grid); break;
+        case 5: RSG_LAUNCH(block_sums_lring<0>, grid); break;
+        case 6: RSG_LAUNCH((block_sums_lring<0, true>), grid); break;
+        case 18: RSG_LAUNCH(block_sums_lring<1>, grid); break;
         case 10: RSG_STAGED(1, 1); break;
         case 11: RSG_STAGED(1, 2); break;
         case 15: RSG_STAGED(1, 3); break;
