@@ -122,8 +122,8 @@ def main():
     extra = {}
     if args.ab:
         from rsync_amd import _lib
-        names = {1: "staged_k1", 5: "line_ring", 6: "line_ring_shared", 4: "regtile",
-                 10: "diag_staged_memory_only", 18: "diag_line_ring_memory_only", 15: "diag_staged_line_aligned_memory",
+        names = {1: "staged_k1", 7: "staged_k1_trim", 2: "staged_k4", 8: "staged_k4_trim", 19: "diag_staged_trim_memory_only",
+                 10: "diag_staged_memory_only", 15: "diag_staged_line_aligned_memory",
                  11: "diag_staged_hash_only", 13: "diag_linear_read", 14: "diag_linear_read_ldsdma"}
         res = {v: [] for v in names}
         for _ in range(5):

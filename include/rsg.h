@@ -50,6 +50,7 @@ typedef int32_t rsg_status;
 #define RSG_ERR_HIP (-3)       /* HIP runtime error, see rsg_last_error      */
 #define RSG_ERR_NODEV (-4)     /* no gfx950 device at that ordinal           */
 #define RSG_ERR_TRUNCATED (-5) /* output capacity too small; size reported   */
+#define RSG_ERR_CORRUPT (-6)   /* whole-file sum mismatch (receiver.go:171)  */
 
 typedef struct rsg_ctx rsg_ctx;
 typedef struct rsg_plan rsg_plan;
@@ -144,8 +145,9 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
  * with 4 blocks per lane, 3 = whole block in registers (blocks <= 703 bytes),
  * 4 = register tiles (blocks <= 703 bytes), 5 = aligned line ring (each line
  * loaded once, realigned through LDS), 6 = line ring with each block's last
- * line taken from the next lane.  These give identical results; only speed
- * differs.  10..18 are timing diagnostics whose outputs are meaningless
+ * line taken from the next lane, 7/8 = variants 1/2 with each block's last
+ * DMA segment cut at the block's end.  These give identical results; only
+ * speed differs.  10..19 are timing diagnostics whose outputs are meaningless
  * (memory-only / hashing-only / plain reads).  Unaligned batches always use
  * variant 0.  The environment variable RSG_BLOCKSUMS_KERNEL sets the initial
  * value. */
@@ -192,6 +194,28 @@ rsg_status rsg_hash_search_device(rsg_ctx *ctx, const void *d_src, uint64_t src_
 rsg_status rsg_encode_tokens(const uint8_t *src, uint64_t src_len, const rsg_sum_head *head,
                              const rsg_match *matches, uint64_t n_matches, uint8_t *out,
                              uint64_t out_cap, uint64_t *out_len);
+
+/* ------------------------------------------ receiver token application
+ * Replaces (*receiver.Transfer).receiveData's token loop (receiver.go:98-188,
+ * recvToken token.go:6-20).  `tokens` = the bytes after the SumHead: literal
+ * runs (int32 LE n > 0 + n bytes), matches (int32 -(i+1) = basis block i,
+ * head->block_len bytes at i*block_len, head->rem for block count-1), the
+ * int32 0 terminator, then the 16-byte whole-file sum.  The file is rebuilt
+ * into out (out == NULL or too small: RSG_ERR_TRUNCATED with *out_len set).
+ * A stream that ends early, a match past the end of the basis or a match
+ * without a basis (basis == NULL) is RSG_ERR_INVALID, as the reference's
+ * ReadFull / ReadAt / "local file not open" errors.
+ *   rsg_apply_tokens: rebuild only; *consumed = offset of the whole-file sum.
+ *   rsg_receive_data: rebuild, then MD4(int32_LE(seed) || file) on the GPU
+ *     (seeded file-sum kernel) against the stream's sum: RSG_ERR_CORRUPT on
+ *     mismatch ("file corruption", receiver.go:171-173); *consumed includes
+ *     the 16 sum bytes. */
+rsg_status rsg_apply_tokens(const uint8_t *tokens, uint64_t tokens_len, const rsg_sum_head *head,
+                            const uint8_t *basis, uint64_t basis_len, uint8_t *out, uint64_t out_cap,
+                            uint64_t *out_len, uint64_t *consumed);
+rsg_status rsg_receive_data(rsg_ctx *ctx, const uint8_t *tokens, uint64_t tokens_len, const rsg_sum_head *head,
+                            const uint8_t *basis, uint64_t basis_len, int32_t seed, uint8_t *out, uint64_t out_cap,
+                            uint64_t *out_len, uint64_t *consumed);
 
 /* ------------------------------------------ whole-file sums
  * MD4 of whole files, one GPU lane per file (MD4 is serial within a message,

@@ -59,6 +59,10 @@ def lib():
             ctypes.c_void_p,
         ]
         L.orc_hash_search.restype = ctypes.c_int64
+        L.orc_receive_data.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                       ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+        L.orc_receive_data.restype = ctypes.c_int64
         del u8p
         _lib = L
     return _lib
@@ -293,3 +297,23 @@ def py_hash_search(src: bytes, head, sum1, sum2, targets, seed: int, c2=None):
                 break
     matched(size, -1)
     return matches, bytes(out)
+
+
+def receive_data(stream: bytes, head, basis, seed: int):
+    """receiveData (receiver.go:98-188): rebuild the file from `stream` (tokens,
+    int32 0, 16-byte whole-file sum) and the basis; checks the seeded whole-file
+    MD4.  -> (rebuilt bytes, bytes consumed).  Raises ValueError with the
+    oracle's code (-1 short stream, -2 basis read out of range, -3 corruption)."""
+    t = _as_u8(stream)
+    b = _as_u8(basis) if basis is not None else None
+    count, blen, _, rem = head
+    used = ctypes.c_int64(0)
+    L = lib()
+    bp = _ptr(b) if b is not None else None
+    blen_b = b.size if b is not None else 0
+    n = L.orc_receive_data(_ptr(t), t.size, count, blen, rem, bp, blen_b, _i32(seed), None, 0, ctypes.byref(used))
+    if n < 0:
+        raise ValueError(int(n))
+    out = np.zeros(max(n, 1), dtype=np.uint8)
+    L.orc_receive_data(_ptr(t), t.size, count, blen, rem, bp, blen_b, _i32(seed), _ptr(out), n, ctypes.byref(used))
+    return out[:n].tobytes(), int(used.value)

@@ -408,3 +408,68 @@ int64_t orc_hash_search(const uint8_t *src, int64_t size,
     free(lens);
     return s.nm; /* callers compare *tok_len with tok_cap to detect truncation */
 }
+
+/* ------------------------------------------------------------------------- */
+/* Receiver: receiveData + recvToken                                           */
+/* (internal/receiver/receiver.go:98-188, internal/receiver/token.go:6-20).   */
+/* ------------------------------------------------------------------------- */
+static int32_t rd_i32(const uint8_t *p) {
+    return (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24));
+}
+
+/*
+ * Rebuilds the file from the token stream `tok` (the bytes after the SumHead:
+ * tokens, the int32 0 terminator, then the sender's 16-byte whole-file sum)
+ * and the basis, and checks MD4(int32_LE(seed) || rebuilt) against that sum.
+ * Returns the rebuilt length (stored while it fits in out_cap; out may be
+ * NULL to size), or
+ *   -1 the stream ends early (recvToken / io.ReadFull errors, token.go:8-18,
+ *      receiver.go:167-170),
+ *   -2 a match reads outside the basis (localFile.ReadAt error,
+ *      receiver.go:155-157) or there is no basis (:143-145),
+ *   -3 the whole-file sums differ ("file corruption", receiver.go:171-173).
+ * *consumed = stream bytes read through the whole-file sum.
+ */
+int64_t orc_receive_data(const uint8_t *tok, int64_t tok_len, int32_t count, int32_t blen, int32_t rem,
+                         const uint8_t *basis, int64_t basis_len, int32_t seed,
+                         uint8_t *out, int64_t out_cap, int64_t *consumed) {
+    md4_ctx h;
+    md4_init(&h);
+    uint8_t sb[4];
+    uint32_t us = (uint32_t)seed;
+    sb[0] = (uint8_t)us; sb[1] = (uint8_t)(us >> 8); sb[2] = (uint8_t)(us >> 16); sb[3] = (uint8_t)(us >> 24);
+    md4_update(&h, sb, 4); /* binary.Write(h, LE, rt.Seed), receiver.go:117-118 */
+    int64_t pos = 0, off = 0;
+    for (;;) {
+        if (pos + 4 > tok_len) return -1;
+        int32_t token = rd_i32(tok + pos);
+        pos += 4;
+        if (token == 0) break; /* receiver.go:128-130 */
+        const uint8_t *data;
+        int64_t n;
+        if (token > 0) { /* literal, token.go:15-19 */
+            n = token;
+            if (pos + n > tok_len) return -1;
+            data = tok + pos;
+            pos += n;
+        } else {
+            if (!basis) return -2;
+            int32_t idx = -(token + 1); /* receiver.go:146 */
+            int64_t off2 = (int64_t)idx * (int64_t)blen;
+            n = blen;
+            if (idx == count - 1 && rem != 0) n = rem; /* :148-151 */
+            if (off2 + n > basis_len) return -2;
+            data = basis + off2;
+        }
+        if (out && off + n <= out_cap) memcpy(out + off, data, (size_t)n);
+        md4_update(&h, data, (uint64_t)n);
+        off += n;
+    }
+    uint8_t local[16];
+    md4_final(&h, local);
+    if (pos + 16 > tok_len) return -1;
+    if (memcmp(local, tok + pos, 16) != 0) return -3;
+    pos += 16;
+    if (consumed) *consumed = pos;
+    return off;
+}

@@ -9,8 +9,8 @@ raises ImportError; there is no CPU fallback.
 """
 from ._lib import FILESUM_PLAIN, FILESUM_SEEDED, RsgError, SumHead  # noqa: F401  (loads librsg.so, fails loudly)
 from .engine import (RECORD_BYTES, Conn, DeviceBuffer, Engine, Plan, checksum1, checksum2,  # noqa: F401
-                     default_engine, device_count, encode_tokens, reader_checksum, sum_sizes_sqroot)
+                     apply_tokens, default_engine, device_count, encode_tokens, reader_checksum, sum_sizes_sqroot)
 
 __all__ = ["Engine", "Plan", "DeviceBuffer", "Conn", "SumHead", "RsgError", "RECORD_BYTES",
            "FILESUM_PLAIN", "FILESUM_SEEDED", "sum_sizes_sqroot", "checksum1", "checksum2",
-           "reader_checksum", "encode_tokens", "device_count", "default_engine"]
+           "reader_checksum", "encode_tokens", "apply_tokens", "device_count", "default_engine"]

@@ -30,6 +30,7 @@ ERR_NOMEM = -2
 ERR_HIP = -3
 ERR_NODEV = -4
 ERR_TRUNCATED = -5
+ERR_CORRUPT = -6
 
 
 class SumHead(ctypes.Structure):
@@ -89,6 +90,10 @@ _PROTOS = {
                                      ctypes.POINTER(Match), _u64, ctypes.POINTER(_u64)]),
     "rsg_encode_tokens": (_st, [_vp, _u64, ctypes.POINTER(SumHead), ctypes.POINTER(Match), _u64,
                                 _vp, _u64, ctypes.POINTER(_u64)]),
+    "rsg_apply_tokens": (_st, [_vp, _u64, ctypes.POINTER(SumHead), _vp, _u64, _vp, _u64,
+                               ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
+    "rsg_receive_data": (_st, [_vp, _vp, _u64, ctypes.POINTER(SumHead), _vp, _u64, _i32, _vp, _u64,
+                               ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "rsg_file_sums_host": (_st, [_vp, ctypes.POINTER(File), _u64, _i32, _i32, _vp]),
     "rsg_file_sums_device": (_st, [_vp, _vp, _u64, ctypes.POINTER(File), _u64, _i32, _i32, _vp]),
     "rsg_comm_unique_id": (_st, [_vp]),

@@ -261,7 +261,7 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 // belong to the same lane the two uses are one segment apart and the second
 // is an L2 hit, whereas across lanes they are a whole block apart and the line
 // is often refetched from HBM.  K = 4 cuts those refetches by 4x.
-template <int K, int MODE>
+template <int K, int MODE, bool TRIM = false>
 __device__ __forceinline__ void staged_tile(
     uint32_t tile, uint8_t *slab_all, const uint8_t *__restrict__ arena, uint64_t arena_bytes,
     const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file, uint32_t nwg256,
@@ -367,6 +367,22 @@ __device__ __forceinline__ void staged_tile(
             voff[i] = u < 16u ? v : 0x80000000u;  // pad slot: out of range, no memory request
         }
     };
+    // TRIM: the last segment of a block is cut at the block's end (16-byte
+    // units at or past n_j are dropped like the pad).  Without the cut, lane
+    // j's last piece runs up to 68 bytes into block j+1, whose first line was
+    // fetched by lane j+1 a whole block earlier and is usually gone from L2.
+    auto trim_voff = [&](uint32_t kb, uint32_t s) {
+        uint32_t nn = n[0];
+#pragma unroll
+        for (int k = 1; k < K; k++) nn = (kb == (uint32_t)k) ? n[k] : nn;
+#pragma unroll
+        for (uint32_t i = 0; i < kDmaPerSeg; i++) {
+            const uint32_t idx = 64u * i + lane;
+            const uint32_t j = idx / 17u, u = idx - 17u * j;
+            const uint32_t nj = (uint32_t)__shfl((int)nn, (int)j, 64);
+            voff[i] = (16u * u + kSegBytes * s < nj) ? voff[i] : 0x80000000u;
+        }
+    };
     auto dma_segment = [&](uint32_t s) {
 #pragma unroll
         for (uint32_t i = 0; i < kDmaPerSeg; i++)
@@ -395,6 +411,7 @@ __device__ __forceinline__ void staged_tile(
         if (++s >= sk) { s = 0; k++; }
     };
     build_voff(0);
+    if (TRIM && S[0] == 1) trim_voff(0, 0);
     if (MODE != 2) dma_segment(0);
     next_cursor(dk, ds);
     read_segment();
@@ -417,6 +434,12 @@ __device__ __forceinline__ void staged_tile(
             const bool more = dk < (uint32_t)K;
             if (more) {
                 if (ds == 0) build_voff(dk);
+                if (TRIM) {
+                    uint32_t sk2 = S[0];
+#pragma unroll
+                    for (int q = 1; q < K; q++) sk2 = (dk == (uint32_t)q) ? S[q] : sk2;
+                    if (ds + 1 == sk2) trim_voff(dk, ds);
+                }
                 if (MODE != 2) dma_segment(ds);
                 next_cursor(dk, ds);
             }
@@ -438,13 +461,13 @@ __device__ __forceinline__ void staged_tile(
 }
 
 
-template <int K, int MODE>
+template <int K, int MODE, bool TRIM = false>
 __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
     uint8_t *__restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * kWaveSlab];
-    staged_tile<K, MODE>(blockIdx.x, slab_all, arena, arena_bytes, files, wg_file, nwg256, total_blocks, seed, out);
+    staged_tile<K, MODE, TRIM>(blockIdx.x, slab_all, arena, arena_bytes, files, wg_file, nwg256, total_blocks, seed, out);
 }
 
 // ---------------------------------------------------------------- line-ring layout
@@ -911,8 +934,8 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     dim3 grid(nwg), block(kBlockSumThreads);
 #define RSG_LAUNCH(KERNEL, GRID) \
     hipLaunchKernelGGL(KERNEL, GRID, block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out)
-#define RSG_STAGED(KK, MM)                                                                                      \
-    hipLaunchKernelGGL((block_sums_staged<KK, MM>), dim3((uint32_t)((total_blocks + 256u * KK - 1) / (256u * KK))), \
+#define RSG_STAGED(KK, MM, ...)                                                                                 \
+    hipLaunchKernelGGL((block_sums_staged<KK, MM, ##__VA_ARGS__>), dim3((uint32_t)((total_blocks + 256u * KK - 1) / (256u * KK))), \
                        block, 0, stream, arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out)
     switch (v) {
         case 0:
@@ -945,6 +968,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 10: RSG_STAGED(1, 1); break;
         case 11: RSG_STAGED(1, 2); break;
         case 15: RSG_STAGED(1, 3); break;
+        case 7: RSG_STAGED(1, 0, true); break;
+        case 8: RSG_STAGED(4, 0, true); break;
+        case 19: RSG_STAGED(1, 1, true); break;
         case 16: RSG_STAGED(1, 4); break;
         case 12: RSG_LAUNCH(block_sums_regblock<1>, grid); break;
         case 13:

@@ -8,6 +8,7 @@ for name so parity tests read like the reference's own code:
   (*receiver.Transfer).generateAndSendSums generator.go:325-350     -> Engine.generate_and_send_sums
   (*sender.Transfer).hashSearch            match.go:21-230          -> Engine.hash_search
   matched / simpleSendToken                match.go:233, token.go:4 -> encode_tokens
+  (*receiver.Transfer).receiveData         receiver.go:98-188       -> Engine.receive_data / apply_tokens
 
 Every checksum is computed by the HIP kernels; nothing here hashes bytes on
 the CPU.  Errors surface as RsgError (the Go side maps them to `error`).
@@ -251,6 +252,26 @@ class Engine:
         check(lib.rsg_file_sums_host(self.ctx, desc, n, mode, _i32(seed), _ptr(out)), self.ctx)
         return [out[16 * i: 16 * i + 16].tobytes() for i in range(n)]
 
+    def receive_data(self, stream, head, basis, seed: int) -> Tuple[bytes, int]:
+        """(*receiver.Transfer).receiveData (receiver.go:98-188): rebuild the file
+        from `stream` (tokens, int32 0, 16-byte whole-file sum) and the basis
+        (None = no local file), then check MD4(int32_LE(seed) || file) on the
+        GPU against the sender's sum.  -> (file bytes, stream bytes consumed).
+        RsgError status ERR_CORRUPT = the reference's "file corruption"."""
+        t = _u8(stream)
+        b = _u8(basis) if basis is not None else None
+        h = head if isinstance(head, SumHead) else SumHead(*head)
+        n, used = ctypes.c_uint64(), ctypes.c_uint64()
+        bp, bl = (_ptr(b), b.size) if b is not None else (ctypes.c_void_p(0), 0)
+        st = lib.rsg_apply_tokens(_ptr(t), t.size, ctypes.byref(h), bp, bl, None, 0, ctypes.byref(n),
+                                  ctypes.byref(used))
+        if st != _lib.ERR_TRUNCATED:
+            check(st)
+        out = np.empty(max(n.value, 1), dtype=np.uint8)
+        check(lib.rsg_receive_data(self.ctx, _ptr(t), t.size, ctypes.byref(h), bp, bl, _i32(seed), _ptr(out),
+                                   n.value, ctypes.byref(n), ctypes.byref(used)), self.ctx)
+        return out[: n.value].tobytes(), used.value
+
     def file_sums_device(self, arena: DeviceBuffer, files: Sequence[Tuple[int, int]], mode: int = _lib.FILESUM_PLAIN,
                          seed: int = 0, out: Optional[DeviceBuffer] = None) -> DeviceBuffer:
         """Same for files already in device memory: files = [(offset, len)];
@@ -326,6 +347,23 @@ def encode_tokens(src, head, matches: Iterable[Tuple[int, int]]) -> bytes:
     check(lib.rsg_encode_tokens(_ptr(a), a.size, ctypes.byref(h), arr, len(ms), _ptr(out), n.value,
                                 ctypes.byref(n)))
     return out[: n.value].tobytes()
+
+
+def apply_tokens(stream, head, basis) -> Tuple[bytes, int]:
+    """The token loop of receiveData (receiver.go:122-163) without the sum
+    check: -> (file bytes, offset of the whole-file sum in `stream`)."""
+    t = _u8(stream)
+    b = _u8(basis) if basis is not None else None
+    h = head if isinstance(head, SumHead) else SumHead(*head)
+    n, used = ctypes.c_uint64(), ctypes.c_uint64()
+    bp, bl = (_ptr(b), b.size) if b is not None else (ctypes.c_void_p(0), 0)
+    st = lib.rsg_apply_tokens(_ptr(t), t.size, ctypes.byref(h), bp, bl, None, 0, ctypes.byref(n), ctypes.byref(used))
+    if st != _lib.ERR_TRUNCATED:
+        check(st)
+    out = np.empty(max(n.value, 1), dtype=np.uint8)
+    check(lib.rsg_apply_tokens(_ptr(t), t.size, ctypes.byref(h), bp, bl, _ptr(out), n.value, ctypes.byref(n),
+                               ctypes.byref(used)))
+    return out[: n.value].tobytes(), used.value
 
 
 _default: Optional[Engine] = None

@@ -94,3 +94,37 @@ def test_plan_block_sums_layout():
         assert first[i] == acc
         acc += heads[i].count
     assert total.value == acc
+
+
+def _token_stream(name):
+    src, basis, blen, seed = cases.match_cases()[name]
+    head = orc.sum_head(basis.size, blen)
+    rec = orc.block_sums(basis, blen, seed)
+    s1, s2 = orc.parse_records(rec) if head[0] else (np.zeros(0, np.uint32), np.zeros((0, 16), np.uint8))
+    _, tokens, fsum = orc.hash_search(src, head, s1, s2, orc.stable_targets(s1), seed)
+    return src, basis, head, seed, tokens, fsum
+
+
+@pytest.mark.parametrize("name", sorted(cases.match_cases()))
+def test_apply_tokens_matches_oracle(name):
+    """rsg_apply_tokens (host byte copying of receiveData's token loop,
+    receiver.go:122-163) rebuilds what the oracle's receive_data rebuilds."""
+    import rsync_amd
+    src, basis, head, seed, tokens, fsum = _token_stream(name)
+    want, used = orc.receive_data(tokens + fsum, head, basis, seed)
+    got, sum_at = rsync_amd.apply_tokens(tokens + fsum, head, basis)
+    assert got == want == src.tobytes()
+    assert sum_at == len(tokens) and used == sum_at + 16
+
+
+def test_apply_tokens_errors():
+    import rsync_amd
+    src, basis, head, seed, tokens, fsum = _token_stream("shifted_700")
+    for stream, b in [(tokens[:-4], basis), (tokens[:10], basis), (tokens, basis[:1000]), (tokens, None)]:
+        with pytest.raises(rsync_amd.RsgError) as e:
+            rsync_amd.apply_tokens(stream, head, b)
+        assert e.value.status == -1
+    # literal-only stream needs no basis
+    lit = rsync_amd.encode_tokens(src, head, [])
+    got, _ = rsync_amd.apply_tokens(lit, head, None)
+    assert got == src.tobytes()

@@ -110,3 +110,34 @@ def test_identical_large_property(eng):
     assert head[0] == total == 32768
     got = eng.hash_search_device(dev, size, head, s1, s2, orc.stable_targets(s1), cases.SEED)
     assert got == [(i * head[1], i) for i in range(total)]
+
+
+@pytest.mark.parametrize("seed_case", range(4))
+def test_delta_round_trip_on_gpu(eng, seed_case):
+    """The whole delta path through the C-ABI, every checksum on the GPU:
+    receiver block sums of the basis (generator.go:325-350) -> sender search
+    (match.go:21-230) -> tokens (token.go) + whole-file sum -> receiveData
+    (receiver.go:98-188) rebuilds the source and passes the seeded MD4 check;
+    a flipped sum byte is reported as corruption (receiver.go:171-173)."""
+    import rsync_amd
+    rng = np.random.default_rng(900 + seed_case)
+    basis = cases.splitmix64_bytes(910 + seed_case, int(rng.integers(50_000, 2_000_000)))
+    src = cases.mutate(basis, 920 + seed_case, 0.4, 1, 5000, n_ins=3, n_del=3)
+    blen = int(rng.choice([0, 700, 1773]))
+    seed = int(rng.integers(-2**31, 2**31))
+    heads, rec, _ = eng.block_sums([basis], seed, blen)
+    head = heads[0].astuple()
+    assert rec == orc.block_sums(basis, head[1], seed)
+    s1, s2 = orc.parse_records(rec)
+    tg = orc.stable_targets(s1)
+    matches = eng.hash_search(src, head, s1, s2, tg, seed)
+    fsum = eng.file_sums([src], rsync_amd.FILESUM_SEEDED, seed)[0]
+    stream = rsync_amd.encode_tokens(src, head, matches) + fsum
+    want, used_o = orc.receive_data(stream, head, basis, seed)
+    got, used = eng.receive_data(stream, head, basis, seed)
+    assert got == want == src.tobytes() and used == used_o == len(stream)
+    bad = bytearray(stream)
+    bad[-5] ^= 0x40
+    with pytest.raises(rsync_amd.RsgError) as e:
+        eng.receive_data(bytes(bad), head, basis, seed)
+    assert e.value.status == rsync_amd._lib.ERR_CORRUPT

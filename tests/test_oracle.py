@@ -166,3 +166,39 @@ def test_tokens_terminate_and_decode():
             out += basis[i * head[1]: i * head[1] + ln].tobytes()
     assert p == len(tokens)
     assert bytes(out) == src.tobytes()
+
+
+# ---- receiver token application (receiver.go:98-188)
+def _stream(name):
+    src, basis, blen, seed = cases.match_cases()[name]
+    head, s1, s2 = _basis_sums(basis, blen, seed)
+    _, tokens, fsum = orc.hash_search(src, head, s1, s2, orc.stable_targets(s1), seed)
+    return src, basis, head, seed, tokens + fsum
+
+
+@pytest.mark.parametrize("name", sorted(cases.match_cases()))
+def test_receive_data_rebuilds_golden(name):
+    """Every golden search's token stream + whole-file sum rebuilds the source
+    from the basis and passes the seeded MD4 check (receiver.go:166-173)."""
+    src, basis, head, seed, stream = _stream(name)
+    out, used = orc.receive_data(stream, head, basis, seed)
+    assert out == src.tobytes()
+    assert used == len(stream)
+
+
+def test_receive_data_errors():
+    src, basis, head, seed, stream = _stream("shifted_700")
+    bad = bytearray(stream)
+    bad[-1] ^= 1  # sender's sum differs -> "file corruption"
+    with pytest.raises(ValueError, match="-3"):
+        orc.receive_data(bytes(bad), head, basis, seed)
+    with pytest.raises(ValueError, match="-3"):  # wrong seed
+        orc.receive_data(stream, head, basis, seed + 1)
+    with pytest.raises(ValueError, match="-1"):  # stream cut inside the sum
+        orc.receive_data(stream[:-3], head, basis, seed)
+    with pytest.raises(ValueError, match="-1"):  # cut before the terminator
+        orc.receive_data(stream[:20], head, basis, seed)
+    with pytest.raises(ValueError, match="-2"):  # basis shorter than a matched block
+        orc.receive_data(stream, head, basis[:1000], seed)
+    with pytest.raises(ValueError, match="-2"):  # match token, no basis
+        orc.receive_data(stream, head, None, seed)
