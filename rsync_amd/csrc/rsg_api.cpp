@@ -260,7 +260,8 @@ void rsg_ctx_destroy(rsg_ctx *c) {
         if (c->side[i]) hipStreamSynchronize(c->side[i]);
     DevBuf *dbs[] = {&c->d_files, &c->d_wg, &c->d_in[0], &c->d_in[1], &c->d_out[0], &c->d_out[1],
                      &c->d_desc[0], &c->d_desc[1], &c->d_fb[0], &c->d_fb[1], &c->d_agg, &c->d_prefix, &c->d_bits, &c->d_counts,
-                     &c->d_list, &c->d_table, &c->d_filter, &c->d_misc};
+                     &c->d_list, &c->d_table, &c->d_filter, &c->d_misc, &c->d_groups, &c->d_hi16, &c->d_sum2,
+                     &c->d_res};
     for (DevBuf *b : dbs)
         if (b->p) hipFree(b->p);
     PinBuf *pbs[] = {&c->h_in[0], &c->h_in[1], &c->h_out[0], &c->h_out[1], &c->h_desc[0], &c->h_desc[1], &c->h_misc};
@@ -408,8 +409,8 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
 }
 
 rsg_status rsg_set_block_sums_kernel(int32_t variant) {
-    if (variant < -1 || variant == 9 || variant > 19)
-        return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..8 or 10..19");
+    if (variant < -1 || variant > 19)
+        return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..19");
     rsg::set_block_sums_variant(variant);
     return RSG_OK;
 }

@@ -216,6 +216,85 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_direct(
     store_record(out, g, n, s1, t, h);
 }
 
+// ---------------------------------------------------------------- long-block variant
+// Few long blocks (the sender's 32 KiB confirmation windows, 128 KiB blocks):
+// there are too few lanes to hide HBM latency by occupancy, so each lane keeps
+// P chunks of its own block in flight (P x 16 VGPRs; one wave per SIMD is
+// plenty here).  Chunk c lives in buffer c % P; after chunk c is hashed its
+// buffer is refilled with chunk c + P.
+template <int P, bool ALIGNED>
+__device__ __forceinline__ void hash_block_deep(const uint8_t *arena, uintptr_t end, uint64_t off, uint32_t n,
+                                                uint32_t seed, uint32_t h[4], int32_t &s1, uint32_t &t) {
+    const uint8_t *p = arena + off;
+    const uint32_t sh = ALIGNED ? 0u : (uint32_t)((uintptr_t)p & 3u);
+    const uint8_t *p0 = p - sh;
+    const uint32_t nfull = n >> 6;
+    // Fast path: chunks 0..nfull+1 lie inside the arena, so every load in the
+    // ring is a plain unconditional load (branch-free loop: the compiler can
+    // keep P - 1 chunks in flight).  Blocks ending near the arena's end take
+    // the guarded single-chunk path.
+    if ((uintptr_t)p0 + 64u * (uint64_t)(nfull + 2) + (ALIGNED ? 0u : 4u) > end) {
+        hash_block_direct<ALIGNED>(arena, end, off, n, seed, h, s1, t);
+        return;
+    }
+    const uint32_t last = nfull + 1;  // loads are clamped to this chunk
+    // buf[u] = chunk words; nxt[u] = the next aligned word after the chunk
+    // (funnel-shift input when not ALIGNED), loaded with it so that a chunk
+    // never waits on a younger load.
+    uint32_t buf[P][16], nxt[P];
+#define RSG_FETCH(U, CHUNK)                                                        \
+    do {                                                                           \
+        const uint8_t *q_ = p0 + 64u * (CHUNK);                                    \
+        load16(q_, buf[U]);                                                        \
+        if (!ALIGNED) nxt[U] = *reinterpret_cast<const uint32_t *>(q_ + 64);       \
+    } while (0)
+#pragma unroll
+    for (int u = 0; u < P; u++) RSG_FETCH(u, min((uint32_t)u, last));
+    uint32_t c = 0;
+#pragma unroll 1
+    for (; c + P <= nfull; c += P) {
+#pragma unroll
+        for (int u = 0; u < P; u++) {
+            hash_chunk<ALIGNED>(buf[u], ALIGNED ? 0u : nxt[u], sh, c + u, h, s1, t);
+            RSG_FETCH(u, min(c + (uint32_t)u + P, last));
+        }
+    }
+#undef RSG_FETCH
+    // Fewer than P data chunks left: they and the tail chunk (chunk c+u sits in
+    // buffer u) are already in the ring; one last predicated round, no loads.
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+        const uint32_t cc = c + (uint32_t)u;
+        if (cc < nfull) hash_chunk<ALIGNED>(buf[u], ALIGNED ? 0u : nxt[u], sh, cc, h, s1, t);
+        else if (cc == nfull) hash_tail<ALIGNED>(buf[u], ALIGNED ? 0u : nxt[u], sh, n, seed, h, s1, t);
+    }
+}
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(64) void block_sums_long(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (g >= total_blocks) return;
+    // wg_file is indexed per 256-lane workgroup of the plan
+    uint32_t lo = wg_file[g / kBlockSumThreads], hi = wg_file[g / kBlockSumThreads + 1];
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (files[mid].first_block <= g) lo = mid; else hi = mid - 1;
+    }
+    const DevFile F = files[lo];
+    const uint64_t boff = (g - F.first_block) * F.blen;
+    const uint64_t left = F.len - boff;
+    const uint32_t n = left < F.blen ? (uint32_t)left : F.blen;  // generator.go:334
+    uint32_t h[4];
+    md4_init(h);
+    int32_t s1 = 0;
+    uint32_t t = 0;
+    hash_block_deep<8, ALIGNED>(arena, (uintptr_t)(arena + arena_bytes), F.offset + boff, n, seed, h, s1, t);
+    store_record(out, g, n, s1, t, h);
+}
+
 // ---------------------------------------------------------------- staged variant
 // Coalesced HBM reads: a wave owns 64 consecutive blocks (one per lane) and
 // streams them through a private LDS slab 256 bytes (4 MD4 chunks) of every
@@ -910,7 +989,9 @@ __global__ __launch_bounds__(kRtThreads) void block_sums_regtile(
 
 // Kernel variants (rsg_set_block_sums_kernel): -1 = automatic, 0 = direct,
 // 1 = staged K=1, 2 = staged K=4, 3 = register-block, 4 = register-tile,
-// 5 = loaded line ring, 6 = line ring with shared boundary lines.  Timing
+// 5 = loaded line ring, 6 = line ring with shared boundary lines, 7/8 = 1/2
+// with the last segment cut at the block end, 9 = long blocks with deep
+// per-lane prefetch (automatic for few blocks >= kLongBlockBytes).  Timing
 // diagnostics with meaningless outputs: 10 = staged K=1 memory only, 11 =
 // staged K=1 hashing only, 12 = register-block memory only, 13/14 = linear
 // read of the arena (plain loads / LDS DMA), 15 = staged with line-aligned
@@ -927,8 +1008,8 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         g_variant = e ? atoi(e) : -1;
     }
     int v = g_variant;
-    if (v == -1) v = 1;  // automatic choice
-    if (!aligned && v < 13) v = 0;
+    if (v == -1) v = (max_blen >= kLongBlockBytes && total_blocks < kLongBlockMaxCount) ? 9 : 1;  // automatic
+    if (!aligned && v < 13 && v != 9) v = 0;
     if ((v == 3 || v == 4 || v == 12 || v == 17) && max_blen > kRegMaxBytes) v = 1;
     if ((v == 4 || v == 17) && !scratch) v = 1;
     dim3 grid(nwg), block(kBlockSumThreads);
@@ -943,6 +1024,16 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             else RSG_LAUNCH(block_sums_direct<false>, grid);
             break;
         case 2: RSG_STAGED(4, 0); break;
+        case 9: {
+            dim3 g64((uint32_t)((total_blocks + 63) / 64)), b64(64);
+            if (aligned)
+                hipLaunchKernelGGL(block_sums_long<true>, g64, b64, 0, stream, arena, arena_bytes, files, wg_file,
+                                   total_blocks, seed, out);
+            else
+                hipLaunchKernelGGL(block_sums_long<false>, g64, b64, 0, stream, arena, arena_bytes, files, wg_file,
+                                   total_blocks, seed, out);
+            break;
+        }
         case 3: RSG_LAUNCH(block_sums_regblock<0>, grid); break;
         case 4:
         case 17: {

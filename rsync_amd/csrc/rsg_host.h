@@ -36,6 +36,7 @@ struct rsg_ctx {
     PinBuf h_in[2], h_out[2], h_desc[2];
     // sender scratch
     DevBuf d_agg, d_prefix, d_bits, d_counts, d_list, d_table, d_filter, d_misc;
+    DevBuf d_groups, d_hi16, d_sum2, d_res;  // resolve tables (basis sums grouped by Sum1)
     PinBuf h_misc;
     // multi-GPU
     ncclComm_t comm = nullptr;

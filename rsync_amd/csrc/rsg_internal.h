@@ -8,6 +8,10 @@ namespace rsg {
 
 constexpr uint32_t kRecordBytes = 20;       // int32 sum1 + sum2[16], generator.go:341-346
 constexpr uint32_t kBlockSumThreads = 256;  // lanes (= blocks) per workgroup
+// Batches of few long blocks (< kLongBlockMaxCount blocks of >= kLongBlockBytes)
+// take the deep-prefetch kernel: too few lanes to hide HBM latency otherwise.
+constexpr uint32_t kLongBlockBytes = 8192;
+constexpr uint64_t kLongBlockMaxCount = 1u << 18;
 
 // Per-file descriptor of a block-sum batch, resident in HBM (32 bytes).
 struct DevFile {
@@ -57,6 +61,13 @@ __host__ __device__ inline uint32_t bucket_hash2(uint32_t s) { return ((s ^ (s >
 hipError_t launch_tile_agg(const uint8_t *src, uint64_t size, uint32_t r, TileAgg *out, uint32_t ntiles,
                            hipStream_t stream);
 hipError_t launch_tile_scan(const TileAgg *agg, uint32_t ntiles, TilePrefix *pre, hipStream_t stream);
+// Resolve confirmed windows to blocks (match.go:108-136): window i (record i,
+// length files[i].len) -> the first block in targets order with equal Sum1,
+// equal length and equal sum2[:s2len], or -1.  groups = (sum1, block) sorted
+// by sum1 (stable in targets order), hi16[h] = first group with sum1 >> 16 == h.
+hipError_t launch_resolve(const uint8_t *records, const DevFile *files, uint64_t n, const uint2 *groups,
+                          const uint32_t *hi16, const uint8_t *sum2, int32_t count, int32_t blen, int32_t rem,
+                          int32_t s2len, int32_t *res, hipStream_t stream);
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
                        const uint32_t *bitmap, const uint64_t *table, uint32_t bmask, uint64_t *cand,

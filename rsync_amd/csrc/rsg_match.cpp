@@ -113,30 +113,21 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
     if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, S.d_src, S.seed, ctx->d_out[0].p, ctx->d_fb[0].p,
                          S.st)) != RSG_OK)
         return s;
-    if ((s = ensure_pin(ctx, ctx->h_out[0], plan.total_blocks * kRecordBytes)) != RSG_OK) return s;
-    const uint8_t *rec = (const uint8_t *)ctx->h_out[0].p;
-    RSG_HIP(ctx, hipMemcpyAsync(ctx->h_out[0].p, ctx->d_out[0].p, plan.total_blocks * kRecordBytes,
-                                hipMemcpyDeviceToHost, S.st));
+    // Each window resolves on the GPU to the first block in targets order with
+    // equal Sum1, length and sum2[:s2len] (match.go:108-136); only the block
+    // indices come back.
+    if ((s = ensure_dev(ctx, ctx->d_res, plan.total_blocks * 4)) != RSG_OK) return s;
+    RSG_HIP(ctx, rsg::launch_resolve((const uint8_t *)ctx->d_out[0].p, (const DevFile *)ctx->d_files.p,
+                                     plan.total_blocks, (const uint2 *)ctx->d_groups.p,
+                                     (const uint32_t *)ctx->d_hi16.p, (const uint8_t *)ctx->d_sum2.p,
+                                     S.head.count, S.head.block_len, S.head.rem, S.head.s2len,
+                                     (int32_t *)ctx->d_res.p, S.st));
+    if ((s = ensure_pin(ctx, ctx->h_out[0], plan.total_blocks * 4)) != RSG_OK) return s;
+    const int32_t *found = (const int32_t *)ctx->h_out[0].p;
+    RSG_HIP(ctx, hipMemcpyAsync(ctx->h_out[0].p, ctx->d_res.p, plan.total_blocks * 4, hipMemcpyDeviceToHost, S.st));
     RSG_HIP(ctx, hipStreamSynchronize(S.st));
     S.pt->mark("v.kernel");
-    for (size_t i = 0; i < idx.size(); i++) {
-        const uint8_t *r = rec + i * kRecordBytes;
-        uint32_t w;
-        memcpy(&w, r, 4);
-        int32_t found = -1;
-        const int64_t k = (int64_t)wlen[i];
-        auto it = S.groups.begin() + S.hi16[w >> 16];
-        const auto stop = S.groups.begin() + S.hi16[(w >> 16) + 1];
-        while (it != stop && it->first < w) ++it;
-        for (; it != stop && it->first == w; ++it) {  // targets order, match.go:108
-            const int32_t b = it->second;
-            if (S.len_of(b) != k) continue;                                                        // :118
-            if (memcmp(r + 4, S.sum2 + 16 * (int64_t)b, (size_t)S.head.s2len) != 0) continue;  // :133
-            found = b;
-            break;
-        }
-        res[idx[i]] = found;
-    }
+    for (size_t i = 0; i < idx.size(); i++) res[idx[i]] = found[i];
     S.pt->mark("v.resolve");
     return RSG_OK;
 }
@@ -214,6 +205,22 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
     const int64_t last_len = (head->rem != 0) ? head->rem : B;
     S.end = std::max<int64_t>((int64_t)size + 1 - last_len, 1);  // match.go:70 (offset 0 always visited)
 
+    // The prefix pass over the source needs only B: it runs on the GPU while
+    // the host builds the filter tables below.
+    const uint64_t ntiles64 = (size + kScanTile - 1) / kScanTile;
+    if (ntiles64 >= 0xFFFFFFF0ull) return fail(ctx, RSG_ERR_INVALID, "source too large");
+    const uint32_t ntiles = (uint32_t)ntiles64;
+    rsg_status s;
+    if ((s = ensure_dev(ctx, ctx->d_agg, (uint64_t)ntiles * sizeof(TileAgg) + 64)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_prefix, ((uint64_t)ntiles + 1) * sizeof(TilePrefix) + 64)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_list, (uint64_t)kCandCap * 8)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_counts, 64)) != RSG_OK) return s;
+    {
+        const uint32_t r = (uint32_t)(B % kScanTile);
+        RSG_HIP(ctx, rsg::launch_tile_agg(d_src, size, r, (TileAgg *)ctx->d_agg.p, ntiles, S.st));
+        RSG_HIP(ctx, rsg::launch_tile_scan((const TileAgg *)ctx->d_agg.p, ntiles, (TilePrefix *)ctx->d_prefix.p, S.st));
+    }
+
     // Basis sums grouped by Sum1 in targets order; device filter = bitmap of
     // every Sum1 + a 2-choice bucketed table {Sum1, flags: bit1 = a block of
     // length B, bit2 = the remainder block}.
@@ -239,6 +246,19 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
         for (size_t h = 1; h < S.hi16.size(); h++) S.hi16[h] += S.hi16[h - 1];
     }
     pt.mark("groups");
+    {
+        // device copies for the resolve kernel: (sum1, block) pairs, hi16 index, sum2
+        const uint64_t ng = S.groups.size();
+        if ((s = ensure_dev(ctx, ctx->d_groups, ng * 8 + 8)) != RSG_OK) return s;
+        if ((s = ensure_dev(ctx, ctx->d_hi16, S.hi16.size() * 4)) != RSG_OK) return s;
+        if ((s = ensure_dev(ctx, ctx->d_sum2, (uint64_t)count * 16 + 16)) != RSG_OK) return s;
+        static_assert(sizeof(S.groups[0]) == 8, "(sum1, block) pair must be 8 bytes");
+        if (ng) {
+            RSG_HIP(ctx, hipMemcpyAsync(ctx->d_groups.p, S.groups.data(), ng * 8, hipMemcpyHostToDevice, S.st));
+            RSG_HIP(ctx, hipMemcpyAsync(ctx->d_sum2.p, sum2, (uint64_t)count * 16, hipMemcpyHostToDevice, S.st));
+        }
+        RSG_HIP(ctx, hipMemcpyAsync(ctx->d_hi16.p, S.hi16.data(), S.hi16.size() * 4, hipMemcpyHostToDevice, S.st));
+    }
     std::vector<std::pair<uint32_t, uint32_t>> keys;  // distinct sum1 -> flags
     for (size_t i = 0; i < S.groups.size(); i++) {
         const uint32_t f = 1u | ((S.len_of(S.groups[i].second) == B) ? 2u : 4u);
@@ -267,22 +287,11 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
         nb <<= 1;
     }
     pt.mark("tables");
-    const uint64_t ntiles64 = (size + kScanTile - 1) / kScanTile;
-    if (ntiles64 >= 0xFFFFFFF0ull) return fail(ctx, RSG_ERR_INVALID, "source too large");
-    const uint32_t ntiles = (uint32_t)ntiles64;
-    rsg_status s;
     if ((s = ensure_dev(ctx, ctx->d_filter, bitmap.size() * 4)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, ctx->d_table, table.size() * 8)) != RSG_OK) return s;
     const uint32_t bmask = nb - 1;
-    if ((s = ensure_dev(ctx, ctx->d_agg, (uint64_t)ntiles * sizeof(TileAgg) + 64)) != RSG_OK) return s;
-    if ((s = ensure_dev(ctx, ctx->d_prefix, ((uint64_t)ntiles + 1) * sizeof(TilePrefix) + 64)) != RSG_OK) return s;
-    if ((s = ensure_dev(ctx, ctx->d_list, (uint64_t)kCandCap * 8)) != RSG_OK) return s;
-    if ((s = ensure_dev(ctx, ctx->d_counts, 64)) != RSG_OK) return s;
     RSG_HIP(ctx, hipMemcpyAsync(ctx->d_filter.p, bitmap.data(), bitmap.size() * 4, hipMemcpyHostToDevice, S.st));
     RSG_HIP(ctx, hipMemcpyAsync(ctx->d_table.p, table.data(), table.size() * 8, hipMemcpyHostToDevice, S.st));
-    const uint32_t r = (uint32_t)(B % kScanTile);
-    RSG_HIP(ctx, rsg::launch_tile_agg(d_src, size, r, (TileAgg *)ctx->d_agg.p, ntiles, S.st));
-    RSG_HIP(ctx, rsg::launch_tile_scan((const TileAgg *)ctx->d_agg.p, ntiles, (TilePrefix *)ctx->d_prefix.p, S.st));
 
     if (pt.on) {
         RSG_HIP(ctx, hipStreamSynchronize(S.st));

@@ -362,6 +362,45 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     }
 }
 
+// --------------------------------------------------------------- resolve
+__global__ __launch_bounds__(256) void resolve_kernel(const uint8_t *__restrict__ records,
+                                                      const DevFile *__restrict__ files, uint64_t n,
+                                                      const uint2 *__restrict__ groups,
+                                                      const uint32_t *__restrict__ hi16,
+                                                      const uint8_t *__restrict__ sum2, int32_t count, int32_t blen,
+                                                      int32_t rem, int32_t s2len, int32_t *__restrict__ res) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t *r = reinterpret_cast<const uint32_t *>(records + i * kRecordBytes);
+    const uint32_t w = r[0];
+    const uint32_t d[4] = {r[1], r[2], r[3], r[4]};
+    const uint64_t k = files[i].len;
+    int32_t found = -1;
+    for (uint32_t j = hi16[w >> 16], stop = hi16[(w >> 16) + 1]; j < stop; j++) {
+        const uint2 gb = groups[j];
+        if (gb.x < w) continue;
+        if (gb.x > w) break;
+        const int32_t b = (int32_t)gb.y;
+        const uint64_t len = (b == count - 1 && rem != 0) ? (uint64_t)rem : (uint64_t)blen;  // sender.go:135-139
+        if (len != k) continue;                                                                // match.go:118
+        const uint8_t *want = sum2 + 16 * (uint64_t)b;
+        bool eq = true;
+        for (int32_t q = 0; q < s2len; q++)                                                    // match.go:133
+            eq = eq && (want[q] == (uint8_t)(d[q >> 2] >> (8 * (q & 3))));
+        if (eq) { found = b; break; }
+    }
+    res[i] = found;
+}
+
+hipError_t launch_resolve(const uint8_t *records, const DevFile *files, uint64_t n, const uint2 *groups,
+                          const uint32_t *hi16, const uint8_t *sum2, int32_t count, int32_t blen, int32_t rem,
+                          int32_t s2len, int32_t *res, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(resolve_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, records, files, n,
+                       groups, hi16, sum2, count, blen, rem, s2len, res);
+    return hipGetLastError();
+}
+
 hipError_t launch_tile_agg(const uint8_t *src, uint64_t size, uint32_t r, TileAgg *out, uint32_t ntiles,
                            hipStream_t stream) {
     if (ntiles == 0) return hipSuccess;
