@@ -146,10 +146,12 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
  * 4 = register tiles (blocks <= 703 bytes), 5 = aligned line ring (each line
  * loaded once, realigned through LDS), 6 = line ring with each block's last
  * line taken from the next lane, 7/8 = variants 1/2 with each block's last
- * DMA segment cut at the block's end.  These give identical results; only
- * speed differs.  10..19 are timing diagnostics whose outputs are meaningless
- * (memory-only / hashing-only / plain reads).  Unaligned batches always use
- * variant 0.  The environment variable RSG_BLOCKSUMS_KERNEL sets the initial
+ * DMA segment cut at the block's end, 9 = deep per-lane prefetch for long
+ * blocks (automatic for unaligned batches with blocks >= 8 KiB; otherwise
+ * automatic = 1 for aligned batches, 0 for unaligned ones).  These give
+ * identical results; only speed differs.  10..19 are timing diagnostics whose outputs are meaningless
+ * (memory-only / hashing-only / plain reads).  Unaligned batches use
+ * variant 0 or 9.  The environment variable RSG_BLOCKSUMS_KERNEL sets the initial
  * value. */
 rsg_status rsg_set_block_sums_kernel(int32_t variant);
 

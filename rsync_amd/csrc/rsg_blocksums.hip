@@ -991,7 +991,7 @@ __global__ __launch_bounds__(kRtThreads) void block_sums_regtile(
 // 1 = staged K=1, 2 = staged K=4, 3 = register-block, 4 = register-tile,
 // 5 = loaded line ring, 6 = line ring with shared boundary lines, 7/8 = 1/2
 // with the last segment cut at the block end, 9 = long blocks with deep
-// per-lane prefetch (automatic for few blocks >= kLongBlockBytes).  Timing
+// per-lane prefetch (automatic for unaligned blocks >= kLongBlockBytes).  Timing
 // diagnostics with meaningless outputs: 10 = staged K=1 memory only, 11 =
 // staged K=1 hashing only, 12 = register-block memory only, 13/14 = linear
 // read of the arena (plain loads / LDS DMA), 15 = staged with line-aligned
@@ -1008,7 +1008,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         g_variant = e ? atoi(e) : -1;
     }
     int v = g_variant;
-    if (v == -1) v = (max_blen >= kLongBlockBytes && total_blocks < kLongBlockMaxCount) ? 9 : 1;  // automatic
+    // automatic: staged for aligned batches (also the faster one for long
+    // aligned blocks, tools/blocklen_sweep.py); unaligned batches (the sender's
+    // confirmation windows) take the deep-prefetch kernel when blocks are long
+    if (v == -1) v = aligned ? 1 : (max_blen >= kLongBlockBytes ? 9 : 0);
     if (!aligned && v < 13 && v != 9) v = 0;
     if ((v == 3 || v == 4 || v == 12 || v == 17) && max_blen > kRegMaxBytes) v = 1;
     if ((v == 4 || v == 17) && !scratch) v = 1;

@@ -8,10 +8,10 @@ namespace rsg {
 
 constexpr uint32_t kRecordBytes = 20;       // int32 sum1 + sum2[16], generator.go:341-346
 constexpr uint32_t kBlockSumThreads = 256;  // lanes (= blocks) per workgroup
-// Batches of few long blocks (< kLongBlockMaxCount blocks of >= kLongBlockBytes)
-// take the deep-prefetch kernel: too few lanes to hide HBM latency otherwise.
+// Unaligned batches of long blocks (>= kLongBlockBytes; the sender's
+// confirmation windows) take the deep-prefetch kernel: per-lane loads with
+// only one chunk in flight leave HBM latency exposed.
 constexpr uint32_t kLongBlockBytes = 8192;
-constexpr uint64_t kLongBlockMaxCount = 1u << 18;
 
 // Per-file descriptor of a block-sum batch, resident in HBM (32 bytes).
 struct DevFile {

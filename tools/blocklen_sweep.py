@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Kernel-variant timing for other block-sum shapes than bench.py's cfg2.
+
+    python tools/blocklen_sweep.py
+
+For each shape (files x file bytes, block length) and each variant, the
+block-sum launch is timed with HIP events over rotating input arenas (inputs
+resident in HBM).  Prints one JSON line per shape.  Diagnostic only: bench.py
+is the metric.
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SEED = 0x1BADB002
+SHAPES = [  # (files, file bytes, block length, arenas)
+    (1, 1 << 30, 131072, 2),      # one 1 GiB file, cfg5's block length
+    (1, 32 << 30, 131072, 1),     # cfg5's per-GPU share: one 32 GiB file
+    (1024, 1 << 20, 700, 2),      # cfg2
+]
+VARIANTS = {1: "staged", 9: "long_deep_prefetch"}
+
+
+def main():
+    import torch
+    import rsync_amd
+    from rsync_amd import _lib
+    eng = rsync_amd.Engine(0)
+    stream = torch.cuda.Stream()
+    sp = stream.cuda_stream
+    for nf, fb, blen, narena in SHAPES:
+        total = nf * fb
+        arenas = [eng.alloc(total) for _ in range(narena)]
+        for k, a in enumerate(arenas):
+            for f in range(nf):
+                eng.fill_splitmix64(a, fb, 1 + f + 7919 * k, offset=f * fb, stream=sp)
+        plan = eng.plan([(f * fb, fb, blen) for f in range(nf)], total)
+        recs = eng.alloc(plan.total_records * rsync_amd.RECORD_BYTES)
+        eng.synchronize(sp)
+        res = {}
+        for v, name in VARIANTS.items():
+            _lib.check(_lib.lib.rsg_set_block_sums_kernel(v))
+            steps = 5 if total > (4 << 30) else 30
+            for i in range(10):
+                plan.run(arenas[i % narena], SEED, recs, stream=sp)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for i in range(steps):
+                plan.run(arenas[i % narena], SEED, recs, stream=sp)
+            e1.record(stream)
+            eng.synchronize(sp)
+            ms = e0.elapsed_time(e1) / steps
+            res[name] = {"kernel_ms": round(ms, 4), "gib_s": round(total / 2**30 / (ms / 1e3), 1),
+                         "hbm_frac_8tbs": round((total + plan.total_records * 20) / (ms / 1e3) / 8e12, 4)}
+        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+        print(json.dumps({"files": nf, "file_bytes": fb, "block_len": blen, "records": plan.total_records,
+                          "variants": res}), flush=True)
+        plan.close()
+        for a in arenas:
+            a.free()
+        recs.free()
+
+
+if __name__ == "__main__":
+    main()
