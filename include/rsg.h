@@ -253,6 +253,47 @@ rsg_status rsg_comm_init(rsg_ctx *ctx, int32_t nranks, int32_t rank, const uint8
 rsg_status rsg_gather_bytes(rsg_ctx *ctx, const void *d_send, const uint64_t *send_bytes,
                             void *d_recv, int32_t root, void *stream);
 
+/* ------------------------------------------ wire formats
+ * Host byte formatting around the checksum path, so the engine's records
+ * leave wire-ready.  No GPU work; re-entrant.  Outputs follow the
+ * rsg_encode_tokens convention: out == NULL queries *out_len; a too-small
+ * out is RSG_ERR_TRUNCATED with *out_len set. */
+
+/* SumHead.ReadFrom validation (types.go:38-77): count >= 0,
+ * 0 <= block_len <= 1<<29, 0 <= s2len <= 16, 0 <= rem <= block_len. */
+rsg_status rsg_check_sum_head(const rsg_sum_head *head);
+/* The generator's stream for a batch (replaces the per-block Conn writes of
+ * generateAndSendSums, generator.go:325-350): for file f, int32 file_idx[f]
+ * (recvGenerator, generator.go:317; omitted when file_idx == NULL), the
+ * SumHead (types.go:79-86), then heads[f].count x (int32 LE sum1,
+ * sum2[:s2len]) taken from the 20-byte records (files back to back, as
+ * rsg_block_sums_* write them).  terminate != 0 appends GenerateFiles'
+ * two int32 -1 phase markers (generator.go:31,40). */
+rsg_status rsg_encode_sums(const int32_t *file_idx, const rsg_sum_head *heads, uint64_t nfiles,
+                           const uint8_t *records, int32_t terminate, uint8_t *out, uint64_t out_cap,
+                           uint64_t *out_len);
+/* Sender side: SumHead.ReadFrom + receiveSums (sender.go:118-151) into the
+ * arrays rsg_hash_search_* take: sum1[count], sum2[count*16] (bytes past
+ * s2len zeroed).  *consumed = 16 + count*(4+s2len) is set once the head
+ * parsed; cap < count is RSG_ERR_TRUNCATED (head filled in), a short stream
+ * or an invalid head is RSG_ERR_INVALID with the reference's message. */
+rsg_status rsg_decode_sums(const uint8_t *wire, uint64_t wire_len, rsg_sum_head *head, uint32_t *sum1,
+                           uint8_t *sum2, uint64_t cap, uint64_t *consumed);
+/* MultiplexWriter.WriteMsg (wire.go:28-36): data split into messages of at
+ * most max_message (<= 256 KiB, the reader's limit, wire.go:46-62) bytes,
+ * each prefixed by int32 LE ((7 + tag) << 24 | len). */
+rsg_status rsg_mux_frame(const uint8_t *data, uint64_t len, int32_t tag, uint32_t max_message, uint8_t *out,
+                         uint64_t out_cap, uint64_t *out_len);
+/* MultiplexReader (wire.go:49-95): concatenated MsgData payloads; MsgInfo is
+ * skipped, MsgError or another tag, a length > 256 KiB or a cut message is
+ * RSG_ERR_INVALID. */
+rsg_status rsg_mux_deframe(const uint8_t *wire, uint64_t wire_len, uint8_t *out, uint64_t out_cap,
+                           uint64_t *out_len);
+/* Conn.WriteInt64 / ReadInt64 (wire.go:108-117,177-195): int32 when
+ * 0 <= v <= 0x7fffffff, else int32 -1 then int64 LE. */
+rsg_status rsg_put_int64(int64_t v, uint8_t out[12], uint64_t *out_len);
+rsg_status rsg_get_int64(const uint8_t *in, uint64_t in_len, int64_t *v, uint64_t *consumed);
+
 #ifdef __cplusplus
 }
 #endif

@@ -317,3 +317,83 @@ def receive_data(stream: bytes, head, basis, seed: int):
     out = np.zeros(max(n, 1), dtype=np.uint8)
     L.orc_receive_data(_ptr(t), t.size, count, blen, rem, bp, blen_b, _i32(seed), _ptr(out), n, ctypes.byref(used))
     return out[:n].tobytes(), int(used.value)
+
+
+# ---------------------------------------------------------------- wire formats
+# Pure-Python restatements of the Go wire code around the checksum path
+# (SURVEY.md §8f row 4); small inputs only.
+
+def py_generate_files_stream(files, seed: int, block_lens, s2len: int = 16) -> bytes:
+    """GenerateFiles' bytes for files that all go through generateAndSendSums
+    (generator.go:20-41,317-321,325-350): per file int32 idx, SumHead, per block
+    int32 sum1 + Checksum2[:s2len]; then int32 -1 twice (phase markers)."""
+    out = bytearray()
+    for idx, (data, bl) in enumerate(zip(files, block_lens)):
+        h = sum_head(len(data), bl)
+        h = (h[0], h[1], s2len, h[3])
+        out += struct.pack("<i", idx) + head_bytes(h)
+        for i in range(h[0]):
+            blk = bytes(data[i * h[1]:(i + 1) * h[1]])
+            out += struct.pack("<I", checksum1(blk)) + checksum2(seed, blk)[:s2len]
+    out += struct.pack("<ii", -1, -1)
+    return bytes(out)
+
+
+def py_receive_sums(wire: bytes):
+    """SumHead.ReadFrom + receiveSums (types.go:38-77, sender.go:118-151)
+    -> (head tuple, [(sum1, sum2 bytes padded to 16)], consumed); raises
+    ValueError with the reference's message on an invalid head."""
+    if len(wire) < 16:
+        raise ValueError("unexpected EOF")
+    count, blen, s2len, rem = struct.unpack_from("<4i", wire)
+    if count < 0:
+        raise ValueError(f"invalid checksum count {count}")
+    if blen < 0 or blen > 1 << 29:
+        raise ValueError(f"invalid block length {blen}")
+    if s2len < 0 or s2len > 16:
+        raise ValueError(f"invalid checksum length {s2len}")
+    if rem < 0 or rem > blen:
+        raise ValueError(f"invalid remainder length {rem}")
+    pos, sums = 16, []
+    for _ in range(count):
+        if pos + 4 + s2len > len(wire):
+            raise ValueError("unexpected EOF")
+        s1 = struct.unpack_from("<I", wire, pos)[0]
+        sums.append((s1, wire[pos + 4:pos + 4 + s2len] + bytes(16 - s2len)))
+        pos += 4 + s2len
+    return (count, blen, s2len, rem), sums, pos
+
+
+def py_mux_write(data: bytes, tag: int = 0, max_message: int = CHUNK_SIZE) -> bytes:
+    """MultiplexWriter.WriteMsg (wire.go:28-36), one message per <= max_message piece."""
+    out = bytearray()
+    for at in range(0, len(data), max_message):
+        p = data[at:at + max_message]
+        out += struct.pack("<I", ((7 + tag) << 24) | len(p)) + p
+    return bytes(out)
+
+
+def py_mux_read(wire: bytes) -> bytes:
+    """MultiplexReader.ReadMsg/Read (wire.go:49-95) over a whole stream."""
+    out, at = bytearray(), 0
+    while at < len(wire):
+        (hdr,) = struct.unpack_from("<I", wire, at)
+        tag, n = ((hdr >> 24) - 7) & 0xFF, hdr & 0xFFFFFF
+        if n > CHUNK_SIZE:
+            raise ValueError(f"length {n} exceeds max message size ({CHUNK_SIZE})")
+        p = wire[at + 4:at + 4 + n]
+        if len(p) != n:
+            raise ValueError("unexpected EOF")
+        at += 4 + n
+        if tag == 0:
+            out += p
+        elif tag == 1:
+            raise ValueError(p.decode(errors="replace"))
+        elif tag != 2:
+            raise ValueError(f"unexpected tag: got {tag}, want 0")
+    return bytes(out)
+
+
+def py_write_int64(v: int) -> bytes:
+    """Buffer.WriteInt64 / Conn.WriteInt64 (wire.go:108-117)."""
+    return struct.pack("<i", v) if 0 <= v <= 0x7FFFFFFF else struct.pack("<iq", -1, v)

@@ -9,8 +9,10 @@ raises ImportError; there is no CPU fallback.
 """
 from ._lib import FILESUM_PLAIN, FILESUM_SEEDED, RsgError, SumHead  # noqa: F401  (loads librsg.so, fails loudly)
 from .engine import (RECORD_BYTES, Conn, DeviceBuffer, Engine, Plan, checksum1, checksum2,  # noqa: F401
-                     apply_tokens, default_engine, device_count, encode_tokens, reader_checksum, sum_sizes_sqroot)
+                     apply_tokens, decode_sums, default_engine, device_count, encode_sums, encode_tokens,
+                     get_int64, mux_deframe, mux_frame, put_int64, reader_checksum, sum_sizes_sqroot)
 
 __all__ = ["Engine", "Plan", "DeviceBuffer", "Conn", "SumHead", "RsgError", "RECORD_BYTES",
            "FILESUM_PLAIN", "FILESUM_SEEDED", "sum_sizes_sqroot", "checksum1", "checksum2",
-           "reader_checksum", "encode_tokens", "apply_tokens", "device_count", "default_engine"]
+           "reader_checksum", "encode_tokens", "apply_tokens", "device_count", "default_engine",
+           "encode_sums", "decode_sums", "mux_frame", "mux_deframe", "put_int64", "get_int64"]

@@ -99,6 +99,13 @@ _PROTOS = {
     "rsg_comm_unique_id": (_st, [_vp]),
     "rsg_comm_init": (_st, [_vp, _i32, _i32, _vp]),
     "rsg_gather_bytes": (_st, [_vp, _vp, ctypes.POINTER(_u64), _vp, _i32, _vp]),
+    "rsg_check_sum_head": (_st, [ctypes.POINTER(SumHead)]),
+    "rsg_encode_sums": (_st, [_vp, ctypes.POINTER(SumHead), _u64, _vp, _i32, _vp, _u64, ctypes.POINTER(_u64)]),
+    "rsg_decode_sums": (_st, [_vp, _u64, ctypes.POINTER(SumHead), _vp, _vp, _u64, ctypes.POINTER(_u64)]),
+    "rsg_mux_frame": (_st, [_vp, _u64, _i32, ctypes.c_uint32, _vp, _u64, ctypes.POINTER(_u64)]),
+    "rsg_mux_deframe": (_st, [_vp, _u64, _vp, _u64, ctypes.POINTER(_u64)]),
+    "rsg_put_int64": (_st, [ctypes.c_int64, _vp, ctypes.POINTER(_u64)]),
+    "rsg_get_int64": (_st, [_vp, _u64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(_u64)]),
 }
 
 for _name, (_res, _args) in _PROTOS.items():

@@ -366,6 +366,74 @@ def apply_tokens(stream, head, basis) -> Tuple[bytes, int]:
     return out[: n.value].tobytes(), used.value
 
 
+# ------------------------------------------------------------------ wire formats
+MSG_DATA, MSG_ERROR, MSG_INFO = 0, 1, 2  # wire.go:12-14
+
+
+def _sized(call) -> bytes:
+    """Runs a size-query/fill pair of an rsg_* formatter (out == NULL first)."""
+    n = ctypes.c_uint64()
+    check(call(None, 0, ctypes.byref(n)))
+    out = np.empty(max(n.value, 1), dtype=np.uint8)
+    check(call(_ptr(out), n.value, ctypes.byref(n)))
+    return out[: n.value].tobytes()
+
+
+def encode_sums(heads, records, file_idx: Optional[Sequence[int]] = None, terminate: bool = False) -> bytes:
+    """The generator's sums stream for a batch (generator.go:317,325-350 and the
+    phase markers at :31,40): [int32 idx] SumHead records per file."""
+    hs = [h if isinstance(h, SumHead) else SumHead(*h) for h in heads]
+    ha = (SumHead * max(len(hs), 1))(*hs)
+    r = _u8(records)
+    ix = None
+    if file_idx is not None:
+        ix = np.ascontiguousarray(np.asarray(file_idx, dtype=np.int64).astype(np.int32))
+    return _sized(lambda o, cap, n: lib.rsg_encode_sums(_ptr(ix) if ix is not None else None, ha, len(hs),
+                                                        _ptr(r), int(terminate), o, cap, n))
+
+
+def decode_sums(wire) -> Tuple[SumHead, np.ndarray, np.ndarray, int]:
+    """SumHead.ReadFrom + receiveSums (types.go:38-77, sender.go:118-151)
+    -> (head, sum1[count] u32, sum2[count,16] u8, bytes consumed)."""
+    w = _u8(wire)
+    h, used = SumHead(), ctypes.c_uint64()
+    st = lib.rsg_decode_sums(_ptr(w), w.size, ctypes.byref(h), None, None, 0, ctypes.byref(used))
+    if st != _lib.ERR_TRUNCATED:
+        check(st)
+    s1 = np.empty(max(h.count, 1), dtype=np.uint32)
+    s2 = np.empty((max(h.count, 1), 16), dtype=np.uint8)
+    check(lib.rsg_decode_sums(_ptr(w), w.size, ctypes.byref(h), _ptr(s1), _ptr(s2), h.count, ctypes.byref(used)))
+    return h, s1[: h.count], s2[: h.count], used.value
+
+
+def mux_frame(data, tag: int = MSG_DATA, max_message: int = _lib.CHUNK_SIZE) -> bytes:
+    """MultiplexWriter.WriteMsg (wire.go:28-36) in <= max_message pieces."""
+    d = _u8(data)
+    return _sized(lambda o, cap, n: lib.rsg_mux_frame(_ptr(d), d.size, tag, max_message, o, cap, n))
+
+
+def mux_deframe(wire) -> bytes:
+    """MultiplexReader (wire.go:49-95): the MsgData payloads, MsgInfo skipped."""
+    w = _u8(wire)
+    return _sized(lambda o, cap, n: lib.rsg_mux_deframe(_ptr(w), w.size, o, cap, n))
+
+
+def put_int64(v: int) -> bytes:
+    """Conn.WriteInt64 (wire.go:108-117)."""
+    out = np.empty(12, dtype=np.uint8)
+    n = ctypes.c_uint64()
+    check(lib.rsg_put_int64(v, _ptr(out), ctypes.byref(n)))
+    return out[: n.value].tobytes()
+
+
+def get_int64(b) -> Tuple[int, int]:
+    """Conn.ReadInt64 (wire.go:177-195) -> (value, bytes consumed)."""
+    a = _u8(b)
+    v, n = ctypes.c_int64(), ctypes.c_uint64()
+    check(lib.rsg_get_int64(_ptr(a), a.size, ctypes.byref(v), ctypes.byref(n)))
+    return v.value, n.value
+
+
 _default: Optional[Engine] = None
 
 
