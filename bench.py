@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--ab", action="store_true", help="A/B the block-sum kernel variants (interleaved rounds)")
-    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3"],
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4"],
                     help="cfg2 = receiver block sums (the metric); cfg3 = sender match, reported separately")
     ap.add_argument("--cfg3-files", type=int, default=10)
     return ap.parse_args()
@@ -70,6 +70,8 @@ def main():
     import rsync_amd
     if args.workload == "cfg3":
         return bench_sender(args, rank, world, local)
+    if args.workload == "cfg4":
+        return bench_mixed(args, rank, world, local)
 
     eng = rsync_amd.Engine(local)
     stream = torch.cuda.Stream(device=local)
@@ -358,6 +360,111 @@ def bench_sender(args, rank, world, local):
                                      "files": args.cfg3_files, "matches_per_pass": nm // steps},
                           "ms_per_file": round(dt * 1e3 / (steps * len(metas)), 3)}), flush=True)
     eng.close()
+
+
+def bench_mixed(args, rank, world, local):
+    """cfg4: 100 000 files of uniform length in [4096, 65536] (PRNG seed 4),
+    B = 700, block sums with the file list sharded by bytes over the ranks
+    (rsync_amd.shard.plan_shards: contiguous block ranges, so rank order of the
+    records is the global order; strong scaling, total work fixed).  Each
+    rank's pieces sit back to back at 16-byte aligned offsets of one arena; a
+    piece that starts inside a file starts on a block boundary, so it is
+    planned as a file of its own with the same blocks.  Reported beside cfg2,
+    never as the headline value."""
+    import torch
+    import torch.distributed as dist
+    import rsync_amd
+    from rsync_amd.shard import plan_shards
+    NF = 100_000
+    lengths = np.random.default_rng(4).integers(4096, 65537, NF).tolist()
+    mine = plan_shards(lengths, world, BLOCK_LEN)[rank]
+    eng = rsync_amd.Engine(local)
+    stream = torch.cuda.Stream(device=local)
+    sptr = stream.cuda_stream
+    # whole files of this rank's pieces, then each piece's block range inside
+    files = sorted({p.file for p in mine})
+    at, fpos = 0, {}
+    for f in files:
+        fpos[f] = at
+        at += (lengths[f] + 15) & ~15
+    arena_bytes = max(at, 16)
+    arenas = [eng.alloc(arena_bytes) for _ in range(2)]
+    for a in arenas:
+        for f in files:
+            eng.fill_splitmix64(a, lengths[f], f + 1, offset=fpos[f], stream=sptr)
+    desc = [(fpos[p.file] + p.offset, p.length, BLOCK_LEN) for p in mine]
+    plan = eng.plan(desc, arena_bytes)
+    recs = eng.alloc(max(plan.total_records, 1) * rsync_amd.RECORD_BYTES)
+    eng.synchronize(sptr)
+    my_bytes = sum(p.length for p in mine)
+    for i in range(max(args.warmup, 20)):
+        plan.run(arenas[i & 1], SEED, recs, stream=sptr)
+    eng.synchronize(sptr)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(args.steps):
+        plan.run(arenas[i & 1], SEED, recs, stream=sptr)
+    ev1.record(stream)
+    eng.synchronize(sptr)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    if world > 1:
+        tt = torch.tensor([wall, kernel_ms], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall, kernel_ms = float(tt[0]), float(tt[1])
+    total = sum(lengths)
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        # cpu_baseline leg: the oracle on a bounded sample of this rank's
+        # pieces, which also spot-checks the benchmarked records
+        from oracle import oracle as orc
+        lib = orc.lib()
+        t_cpu, done, k, parity = 0.0, 0, 0, True
+        first = plan.first_record
+        while t_cpu < args.cpu_seconds / 2 and k < 4 * len(mine):
+            j = k % len(mine)
+            p = mine[j]
+            data = orc.splitmix64_bytes(p.file + 1, lengths[p.file])[p.offset:p.offset + p.length]
+            data = np.ascontiguousarray(data)
+            cnt = (p.length + BLOCK_LEN - 1) // BLOCK_LEN
+            out = np.empty(cnt * 20, np.uint8)
+            c0 = time.perf_counter()
+            lib.orc_block_sums(orc._ptr(data), data.size, BLOCK_LEN, orc._i32(SEED), orc._ptr(out))
+            t_cpu += time.perf_counter() - c0
+            done += data.size
+            if k < 64:
+                parity &= bool((recs.download(cnt * 20, offset=first[j] * 20) == out).all())
+            k += 1
+        cpu = {"value": round(done / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+               "sample": f"{k} pieces of rank 0's cfg4 shard at B=700, oracle/rsg_oracle.c orc_block_sums, "
+                         f"1 thread, {t_cpu:.1f} s", "gpu_parity_on_sample": parity}
+    if rank == 0:
+        algo = my_bytes + plan.total_records * rsync_amd.RECORD_BYTES
+        print(json.dumps({
+            "metric": "GiB/s block-checksummed (weak+MD4), device-resident, at 1/2/4/8 MI355X",
+            "value": round(total * args.steps / wall / GIB, 2), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall * 1e3 / args.steps, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (splitmix64 bytes generated on device)",
+            "config": {"workload": "cfg4: 100k files, lengths uniform in [4096, 65536], B=700, block sums, "
+                                   "file list sharded by bytes", "files": NF, "total_bytes": total,
+                       "rank0_pieces": len(mine), "rank0_records": plan.total_records,
+                       "parallelism": f"file list sharded, {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": round(algo / (kernel_ms * 1e-3) / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(algo / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": int(algo)},
+            "cpu_baseline": cpu}), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
