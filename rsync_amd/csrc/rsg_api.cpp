@@ -505,6 +505,17 @@ rsg_status rsg_block_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfi
         if ((s = ensure_pin(ctx, ctx->h_out[k], max_recs * kRecordBytes)) != RSG_OK) return s;
         if ((s = ensure_pin(ctx, ctx->h_desc[k], desc_bytes)) != RSG_OK) return s;
     }
+    constexpr size_t kDirectPieces = 1024;  // per-piece DMA calls stay cheap up to here
+    std::vector<int8_t> pinned(nfiles, -1);
+    auto is_pinned = [&](uint64_t i) -> bool {
+        if (pinned[i] < 0) {
+            hipPointerAttribute_t a{};
+            const hipError_t e = files[i].len ? hipPointerGetAttributes(&a, files[i].data) : hipErrorInvalidValue;
+            if (e != hipSuccess) (void)hipGetLastError();  // plain pageable memory: not an error
+            pinned[i] = (e == hipSuccess && a.type == hipMemoryTypeHost) ? 1 : 0;
+        }
+        return pinned[i] == 1;
+    };
     int64_t pending[2] = {-1, -1};  // batch index in flight per slot
     auto drain = [&](int slot) -> rsg_status {
         if (pending[slot] < 0) return RSG_OK;
@@ -535,7 +546,12 @@ rsg_status rsg_block_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfi
             vf[j].block_len = (int32_t)B;
             off += ((end - start) + 15) & ~15ull;
         }
-        parallel_copy(copies);
+        // Pieces whose source already lies in page-locked memory (the
+        // caller read the files into rsg_alloc_pinned buffers)
+        // go to HBM by DMA straight from there: no staging copy.
+        bool direct = b.pieces.size() <= kDirectPieces;
+        for (size_t j = 0; direct && j < b.pieces.size(); j++) direct = is_pinned(b.pieces[j].file);
+        if (!direct) parallel_copy(copies);
         HostPlan plan;
         if ((s = build_plan(ctx, vf.data(), vf.size(), off, true, plan)) != RSG_OK) return s;
         uint8_t *hd = (uint8_t *)ctx->h_desc[slot].p;
@@ -546,7 +562,13 @@ rsg_status rsg_block_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfi
         hipStream_t st = ctx->side[slot];
         uint8_t *dd = (uint8_t *)ctx->d_desc[slot].p;
         RSG_HIP(ctx, hipMemcpyAsync(dd, hd, wg_off + plan.wg_file.size() * 4, hipMemcpyHostToDevice, st));
-        RSG_HIP(ctx, hipMemcpyAsync(ctx->d_in[slot].p, stage, off, hipMemcpyHostToDevice, st));
+        if (direct) {
+            for (size_t j = 0; j < copies.size(); j++)
+                RSG_HIP(ctx, hipMemcpyAsync((uint8_t *)ctx->d_in[slot].p + vf[j].offset, copies[j].src, copies[j].n,
+                                            hipMemcpyHostToDevice, st));
+        } else {
+            RSG_HIP(ctx, hipMemcpyAsync(ctx->d_in[slot].p, stage, off, hipMemcpyHostToDevice, st));
+        }
         if ((s = launch_plan(ctx, plan, dd, dd + wg_off, ctx->d_in[slot].p, seed, ctx->d_out[slot].p,
                              ctx->d_fb[slot].p, st)) != RSG_OK)
             return s;

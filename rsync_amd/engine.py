@@ -176,6 +176,18 @@ class Engine:
     def alloc(self, nbytes: int) -> DeviceBuffer:
         return DeviceBuffer(self, nbytes)
 
+    def alloc_pinned(self, nbytes: int) -> np.ndarray:
+        """Page-locked host memory (rsg_alloc_pinned) as a uint8 array.  Files
+        read into it go to HBM by DMA with no staging copy.  Release with
+        free_pinned(arr) before the engine closes."""
+        p = ctypes.c_void_p()
+        check(lib.rsg_alloc_pinned(self.ctx, max(nbytes, 1), ctypes.byref(p)), self.ctx)
+        buf = (ctypes.c_uint8 * max(nbytes, 1)).from_address(p.value)
+        return np.frombuffer(buf, dtype=np.uint8)[:nbytes]
+
+    def free_pinned(self, arr: np.ndarray):
+        check(lib.rsg_free_pinned(self.ctx, ctypes.c_void_p(arr.ctypes.data)), self.ctx)
+
     def fill_splitmix64(self, buf: DeviceBuffer, nbytes: int, seed: int, offset: int = 0, stream=None):
         check(lib.rsg_fill_splitmix64(self.ctx, ctypes.c_void_p(buf.ptr + offset), nbytes, seed & (2**64 - 1),
                                       ctypes.c_void_p(stream or 0)), self.ctx)
