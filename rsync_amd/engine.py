@@ -246,6 +246,20 @@ class Engine:
         conn.write(rec)
         return h
 
+    def generate_files(self, conn: Conn, files: Sequence, seed: int, block_len=0, s2len: int = 16,
+                       mux: bool = False) -> List[SumHead]:
+        """GenerateFiles (generator.go:20-41) for a file list whose every entry
+        goes to generateAndSendSums (regular files with a basis, -I): one
+        batched kernel call, then the whole sums stream -- idx, SumHead and
+        records per file, the two -1 phase markers -- in one buffer, framed in
+        <= 256 KiB MsgData messages when mux (the server side, wire.go:28-36)."""
+        heads, rec, _ = self.block_sums(files, seed, block_len)
+        if s2len != 16:
+            heads = [SumHead(h.count, h.block_len, s2len, h.rem) for h in heads]
+        stream = encode_sums(heads, rec, file_idx=range(len(heads)), terminate=True)
+        conn.write(mux_frame(stream) if mux else stream)
+        return heads
+
     # ------------------------------------------------------------ whole-file sums
     def file_sums(self, files: Sequence, mode: int = _lib.FILESUM_PLAIN, seed: int = 0) -> List[bytes]:
         """Whole-file MD4 of each host buffer, one GPU lane per file:

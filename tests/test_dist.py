@@ -96,3 +96,25 @@ def test_plan_shards_partition(world):
     total = sum(lens)
     for s in shards:
         assert sum(p.length for p in s) <= total / world + 700
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_cfg4_shard_plan(world):
+    """bench.py --workload cfg4's plan: 100k files of 4-64 KiB at B = 700 cut
+    into `world` contiguous ranges that cover every block exactly once, in
+    global order, each within one block (+ one file tail) of the byte share."""
+    from rsync_amd.shard import file_heads, plan_shards
+    lengths = np.random.default_rng(4).integers(4096, 65537, 100_000).tolist()
+    shards = plan_shards(lengths, world, 700)
+    heads = file_heads(lengths, 700)
+    flat = [p for s in shards for p in s]
+    expect = [(f, b) for f, h in enumerate(heads) for b in [0]]  # every file starts once
+    assert sum(p.b1 - p.b0 for p in flat) == sum(h.count for h in heads)
+    nxt = {}
+    for p in flat:  # contiguity: each piece continues where the last one of its file ended
+        assert p.b0 == nxt.get(p.file, 0) and p.offset == p.b0 * 700
+        nxt[p.file] = p.b1
+    assert all(nxt[f] == h.count for f, h in enumerate(heads)) and len(nxt) == len(expect)
+    share = sum(lengths) / world
+    for s in shards:
+        assert abs(sum(p.length for p in s) - share) <= 2 * 700 + 65536

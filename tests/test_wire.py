@@ -164,3 +164,21 @@ def test_gpu_records_to_wire_and_back():
         assert (s1 == r1).all() and (s2 == r2).all()
         at += 4 + used
     assert stream[at:] == struct.pack("<ii", -1, -1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mux,s2len", [(False, 16), (True, 16), (True, 4)])
+def test_gpu_generate_files(mux, s2len):
+    """Engine.generate_files = the generator's whole output for a batch,
+    byte-identical to the oracle's GenerateFiles restatement (after demux)."""
+    import rsync_amd
+    files = _files(9)
+    conn = rsync_amd.Conn()
+    with rsync_amd.Engine(0) as eng:
+        eng.generate_files(conn, files, SEED, 700, s2len=s2len, mux=mux)
+    got = bytes(conn.buf)
+    if mux:
+        hdr = struct.unpack_from("<I", got)[0]
+        assert hdr >> 24 == 7 and (hdr & 0xFFFFFF) <= 1 << 18  # MsgData, <= 256 KiB
+        got = rsync_amd.mux_deframe(got)
+    assert got == orc.py_generate_files_stream(files, SEED, [700] * len(files), s2len=s2len)
