@@ -126,7 +126,8 @@ def main():
         from rsync_amd import _lib
         names = {1: "staged_k1", 7: "staged_k1_trim", 2: "staged_k4", 8: "staged_k4_trim", 19: "diag_staged_trim_memory_only",
                  10: "diag_staged_memory_only", 15: "diag_staged_line_aligned_memory",
-                 11: "diag_staged_hash_only", 13: "diag_linear_read", 14: "diag_linear_read_ldsdma"}
+                 11: "diag_staged_hash_only", 13: "diag_linear_read", 14: "diag_linear_read_ldsdma",
+                 16: "diag_staged_packed_768_memory"}
         res = {v: [] for v in names}
         for _ in range(5):
             for v in names:
@@ -377,6 +378,19 @@ def bench_sender(args, rank, world, local):
     eng.close()
 
 
+def cfg4_traffic(world, records):
+    """Rank 0's HBM bytes per launch from the committed PMC pass (1 GPU only):
+    FETCH_SIZE x 2 (gfx950) + the records written (the WRITE_SIZE pass of that
+    run did not complete, see profiles/r01c_cfg4_pmc_fetch.json)."""
+    if world != 1:
+        return None
+    try:
+        t = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
+        return int(t["block_sums_kernel_cfg4_fetch_bytes_per_launch"]) + records * 20
+    except Exception:
+        return None
+
+
 def bench_mixed(args, rank, world, local):
     """cfg4: 100 000 files of uniform length in [4096, 65536] (PRNG seed 4),
     B = 700, block sums with the file list sharded by bytes over the ranks
@@ -474,7 +488,8 @@ def bench_mixed(args, rank, world, local):
                        "parallelism": f"file list sharded, {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": round(algo / (kernel_ms * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(algo / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(algo / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": cfg4_traffic(world, plan.total_records),
                          "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": int(algo)},
             "cpu_baseline": cpu}), flush=True)
     eng.close()
