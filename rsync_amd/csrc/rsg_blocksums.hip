@@ -340,7 +340,7 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 // belong to the same lane the two uses are one segment apart and the second
 // is an L2 hit, whereas across lanes they are a whole block apart and the line
 // is often refetched from HBM.  K = 4 cuts those refetches by 4x.
-template <int K, int MODE, bool TRIM = false>
+template <int K, int MODE, bool TRIM = false, int DEPTH = 1>
 __device__ __forceinline__ void staged_tile(
     uint32_t tile, uint8_t *slab_all, const uint8_t *__restrict__ arena, uint64_t arena_bytes,
     const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file, uint32_t nwg256,
@@ -349,7 +349,7 @@ __device__ __forceinline__ void staged_tile(
     // readfirstlane: provably wave-uniform values keep the LDS base (M0) and
     // the buffer descriptor in SGPRs (no waterfall loops around the DMA).
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint8_t *slab = slab_all + wave * kWaveSlab;
+    uint8_t *slab = slab_all + wave * kWaveSlab * DEPTH;
     const uint64_t wave_first = ((uint64_t)tile * (kBlockSumThreads / 64) + wave) * 64u * K;
     const uint64_t g0 = wave_first + (uint64_t)lane * K;
 
@@ -469,6 +469,49 @@ __device__ __forceinline__ void staged_tile(
                 rsrc, (__attribute__((address_space(3))) void *)(slab + 1024u * i), 16, voff[i], kSegBytes * s, 0, 0);
     };
     uint32_t R[64];
+    if constexpr (DEPTH == 2) {
+        // Two slabs per wave: while segment s is hashed, segments s+1 and s+2
+        // are both in flight (the single-slab schedule below keeps only s+1
+        // in flight, so a wave's queue runs dry while it hashes).  K == 1.
+        static_assert(K == 1 && MODE == 0 && !TRIM, "depth-2 schedule: K = 1 product kernel only");
+        static_assert(kDmaPerSeg == 17, "the vmcnt immediate below is kDmaPerSeg");
+        const uint32_t S0 = S[0], nk = n[0], nfull = nk >> 6;
+        build_voff(0);
+        auto dma_into = [&](uint32_t s, uint8_t *dst) {
+#pragma unroll
+            for (uint32_t i = 0; i < kDmaPerSeg; i++)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * i), 16, voff[i], kSegBytes * s, 0, 0);
+        };
+        dma_into(0, slab);
+        if (S0 > 1) dma_into(1, slab + kWaveSlab);
+        uint32_t h[4];
+        md4_init(h);
+        int32_t s1 = 0;
+        uint32_t t = 0;
+#pragma unroll 1
+        for (uint32_t cs = 0; cs < S0; cs++) {
+            uint8_t *buf = slab + (cs & 1u) * kWaveSlab;
+            if (cs + 1 < S0) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");  // segment cs landed, cs+1 may fly
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint8_t *mine2 = buf + lane * kPiece;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(mine2 + 16 * q);
+                R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab read out before it is refilled
+            if (cs + 2 < S0) dma_into(cs + 2, buf);
+#pragma unroll
+            for (uint32_t i = 0; i < 4; i++) {
+                const uint32_t c = 4u * cs + i;
+                if (c < nfull) hash_chunk<true>(R + 16 * i, 0u, 0u, c, h, s1, t);
+                else if (c == nfull) hash_tail<true>(R + 16 * i, 0u, 0u, nk, seed, h, s1, t);
+            }
+        }
+        store_record(out, g0, nk, s1, t, h);
+        return;
+    }
     const uint8_t *mine = slab + lane * kPiece;
     auto read_segment = [&]() {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -547,6 +590,16 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     uint8_t *__restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * kWaveSlab];
     staged_tile<K, MODE, TRIM>(blockIdx.x, slab_all, arena, arena_bytes, files, wg_file, nwg256, total_blocks, seed, out);
+}
+
+// Variant 20: the depth-2 schedule (two slabs per wave, 136 KiB of LDS per
+// 4-wave workgroup, so one workgroup = one wave per SIMD per CU).
+__global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged2(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * kWaveSlab * 2];
+    staged_tile<1, 0, false, 2>(blockIdx.x, slab_all, arena, arena_bytes, files, wg_file, nwg256, total_blocks, seed, out);
 }
 
 // ---------------------------------------------------------------- line-ring layout
@@ -1012,7 +1065,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     // aligned blocks, tools/blocklen_sweep.py); unaligned batches (the sender's
     // confirmation windows) take the deep-prefetch kernel when blocks are long
     if (v == -1) v = aligned ? 1 : (max_blen >= kLongBlockBytes ? 9 : 0);
-    if (!aligned && v < 13 && v != 9) v = 0;
+    if (!aligned && ((v < 13 && v != 9) || v == 20)) v = 0;
     if ((v == 3 || v == 4 || v == 12 || v == 17) && max_blen > kRegMaxBytes) v = 1;
     if ((v == 4 || v == 17) && !scratch) v = 1;
     dim3 grid(nwg), block(kBlockSumThreads);
@@ -1027,6 +1080,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             else RSG_LAUNCH(block_sums_direct<false>, grid);
             break;
         case 2: RSG_STAGED(4, 0); break;
+        case 20:
+            hipLaunchKernelGGL(block_sums_staged2, dim3((uint32_t)((total_blocks + 255u) / 256u)), block, 0, stream,
+                               arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+            break;
         case 9: {
             dim3 g64((uint32_t)((total_blocks + 63) / 64)), b64(64);
             if (aligned)
