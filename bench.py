@@ -41,9 +41,9 @@ SEED = 0x1BADB002
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--warmup-ms", type=float, default=60.0,
+    ap.add_argument("--warmup-ms", type=float, default=200.0,
                     help="keep warming up (beyond --warmup steps) until this much time has passed: the "
                          "GPU takes ~15 ms of back-to-back launches to reach its steady memory clock")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU baseline sample")
@@ -124,7 +124,7 @@ def main():
     extra = {}
     if args.ab:
         from rsync_amd import _lib
-        names = {1: "staged_k1", 20: "staged_k1_depth2", 7: "staged_k1_trim", 2: "staged_k4", 8: "staged_k4_trim", 19: "diag_staged_trim_memory_only",
+        names = {1: "staged_k1", 20: "staged_k1_depth2", 21: "staged_half_depth2", 7: "staged_k1_trim", 2: "staged_k4", 8: "staged_k4_trim", 19: "diag_staged_trim_memory_only",
                  10: "diag_staged_memory_only", 15: "diag_staged_line_aligned_memory",
                  11: "diag_staged_hash_only", 13: "diag_linear_read", 14: "diag_linear_read_ldsdma",
                  16: "diag_staged_packed_768_memory"}

@@ -592,6 +592,104 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     staged_tile<K, MODE, TRIM>(blockIdx.x, slab_all, arena, arena_bytes, files, wg_file, nwg256, total_blocks, seed, out);
 }
 
+// Variant 21: depth 2 at the single-slab LDS budget.  Segments are 128 bytes
+// (2 MD4 chunks) of every block, two of them per wave in flight in two
+// 64 x 144-byte slabs (18 KiB per wave, as the 256-byte single slab), so the
+// workgroup keeps two waves per SIMD while the queue never runs dry.
+constexpr uint32_t kHSeg = 128;
+constexpr uint32_t kHPiece = kHSeg + 16;
+constexpr uint32_t kHSlab = 64 * kHPiece;     // 9216 bytes
+constexpr uint32_t kHDma = kHSlab / 1024;     // 9 DMA instructions per segment
+static_assert(kHSlab % 1024 == 0 && kHDma == 9, "vmcnt immediate below is kHDma");
+
+__global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged_half(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * kHSlab * 2];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t *slab = slab_all + wave * kHSlab * 2;
+    const uint64_t g = ((uint64_t)blockIdx.x * (kBlockSumThreads / 64) + wave) * 64u + lane;
+    uint64_t off = 0;
+    uint32_t n = 0;
+    {
+        uint32_t lo = wg_file[blockIdx.x], hi = wg_file[min(blockIdx.x + 1, nwg256)];
+        const uint64_t gq = g < total_blocks ? g : total_blocks - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (files[mid].first_block <= gq) lo = mid; else hi = mid - 1;
+        }
+        const DevFile F = files[lo];
+        if (g < total_blocks) {
+            const uint64_t boff = (g - F.first_block) * F.blen;
+            const uint64_t left = F.len - boff;
+            n = left < F.blen ? (uint32_t)left : F.blen;  // generator.go:334
+            off = F.offset + boff;
+        }
+    }
+    const uint32_t S = __builtin_amdgcn_readfirstlane((uint32_t)wave_max_u64(n ? (n >> 7) + 1 : 0));
+    const uint64_t base_v = wave_min_u64(n ? off : ~0ull);
+    const uint64_t base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(base_v >> 32)) << 32) |
+                          __builtin_amdgcn_readfirstlane((uint32_t)base_v);
+    const uint64_t top = wave_max_u64(n ? off + (uint64_t)kHSeg * S : 0);
+    const uint64_t wave_first = g - lane;
+    const bool staged = (wave_first + 63 < total_blocks) && top <= arena_bytes && (top - base) <= 0x7FFFFFFFull;
+    uint32_t h[4];
+    md4_init(h);
+    int32_t s1 = 0;
+    uint32_t t = 0;
+    if (!staged) {
+        if (n) {
+            hash_block_direct<true>(arena, (uintptr_t)(arena + arena_bytes), off, n, seed, h, s1, t);
+            store_record(out, g, n, s1, t, h);
+        }
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(arena + base), (short)0, 0x7FFFFFFF, 0x00020000);
+    const uint32_t rel = (uint32_t)(off - base);
+    uint32_t voff[kHDma];
+#pragma unroll
+    for (uint32_t i = 0; i < kHDma; i++) {
+        const uint32_t idx = 64u * i + lane;
+        const uint32_t j = idx / 9u, u = idx - 9u * j;
+        const uint32_t v = __shfl(rel, (int)j, 64) + 16u * u;
+        voff[i] = u < 8u ? v : 0x80000000u;  // pad slot: out of range, no memory request
+    }
+    auto dma_into = [&](uint32_t s, uint8_t *dst) {
+#pragma unroll
+        for (uint32_t i = 0; i < kHDma; i++)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * i), 16, voff[i], kHSeg * s, 0, 0);
+    };
+    dma_into(0, slab);
+    if (S > 1) dma_into(1, slab + kHSlab);
+    const uint32_t nfull = n >> 6;
+    uint32_t R[32];
+#pragma unroll 1
+    for (uint32_t cs = 0; cs < S; cs++) {
+        uint8_t *buf = slab + (cs & 1u) * kHSlab;
+        if (cs + 1 < S) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // segment cs landed, cs+1 may fly
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint8_t *mine = buf + lane * kHPiece;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
+            R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab read out before it is refilled
+        if (cs + 2 < S) dma_into(cs + 2, buf);
+#pragma unroll
+        for (uint32_t i = 0; i < 2; i++) {
+            const uint32_t c = 2u * cs + i;
+            if (c < nfull) hash_chunk<true>(R + 16 * i, 0u, 0u, c, h, s1, t);
+            else if (c == nfull) hash_tail<true>(R + 16 * i, 0u, 0u, n, seed, h, s1, t);
+        }
+    }
+    if (n) store_record(out, g, n, s1, t, h);
+}
+
 // Variant 20: the depth-2 schedule (two slabs per wave, 136 KiB of LDS per
 // 4-wave workgroup, so one workgroup = one wave per SIMD per CU).
 __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged2(
@@ -1065,7 +1163,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     // aligned blocks, tools/blocklen_sweep.py); unaligned batches (the sender's
     // confirmation windows) take the deep-prefetch kernel when blocks are long
     if (v == -1) v = aligned ? 1 : (max_blen >= kLongBlockBytes ? 9 : 0);
-    if (!aligned && ((v < 13 && v != 9) || v == 20)) v = 0;
+    if (!aligned && ((v < 13 && v != 9) || v >= 20)) v = 0;
     if ((v == 3 || v == 4 || v == 12 || v == 17) && max_blen > kRegMaxBytes) v = 1;
     if ((v == 4 || v == 17) && !scratch) v = 1;
     dim3 grid(nwg), block(kBlockSumThreads);
@@ -1080,6 +1178,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             else RSG_LAUNCH(block_sums_direct<false>, grid);
             break;
         case 2: RSG_STAGED(4, 0); break;
+        case 21:
+            hipLaunchKernelGGL(block_sums_staged_half, dim3((uint32_t)((total_blocks + 255u) / 256u)), block, 0, stream,
+                               arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+            break;
         case 20:
             hipLaunchKernelGGL(block_sums_staged2, dim3((uint32_t)((total_blocks + 255u) / 256u)), block, 0, stream,
                                arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
