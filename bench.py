@@ -124,7 +124,7 @@ def main():
     extra = {}
     if args.ab:
         from rsync_amd import _lib
-        names = {1: "staged_k1", 20: "staged_k1_depth2", 21: "staged_half_depth2", 7: "staged_k1_trim", 2: "staged_k4", 8: "staged_k4_trim", 19: "diag_staged_trim_memory_only",
+        names = {1: "staged_k1", 20: "staged_k1_depth2", 21: "staged_half_depth2", 22: "diag_whole_block_tile_memory", 23: "staged_k1_a16", 7: "staged_k1_trim", 2: "staged_k4", 8: "staged_k4_trim", 19: "diag_staged_trim_memory_only",
                  10: "diag_staged_memory_only", 15: "diag_staged_line_aligned_memory",
                  11: "diag_staged_hash_only", 13: "diag_linear_read", 14: "diag_linear_read_ldsdma",
                  16: "diag_staged_packed_768_memory"}

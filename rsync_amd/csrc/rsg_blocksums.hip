@@ -340,7 +340,7 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 // belong to the same lane the two uses are one segment apart and the second
 // is an L2 hit, whereas across lanes they are a whole block apart and the line
 // is often refetched from HBM.  K = 4 cuts those refetches by 4x.
-template <int K, int MODE, bool TRIM = false, int DEPTH = 1>
+template <int K, int MODE, bool TRIM = false, int DEPTH = 1, bool A16 = false>
 __device__ __forceinline__ void staged_tile(
     uint32_t tile, uint8_t *slab_all, const uint8_t *__restrict__ arena, uint64_t arena_bytes,
     const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file, uint32_t nwg256,
@@ -396,11 +396,11 @@ __device__ __forceinline__ void staged_tile(
     for (int k = 0; k < K; k++) {
         if (n[k]) {
             lo_off = off[k] < lo_off ? off[k] : lo_off;
-            const uint64_t e = off[k] + (uint64_t)kSegBytes * S[k];
+            const uint64_t e = off[k] + (uint64_t)kSegBytes * S[k] + (A16 ? 16u : 0u);
             hi_end = e > hi_end ? e : hi_end;
         }
     }
-    const uint64_t base_v = wave_min_u64(lo_off);
+    const uint64_t base_v = wave_min_u64(lo_off) & (A16 ? ~15ull : ~0ull);
     const uint64_t base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(base_v >> 32)) << 32) |
                           __builtin_amdgcn_readfirstlane((uint32_t)base_v);
     const uint64_t top = wave_max_u64(hi_end);
@@ -442,8 +442,11 @@ __device__ __forceinline__ void staged_tile(
         for (uint32_t i = 0; i < kDmaPerSeg; i++) {
             const uint32_t idx = 64u * i + lane;
             const uint32_t j = idx / 17u, u = idx - 17u * j;
-            const uint32_t v = __shfl(r, (int)j, 64) + 16u * u;
-            voff[i] = u < 16u ? v : 0x80000000u;  // pad slot: out of range, no memory request
+            const uint32_t v = __shfl(A16 ? (r & ~15u) : r, (int)j, 64) + 16u * u;
+            // pad slot: out of range, no memory request.  A16: pieces start
+            // on the 16-byte unit below the block's bytes, so every DMA lane
+            // is one aligned 16-byte request, and the 17th unit is data.
+            voff[i] = (A16 || u < 16u) ? v : 0x80000000u;
         }
     };
     // TRIM: the last segment of a block is cut at the block's end (16-byte
@@ -512,13 +515,20 @@ __device__ __forceinline__ void staged_tile(
         store_record(out, g0, nk, s1, t, h);
         return;
     }
-    const uint8_t *mine = slab + lane * kPiece;
+    const uint8_t *mine = slab + lane * kPiece + (A16 ? (rel[0] & 15u) : 0u);
     auto read_segment = [&]() {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (A16) {
+            static_assert(K == 1, "A16: one block per lane");
+            const uint32_t *w = reinterpret_cast<const uint32_t *>(mine);
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
-            R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+            for (int q = 0; q < 64; q++) R[q] = w[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
+                R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+            }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
@@ -688,6 +698,78 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged_half(
         }
     }
     if (n) store_record(out, g, n, s1, t, h);
+}
+
+// Variant 22 (timing diagnostic, outputs meaningless): the memory pattern of
+// a whole-block tile.  A one-wave workgroup DMAs its 64 blocks (B <= 704) in a
+// single pass into a 64 x 720-byte LDS tile -- every byte of the wave's span
+// is requested in one burst of 45 instructions -- then folds the tile.  Asks
+// whether reading a span in one pass restores the linear read's DRAM
+// efficiency that the three-pass staged pattern loses.
+constexpr uint32_t kTPiece = 720;
+constexpr uint32_t kTDma = 64 * kTPiece / 1024;  // 45
+static_assert(64 * kTPiece % 1024 == 0, "tile must be whole DMA instructions");
+
+__global__ __launch_bounds__(64) void block_sums_diag_tile(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t tile[64 * kTPiece];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t g = (uint64_t)blockIdx.x * 64u + lane;
+    const uint32_t wg256 = (uint32_t)(g / 256u);
+    uint64_t off = 0;
+    uint32_t n = 0;
+    {
+        uint32_t lo = wg_file[wg256], hi = wg_file[min(wg256 + 1, nwg256)];
+        const uint64_t gq = g < total_blocks ? g : total_blocks - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (files[mid].first_block <= gq) lo = mid; else hi = mid - 1;
+        }
+        const DevFile F = files[lo];
+        if (g < total_blocks) {
+            const uint64_t boff = (g - F.first_block) * F.blen;
+            const uint64_t left = F.len - boff;
+            n = left < F.blen ? (uint32_t)left : F.blen;
+            off = F.offset + boff;
+        }
+    }
+    const uint64_t base_v = wave_min_u64(n ? off : ~0ull);
+    const uint64_t base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(base_v >> 32)) << 32) |
+                          __builtin_amdgcn_readfirstlane((uint32_t)base_v);
+    const uint64_t top = wave_max_u64(n ? off + 704u : 0);
+    if (!(g - lane + 63 < total_blocks && top <= arena_bytes && n <= 704u)) return;  // diagnostic: skip edge waves
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(arena + base), (short)0, 0x7FFFFFFF, 0x00020000);
+    const uint32_t rel = (uint32_t)(off - base);
+#pragma unroll 5
+    for (uint32_t i = 0; i < kTDma; i++) {
+        const uint32_t idx = 64u * i + lane;
+        const uint32_t j = idx / 45u, u = idx - 45u * j;
+        const uint32_t v = __shfl(rel, (int)j, 64) + 16u * u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(tile + 1024u * i), 16,
+                                                 u < 44u ? v : 0x80000000u, 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t h[4] = {0, 0, 0, 0};
+    const uint8_t *mine = tile + lane * kTPiece;
+#pragma unroll
+    for (int q = 0; q < 44; q++) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
+        h[0] ^= v.x; h[1] ^= v.y; h[2] ^= v.z; h[3] ^= v.w;
+    }
+    store_record(out, g, n, (int32_t)seed, 0u, h);
+}
+
+// Variant 23: the staged kernel with 16-byte aligned DMA units (A16).
+__global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged_a16(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * kWaveSlab];
+    staged_tile<1, 0, false, 1, true>(blockIdx.x, slab_all, arena, arena_bytes, files, wg_file, nwg256, total_blocks,
+                                      seed, out);
 }
 
 // Variant 20: the depth-2 schedule (two slabs per wave, 136 KiB of LDS per
@@ -1178,6 +1260,14 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             else RSG_LAUNCH(block_sums_direct<false>, grid);
             break;
         case 2: RSG_STAGED(4, 0); break;
+        case 23:
+            hipLaunchKernelGGL(block_sums_staged_a16, dim3((uint32_t)((total_blocks + 255u) / 256u)), block, 0, stream,
+                               arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+            break;
+        case 22:
+            hipLaunchKernelGGL(block_sums_diag_tile, dim3((uint32_t)((total_blocks + 63u) / 64u)), dim3(64), 0, stream,
+                               arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+            break;
         case 21:
             hipLaunchKernelGGL(block_sums_staged_half, dim3((uint32_t)((total_blocks + 255u) / 256u)), block, 0, stream,
                                arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
