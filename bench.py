@@ -124,10 +124,13 @@ def main():
     extra = {}
     if args.ab:
         from rsync_amd import _lib
-        names = {1: "staged_k1", 20: "staged_k1_depth2", 21: "staged_half_depth2", 22: "diag_whole_block_tile_memory", 23: "staged_k1_a16", 7: "staged_k1_trim", 2: "staged_k4", 8: "staged_k4_trim", 19: "diag_staged_trim_memory_only",
-                 10: "diag_staged_memory_only", 15: "diag_staged_line_aligned_memory",
-                 11: "diag_staged_hash_only", 13: "diag_linear_read", 14: "diag_linear_read_ldsdma",
-                 16: "diag_staged_packed_768_memory"}
+        names = {1: "staged_k1", 24: "cring_r1_s1_w8", 25: "cring_r2_s1_w5", 26: "cring_r3_s1_w3",
+                 27: "cring_r1_s2_w5", 28: "cring_r2_s2_w2", 29: "diag_cring_r1_s1_memory",
+                 30: "diag_cring_r1_s1_hash", 31: "diag_cring_r2_s1_memory", 32: "diag_cring_r2_s1_hash",
+                 33: "diag_cring_r1_s2_memory", 10: "diag_staged_memory_only", 11: "diag_staged_hash_only",
+                 14: "diag_linear_read_ldsdma"}
+        if os.environ.get("RSG_AB"):
+            names = {int(k): f"variant_{k}" for k in os.environ["RSG_AB"].split(",")}
         res = {v: [] for v in names}
         for _ in range(5):
             for v in names:
@@ -143,6 +146,8 @@ def main():
                 eng.synchronize(sptr)
                 res[v].append(a0.elapsed_time(a1) / args.steps)
         _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+        step(0)  # the records hold the product kernel's output again (diagnostics write garbage)
+        eng.synchronize(sptr)
         extra["ab_kernel_ms"] = {names[v]: [round(x, 4) for x in sorted(res[v])] for v in names}
 
     in_bytes = float(arena_bytes)

@@ -602,6 +602,164 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     staged_tile<K, MODE, TRIM>(blockIdx.x, slab_all, arena, arena_bytes, files, wg_file, nwg256, total_blocks, seed, out);
 }
 
+// ---------------------------------------------------------------- chunk-ring variant
+// Occupancy first.  The staged kernel above holds 4 chunks of every lane's
+// block in VGPRs (R[64]) and a 17 KiB slab per wave, so it runs at 2 waves per
+// SIMD -- and MD4's serial chain then leaves the VALU idle most of the time
+// (hashing alone: ~4.9 cycles per wave-instruction per SIMD against a 2-cycle
+// issue rate).  Here a lane keeps only the chunk it is hashing in VGPRs; the
+// wave's LDS is a ring of R slots, slot = SEGC 64-byte chunks of each of the
+// 64 blocks (4 KiB per chunk), filled by LDS DMA R segments ahead.  Small
+// slots buy waves: R = 1, SEGC = 1 is 4 KiB per wave.
+//
+// Slot layout: lane j's piece at j * 64 * SEGC, its 16-byte quads rotated by
+// f(j) (quad q of the block's segment sits at position (q + f(j)) % Q) so the
+// per-lane ds_read_b128 of one quad is conflict-free in every 16-lane group.
+// The rotation is applied on the DMA side: the DMA lane writing position p of
+// lane j's piece fetches quad (p - f(j)) % Q of the block.
+template <int SEGC>
+struct CRing {
+    static constexpr uint32_t kQ = 4 * SEGC;                 // quads per lane piece
+    static constexpr uint32_t kPieceB = 64 * SEGC;           // bytes per lane piece
+    static constexpr uint32_t kSlotB = 64 * kPieceB;         // bytes per slot (64 lanes)
+    static constexpr uint32_t kDma = kSlotB / 1024;          // DMA instructions per slot
+    static constexpr uint32_t kShift = SEGC == 1 ? 2 : SEGC == 2 ? 1 : 0;  // f(j) = (j >> kShift) % kQ
+    __device__ static uint32_t rot(uint32_t j) { return (j >> kShift) & (kQ - 1); }
+};
+
+// Segment S_ of the wave's 64 blocks into ring slot S_ % R (C::kDma LDS-DMA
+// instructions; the segment advance rides in the scalar offset).  Every
+// builtin argument is of a non-dependent type: hipcc 7.2's host pass silently
+// drops the kernel stub of a template whose builtin call has a
+// type-dependent argument (e.g. C::kPieceB * s).
+#define RSG_CRING_DMA(S_)                                                                                   \
+    do {                                                                                                    \
+        uint8_t *slot_ = ring + ((S_) % R) * C::kSlotB;                                                     \
+        const uint32_t so_ = (uint32_t)(C::kPieceB * (S_));                                                 \
+        _Pragma("unroll") for (uint32_t i_ = 0; i_ < C::kDma; i_++)                                         \
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                       \
+                rsrc, (__attribute__((address_space(3))) void *)(slot_ + 1024u * i_), 16, (uint32_t)voff[i_], so_, 0, 0); \
+    } while (0)
+
+// MODE 0 = product; timing diagnostics (outputs meaningless): 1 = DMA + LDS
+// reads only, 2 = hashing only (no DMA).  WPS = waves per SIMD the launch
+// bound asks for (the LDS of the ring must allow as many workgroups).
+template <int R, int SEGC, int MODE, int WPS>
+__global__ __launch_bounds__(kBlockSumThreads, WPS) void block_sums_cring(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    using C = CRing<SEGC>;
+    constexpr uint32_t kWaveB = R * C::kSlotB;
+    __shared__ __attribute__((aligned(16))) uint8_t ring_all[(kBlockSumThreads / 64) * kWaveB];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t *ring = ring_all + wave * kWaveB;
+    const uint64_t wave_first = (uint64_t)blockIdx.x * kBlockSumThreads + wave * 64u;
+    const uint64_t g = wave_first + lane;
+
+    uint64_t off = 0;
+    uint32_t n = 0;
+    if (g < total_blocks) locate_block(files, wg_file, g, off, n);
+    (void)nwg256;
+    const uint32_t nfull = n >> 6;
+    // segments through the tail chunk (chunk nfull holds the last n % 64 bytes)
+    const uint32_t nseg = n ? (nfull + SEGC) / SEGC : 0;
+    const uint32_t S = __builtin_amdgcn_readfirstlane((uint32_t)wave_max_u64(nseg));
+    const uint64_t lo_v = wave_min_u64(n ? off : ~0ull);
+    const uint64_t base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo_v >> 32)) << 32) |
+                          __builtin_amdgcn_readfirstlane((uint32_t)lo_v);
+    const uint64_t top = wave_max_u64(n ? off + (uint64_t)C::kPieceB * nseg : 0);
+    if (S == 0) return;
+    // Every DMA'd byte must lie inside the arena and the span must fit a 31-bit
+    // buffer offset; otherwise (the wave at the arena's end, giant spans) the
+    // lanes hash their blocks with per-lane loads.
+    if (!(top <= arena_bytes && top - base <= 0x7FFFFFFFull)) {
+        // one chunk at a time (few VGPRs: this path must not raise the
+        // kernel's register budget); only the tail chunk's load is guarded
+        if (n == 0) return;
+        uint32_t h[4];
+        md4_init(h);
+        int32_t s1 = 0;
+        uint32_t t = 0;
+        const uint8_t *p = arena + off;
+        const uintptr_t end = (uintptr_t)(arena + arena_bytes);
+        uint32_t X[16];
+#pragma unroll 1
+        for (uint32_t c = 0; c < nfull; c++) {
+            load16(p + 64u * c, X);
+            hash_chunk<true>(X, 0u, 0u, c, h, s1, t);
+        }
+        load16_guarded(p + 64u * nfull, end, X);
+        hash_tail<true>(X, 0u, 0u, n, seed, h, s1, t);
+        store_record(out, g, n, s1, t, h);
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(arena + base), (short)0, 0x7FFFFFFF, 0x00020000);
+    // idle lanes (past the batch) alias the wave's first block: valid addresses
+    const uint32_t rel = n ? (uint32_t)(off - base) : 0u;
+
+    // DMA instruction i, lane l fills slot bytes [1024 i + 16 l, +16): lane
+    // j's piece, position p -> the block's quad (p - f(j)) % Q.
+    uint32_t voff[C::kDma];
+#pragma unroll
+    for (uint32_t i = 0; i < C::kDma; i++) {
+        const uint32_t pos = 1024u * i + 16u * lane;
+        const uint32_t j = pos / C::kPieceB;
+        const uint32_t p = (pos % C::kPieceB) / 16u;
+        const uint32_t q = (p - C::rot(j)) & (C::kQ - 1);
+        voff[i] = (uint32_t)__shfl((int)rel, (int)j, 64) + 16u * q;
+    }
+    const uint32_t rj = C::rot(lane);
+    const uint8_t *mine = ring + lane * C::kPieceB;
+
+    uint32_t h[4];
+    md4_init(h);
+    int32_t s1 = 0;
+    uint32_t t = 0;
+    if (MODE != 2) {
+#pragma unroll
+        for (uint32_t s = 0; s < (uint32_t)R; s++)
+            if (s < S) RSG_CRING_DMA(s);
+    }
+#pragma unroll 1
+    for (uint32_t s = 0; s < S; s++) {
+        if (MODE != 2) {
+            // segment s has landed once at most the younger in-flight ones remain
+            if (s + R <= S) {
+                if constexpr (R == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                else if constexpr (R == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::kDma) : "memory");
+                else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * C::kDma) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        const uint8_t *slot = mine + (s % R) * C::kSlotB;
+        uint32_t X[16 * SEGC];
+#pragma unroll
+        for (uint32_t q = 0; q < C::kQ; q++) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(slot + 16u * ((q + rj) & (C::kQ - 1)));
+            X[4 * q + 0] = v.x; X[4 * q + 1] = v.y; X[4 * q + 2] = v.z; X[4 * q + 3] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read out: it may be refilled
+        if (MODE != 2 && s + R < S) RSG_CRING_DMA(s + R);
+        if (MODE == 1) {
+#pragma unroll
+            for (int q = 0; q < 16 * SEGC; q++) h[q & 3] ^= X[q];
+        } else {
+#pragma unroll
+            for (uint32_t cc = 0; cc < (uint32_t)SEGC; cc++) {
+                const uint32_t c = SEGC * s + cc;
+                if (c < nfull) hash_chunk<true>(X + 16 * cc, 0u, 0u, c, h, s1, t);
+                else if (c == nfull) hash_tail<true>(X + 16 * cc, 0u, 0u, n, seed, h, s1, t);
+            }
+        }
+    }
+    if (n) store_record(out, g, n, s1, t, h);
+}
+#undef RSG_CRING_DMA
+
 // Variant 21: depth 2 at the single-slab LDS budget.  Segments are 128 bytes
 // (2 MD4 chunks) of every block, two of them per wave in flight in two
 // 64 x 144-byte slabs (18 KiB per wave, as the 256-byte single slab), so the
@@ -1220,6 +1378,472 @@ __global__ __launch_bounds__(kRtThreads) void block_sums_regtile(
     }
 }
 
+// ---------------------------------------------------------------- loader / register-park variant
+// For blocks of at most kRegMaxBytes (703: the reference's 700-byte blocks).
+// Every byte should cross HBM once, in long runs: a tile = 64 consecutive
+// blocks (45 KiB) is fetched as one near-linear LDS-DMA burst, and each
+// block then parks in its lane's VGPRs (176 registers) while it is hashed,
+// so LDS only holds tiles in transit.  One persistent 8-wave workgroup per CU:
+//   wave 0 (loader) locates the tiles of this workgroup (scalar loads, no
+//     vmcnt coupling with its DMA), writes their block lengths to LDS and
+//     keeps up to three tiles' DMA in flight in a 3-slot ring;
+//   waves 1..7 (hashers) take tiles in order by an LDS ticket, copy the slot
+//     into registers, free it, hash 64 blocks and store the records.
+// LDS handshake per slot: full[s] = the ticket it holds (set by the loader
+// after its covering vmcnt), freeq[s] = the ticket it may take next (set by
+// the hasher once its ds_reads of the slot completed).  Tiles that cannot be
+// staged (the batch's partial last tile, a tile whose 704-byte reads would
+// run past the arena, a span past a 31-bit offset) are marked direct: the
+// hasher locates and loads its blocks itself.
+constexpr uint32_t kPkPiece = 720;                // LDS bytes per block (44 data quads + 1 pad quad)
+constexpr uint32_t kPkTile = 64 * kPkPiece;       // 46080 B
+constexpr uint32_t kPkDma = kPkTile / 1024;       // 45 DMA instructions per tile
+constexpr uint32_t kPkSlots = 3;
+constexpr uint32_t kPkWaves = 8;
+constexpr uint32_t kPkThreads = 64 * kPkWaves;
+static_assert(kPkTile % 1024 == 0 && kPkPiece % 16 == 0, "tile = whole DMA instructions");
+
+struct PkShared {
+    uint8_t tile[kPkSlots][kPkTile];
+    uint32_t n[kPkSlots][64];  // block lengths of the slot's tile
+    uint32_t full[kPkSlots];
+    uint32_t freeq[kPkSlots];
+    uint32_t kind[kPkSlots];   // 1 = staged in the slot, 0 = direct
+    uint32_t ticket;
+};
+
+__device__ __forceinline__ uint32_t pk_load(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void pk_store(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Tile descriptor (64 blocks = one tile).  Regular tile = all 64 blocks in
+// one file: block j at base + B j, length B except the file's last block
+// (lane jl, length nl).  Otherwise per-lane (off, n), DMA offsets by
+// ds_bpermute.  Every load here is wave-uniform (scalar loads: they do not
+// queue behind the caller's LDS DMA in vmcnt).
+struct PkDesc {
+    uint64_t base;
+    uint32_t B, jl, nl;
+    bool regular, staged;
+    bool fast;  // staged and every block has its tail in chunk 10 (640 <= n <= 703)
+    uint64_t off;  // per lane
+    uint32_t n;    // per lane
+};
+
+__device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, const DevFile *__restrict__ files,
+                                          const uint32_t *__restrict__ wg_file, uint32_t nwg256,
+                                          uint64_t total_blocks, uint64_t arena_bytes) {
+    const uint64_t g0 = t * 64;
+    const uint32_t w = (uint32_t)(g0 >> 8);
+    uint32_t lo = wg_file[w], hi = wg_file[min(w + 1, nwg256)];
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (files[mid].first_block <= g0) lo = mid; else hi = mid - 1;
+    }
+    const DevFile F0 = files[__builtin_amdgcn_readfirstlane(lo)];
+    const uint64_t fend = F0.first_block + F0.nblocks;
+    d.regular = g0 >= F0.first_block && g0 + 64 <= fend;
+    const uint64_t g = g0 + lane;
+    if (d.regular) {
+        const uint64_t b0 = g0 - F0.first_block;
+        d.base = F0.offset + b0 * F0.blen;
+        d.B = F0.blen;
+        d.jl = (uint32_t)min<uint64_t>(fend - 1 - g0, 64);
+        d.nl = (uint32_t)(F0.len - (uint64_t)(F0.nblocks - 1) * F0.blen);
+        d.n = lane == d.jl ? d.nl : d.B;
+        d.off = d.base + (uint64_t)d.B * lane;
+        const uint64_t top = d.base + (uint64_t)d.B * 63 + 704u;
+        d.staged = d.B <= kRegMaxBytes && top <= arena_bytes && top - d.base <= 0x7FFFFFFFull;
+        d.fast = d.staged && d.B >= 640 && (d.jl >= 64 || d.nl >= 640);
+        return;
+    }
+    const uint64_t gend = min(g0 + 64, total_blocks);
+    uint64_t off = 0;
+    uint32_t n = 0;
+#pragma unroll 1
+    for (uint32_t f = __builtin_amdgcn_readfirstlane(lo);; f++) {
+        const DevFile F = files[f];
+        if (g >= F.first_block && g < F.first_block + F.nblocks) {
+            const uint64_t boff = (g - F.first_block) * F.blen;
+            const uint64_t left = F.len - boff;
+            n = left < F.blen ? (uint32_t)left : F.blen;  // generator.go:334
+            off = F.offset + boff;
+        }
+        if (F.first_block + F.nblocks >= gend) break;
+    }
+    const uint64_t lo_v = wave_min_u64(n ? off : ~0ull);
+    d.base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo_v >> 32)) << 32) |
+             __builtin_amdgcn_readfirstlane((uint32_t)lo_v);
+    const uint64_t top = wave_max_u64(n ? off + 704u : 0);
+    const uint32_t nmax = (uint32_t)wave_max_u64(n);
+    d.staged = (g0 + 64 <= total_blocks) && nmax <= kRegMaxBytes && top <= arena_bytes &&
+               top - d.base <= 0x7FFFFFFFull;
+    d.fast = d.staged && (uint32_t)wave_min_u64(n) >= 640u;
+    d.off = off;
+    d.n = n;
+    d.B = 0;
+}
+
+// MODE 0 = product; 1 = memory only (diagnostic: DMA + copy, no hashing).
+// AUX = cache policy of the tile DMA (0 default, 2 = nt: read once).
+template <int MODE, int AUX, int NL>
+__global__ __launch_bounds__(kPkThreads) void block_sums_park(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) PkShared sh;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x < kPkSlots) {
+        sh.full[threadIdx.x] = ~0u;
+        sh.freeq[threadIdx.x] = threadIdx.x;
+    }
+    if (threadIdx.x == 0) sh.ticket = 0;
+    __syncthreads();
+    const uint64_t ntiles = (total_blocks + 63) / 64;
+    const uint32_t G = gridDim.x;
+
+    if (wave < NL) {
+        // ------------------------------------------------------------ loaders
+        // DMA instruction i, lane l fills tile bytes [1024 i + 16 l, +16):
+        // block j = (64 i + l) / 45, quad u = (64 i + l) % 45 (u = 44: pad,
+        // marked by an offset no block length reaches).
+        uint32_t jj[kPkDma], uu[kPkDma];
+#pragma unroll
+        for (uint32_t i = 0; i < kPkDma; i++) {
+            const uint32_t idx = 64u * i + lane;
+            jj[i] = idx / 45u;
+            const uint32_t u = idx - 45u * jj[i];
+            uu[i] = u < 44u ? 16u * u : 0x40000000u;  // the pad quad: no block length reaches it
+        }
+        PkDesc cur;
+        uint32_t k = wave;  // loader L takes tickets L, L + NL, ...
+        uint64_t t = blockIdx.x + (uint64_t)wave * G;
+        bool any = false;
+        if (t < ntiles) pk_locate(t, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+#pragma unroll 1
+        for (; t < ntiles; t += (uint64_t)NL * G, k += NL) {
+            const uint32_t slot = k % kPkSlots;
+            // the slot's previous tile must have been copied out by its hasher
+            while (pk_load(&sh.freeq[slot]) != k) __builtin_amdgcn_s_sleep(1);
+            sh.n[slot][lane] = cur.n;
+            if (lane == 0) sh.kind[slot] = cur.staged ? 1u : 0u;
+            const bool staged = cur.staged;
+            if (staged) pk_issue<AUX, true>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
+            // next tile's descriptor while this one and the previous are in flight
+            if (t + (uint64_t)NL * G < ntiles)
+                pk_locate(t + (uint64_t)NL * G, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+            // publish this loader's previous tile once its DMA has landed
+            if (any) {
+                if (staged) asm volatile("s_waitcnt vmcnt(45)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) pk_store(&sh.full[(k - NL) % kPkSlots], k - NL);
+            }
+            any = true;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (any && lane == 0) pk_store(&sh.full[(k - NL) % kPkSlots], k - NL);
+        return;
+    }
+
+    // ---------------------------------------------------------------- hashers
+#pragma unroll 1
+    for (;;) {
+        uint32_t k = 0;
+        if (lane == 0) k = __hip_atomic_fetch_add(&sh.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        k = __builtin_amdgcn_readfirstlane(k);
+        const uint64_t t = blockIdx.x + (uint64_t)k * G;
+        if (t >= ntiles) break;
+        const uint32_t slot = k % kPkSlots;
+        while (pk_load(&sh.full[slot]) != k) __builtin_amdgcn_s_sleep(1);
+        const uint32_t n = sh.n[slot][lane];
+        const uint32_t kind = __builtin_amdgcn_readfirstlane(sh.kind[slot]);
+        const uint64_t g = t * 64 + lane;
+        uint32_t h[4];
+        md4_init(h);
+        int32_t s1 = 0;
+        uint32_t tw = 0;
+        if (kind) {
+            uint32_t R[16 * kRegChunks];
+            const uint8_t *mine = &sh.tile[slot][0] + lane * kPkPiece;
+#pragma unroll
+            for (uint32_t q = 0; q < 4 * kRegChunks; q++) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
+                R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);
+            const uint32_t nfull = n >> 6;
+            if (MODE == 1) {
+#pragma unroll
+                for (int q = 0; q < 16 * (int)kRegChunks; q++) h[q & 3] ^= R[q];
+            } else {
+#pragma unroll
+                for (uint32_t c = 0; c < kRegChunks; c++) {
+                    if (c < nfull) hash_chunk<true>(R + 16 * c, 0u, 0u, c, h, s1, tw);
+                    else if (c == nfull) hash_tail<true>(R + 16 * c, 0u, 0u, n, seed, h, s1, tw);
+                }
+            }
+            store_record(out, g, n, s1, tw, h);
+        } else {
+            if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);
+            if (g < total_blocks) {
+                uint64_t off;
+                uint32_t nn;
+                const uint32_t w = (uint32_t)(g >> 8);
+                uint32_t lo = wg_file[w], hi = wg_file[min(w + 1, nwg256)];
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi + 1) >> 1;
+                    if (files[mid].first_block <= g) lo = mid; else hi = mid - 1;
+                }
+                const DevFile F = files[lo];
+                const uint64_t boff = (g - F.first_block) * F.blen;
+                const uint64_t left = F.len - boff;
+                nn = left < F.blen ? (uint32_t)left : F.blen;
+                off = F.offset + boff;
+                const uint8_t *p = arena + off;
+                const uintptr_t end = (uintptr_t)(arena + arena_bytes);
+                const uint32_t nf = nn >> 6;
+                uint32_t X[16];
+#pragma unroll 1
+                for (uint32_t c = 0; c < nf; c++) {
+                    load16(p + 64u * c, X);
+                    hash_chunk<true>(X, 0u, 0u, c, h, s1, tw);
+                }
+                load16_guarded(p + 64u * nf, end, X);
+                hash_tail<true>(X, 0u, 0u, nn, seed, h, s1, tw);
+                store_record(out, g, nn, s1, tw, h);
+            }
+        }
+    }
+}
+
+// Issue the 45 LDS-DMA instructions of a staged tile into dst.  Instruction
+// i, lane l fills dst bytes [1024 i + 16 l, +16): block j = (64 i + l) / 45,
+// quad u = (64 i + l) % 45 (u = 44 is the pad).  Quads past the block's
+// bytes and the pad get an offset past num_records: no memory request.
+// jj/uu: per-lane block index and byte offset (0x40000000 for the pad) of
+// each instruction, precomputed by a caller with registers to spare (UNROLL);
+// otherwise computed on the fly.
+template <int AUX, bool UNROLL>
+__device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, const PkDesc &d, uint32_t lane,
+                                         const uint32_t *jj = nullptr, const uint32_t *uu = nullptr) {
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(arena + d.base), (short)0, 0x7FFFFFFF, 0x00020000);
+    const int rel = (int)(uint32_t)(d.off - d.base);
+#define RSG_PK_ONE(I_, REG)                                                                                     \
+    do {                                                                                                        \
+        uint32_t j_, u16_;                                                                                      \
+        if (UNROLL) {                                                                                           \
+            j_ = jj[I_];                                                                                        \
+            u16_ = uu[I_];                                                                                      \
+        } else {                                                                                                \
+            const uint32_t idx_ = 64u * (I_) + lane;                                                            \
+            j_ = idx_ / 45u;                                                                                    \
+            const uint32_t u_ = idx_ - 45u * j_;                                                                \
+            u16_ = u_ < 44u ? 16u * u_ : 0x40000000u;                                                           \
+        }                                                                                                       \
+        uint32_t vo_;                                                                                           \
+        if (REG) {                                                                                              \
+            const uint32_t nj_ = j_ == d.jl ? d.nl : d.B;                                                       \
+            vo_ = u16_ < nj_ ? d.B * j_ + u16_ : 0x80000000u;                                                   \
+        } else {                                                                                                \
+            const uint32_t rj_ = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * j_), rel);                  \
+            const uint32_t nj_ = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * j_), (int)d.n);             \
+            vo_ = u16_ < nj_ ? rj_ + u16_ : 0x80000000u;                                                        \
+        }                                                                                                       \
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * (I_)), \
+                                                 16, vo_, 0, 0, AUX);                                           \
+    } while (0)
+    // the regular/irregular choice is made once per tile (a branch per
+    // instruction costs an lgkmcnt wait per instruction); UNROLL = false when
+    // the caller holds a parked block (176 VGPRs)
+    if (d.regular) {
+        if constexpr (UNROLL) {
+#pragma unroll
+            for (uint32_t i = 0; i < kPkDma; i++) RSG_PK_ONE(i, true);
+        } else {
+#pragma unroll 1
+            for (uint32_t i = 0; i < kPkDma; i++) RSG_PK_ONE(i, true);
+        }
+    } else {
+        if constexpr (UNROLL) {
+#pragma unroll
+            for (uint32_t i = 0; i < kPkDma; i++) RSG_PK_ONE(i, false);
+        } else {
+#pragma unroll 1
+            for (uint32_t i = 0; i < kPkDma; i++) RSG_PK_ONE(i, false);
+        }
+    }
+#undef RSG_PK_ONE
+}
+
+// Hash a parked block (R = its 704 bytes, chunks 0..10) from chunk C_LO up to
+// C_HI (exclusive).
+template <uint32_t C_LO, uint32_t C_HI>
+__device__ __forceinline__ void pk_hash(const uint32_t *R, uint32_t n, uint32_t seed, uint32_t h[4], int32_t &s1,
+                                        uint32_t &tw) {
+    const uint32_t nfull = n >> 6;
+#pragma unroll
+    for (uint32_t c = C_LO; c < C_HI; c++) {
+        if (c < nfull) hash_chunk<true>(R + 16 * c, 0u, 0u, c, h, s1, tw);
+        else if (c == nfull) hash_tail<true>(R + 16 * c, 0u, 0u, n, seed, h, s1, tw);
+    }
+}
+
+// A block of a direct tile: the lane locates and loads it itself.
+__device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uint64_t arena_bytes,
+                                       const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file,
+                                       uint32_t nwg256, uint64_t g, uint32_t seed, uint8_t *__restrict__ out) {
+    const uint32_t w = (uint32_t)(g >> 8);
+    uint32_t lo = wg_file[w], hi = wg_file[min(w + 1, nwg256)];
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (files[mid].first_block <= g) lo = mid; else hi = mid - 1;
+    }
+    const DevFile F = files[lo];
+    const uint64_t boff = (g - F.first_block) * F.blen;
+    const uint64_t left = F.len - boff;
+    const uint32_t nn = left < F.blen ? (uint32_t)left : F.blen;
+    const uint8_t *p = arena + F.offset + boff;
+    const uintptr_t end = (uintptr_t)(arena + arena_bytes);
+    const uint32_t nf = nn >> 6;
+    uint32_t h[4];
+    md4_init(h);
+    int32_t s1 = 0;
+    uint32_t tw = 0;
+    uint32_t X[16];
+#pragma unroll 1
+    for (uint32_t c = 0; c < nf; c++) {
+        load16(p + 64u * c, X);
+        hash_chunk<true>(X, 0u, 0u, c, h, s1, tw);
+    }
+    load16_guarded(p + 64u * nf, end, X);
+    hash_tail<true>(X, 0u, 0u, nn, seed, h, s1, tw);
+    store_record(out, g, nn, s1, tw, h);
+}
+
+// ---------------------------------------------------------------- relay variant
+// The loader wave above is capped by its 6-bit vmcnt: at most 63 DMA
+// instructions (63 KiB) in flight per wave, i.e. per CU.  Here there is no
+// loader: all 8 waves hash, and each one relays the ring forward.  The wave
+// that takes ticket k copies slot k % 3 into its registers and immediately
+// refills that slot with tile k + 3 (its own DMA, at most 45 instructions in
+// its own vmcnt), hashes chunks 0..C0-1 of its blocks while the DMA flies,
+// then waits for it, publishes tile k + 3 and hashes the rest.  Up to three
+// tiles (138 KiB) are in flight per CU, spread over three waves' counters.
+template <int AUX, uint32_t C0>
+__global__ __launch_bounds__(kPkThreads) void block_sums_relay(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) PkShared sh;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x < kPkSlots) sh.full[threadIdx.x] = ~0u;
+    if (threadIdx.x == 0) sh.ticket = 0;
+    __syncthreads();
+    const uint64_t ntiles = (total_blocks + 63) / 64;
+    const uint32_t G = gridDim.x;
+    // prologue: waves 0..2 load tickets 0..2
+    if (wave < kPkSlots && blockIdx.x + (uint64_t)wave * G < ntiles) {
+        PkDesc d;
+        pk_locate(blockIdx.x + (uint64_t)wave * G, d, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+        sh.n[wave][lane] = d.n;
+        if (lane == 0) sh.kind[wave] = d.fast ? 1u : (d.staged ? 2u : 0u);
+        if (d.staged) pk_issue<AUX, false>(arena, &sh.tile[wave][0], d, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) pk_store(&sh.full[wave], wave);
+    }
+#pragma unroll 1
+    for (;;) {
+        uint32_t k = 0;
+        if (lane == 0) k = __hip_atomic_fetch_add(&sh.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        k = __builtin_amdgcn_readfirstlane(k);
+        const uint64_t t = blockIdx.x + (uint64_t)k * G;
+        if (t >= ntiles) break;
+        const uint32_t slot = k % kPkSlots;
+        const uint64_t tn = t + (uint64_t)kPkSlots * G;  // the tile this wave relays
+        const bool relay = tn < ntiles;
+        PkDesc d;
+        if (relay) pk_locate(tn, d, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+        while (pk_load(&sh.full[slot]) != k) __builtin_amdgcn_s_sleep(1);
+        const uint32_t n = sh.n[slot][lane];
+        const uint32_t kind = __builtin_amdgcn_readfirstlane(sh.kind[slot]);
+        const uint64_t g = t * 64 + lane;
+        // refill the slot with tile k + 3 (its descriptor first: the slot's
+        // own n/kind have been read)
+#define RSG_RELAY_ISSUE()                                                      \
+    do {                                                                       \
+        sh.n[slot][lane] = d.n;                                                \
+        if (lane == 0) sh.kind[slot] = d.fast ? 1u : (d.staged ? 2u : 0u);     \
+        if (d.staged) pk_issue<AUX, false>(arena, &sh.tile[slot][0], d, lane);        \
+    } while (0)
+#define RSG_RELAY_PUBLISH()                                                    \
+    do {                                                                       \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                       \
+        if (lane == 0) pk_store(&sh.full[slot], k + kPkSlots);                 \
+    } while (0)
+        uint32_t h[4];
+        md4_init(h);
+        int32_t s1 = 0;
+        uint32_t tw = 0;
+        if (kind == 1) {
+            // every block ends in chunk 10: park it, refill the slot at once,
+            // publish the refill after chunk C0
+            uint32_t R[16 * kRegChunks];
+            const uint8_t *mine = &sh.tile[slot][0] + lane * kPkPiece;
+#pragma unroll
+            for (uint32_t q = 0; q < 4 * kRegChunks; q++) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
+                R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read out
+            if (relay) RSG_RELAY_ISSUE();
+#pragma unroll
+            for (uint32_t c = 0; c < C0; c++) hash_chunk<true>(R + 16 * c, 0u, 0u, c, h, s1, tw);
+            if (relay) RSG_RELAY_PUBLISH();
+#pragma unroll
+            for (uint32_t c = C0; c < kRegChunks - 1; c++) hash_chunk<true>(R + 16 * c, 0u, 0u, c, h, s1, tw);
+            hash_tail<true>(R + 16 * (kRegChunks - 1), 0u, 0u, n, seed, h, s1, tw);
+            store_record(out, g, n, s1, tw, h);
+        } else if (kind == 2) {
+            // ragged block lengths: hash straight out of the slot (few
+            // VGPRs), then refill it
+            const uint8_t *mine = &sh.tile[slot][0] + lane * kPkPiece;
+            const uint32_t nfull = n >> 6;
+            uint32_t X[16];
+#pragma unroll 1
+            for (uint32_t c = 0; c <= nfull; c++) {
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++) {
+                    const uint4 v = *reinterpret_cast<const uint4 *>(mine + 64 * c + 16 * q);
+                    X[4 * q + 0] = v.x; X[4 * q + 1] = v.y; X[4 * q + 2] = v.z; X[4 * q + 3] = v.w;
+                }
+                if (c < nfull) hash_chunk<true>(X, 0u, 0u, c, h, s1, tw);
+                else hash_tail<true>(X, 0u, 0u, n, seed, h, s1, tw);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (relay) {
+                RSG_RELAY_ISSUE();
+                RSG_RELAY_PUBLISH();
+            }
+            store_record(out, g, n, s1, tw, h);
+        } else {
+            if (relay) {
+                RSG_RELAY_ISSUE();
+                RSG_RELAY_PUBLISH();
+            }
+            if (g < total_blocks) pk_direct(arena, arena_bytes, files, wg_file, nwg256, g, seed, out);
+        }
+#undef RSG_RELAY_ISSUE
+#undef RSG_RELAY_PUBLISH
+    }
+}
+
 // Kernel variants (rsg_set_block_sums_kernel): -1 = automatic, 0 = direct,
 // 1 = staged K=1, 2 = staged K=4, 3 = register-block, 4 = register-tile,
 // 5 = loaded line ring, 6 = line ring with shared boundary lines, 7/8 = 1/2
@@ -1246,7 +1870,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     // confirmation windows) take the deep-prefetch kernel when blocks are long
     if (v == -1) v = aligned ? 1 : (max_blen >= kLongBlockBytes ? 9 : 0);
     if (!aligned && ((v < 13 && v != 9) || v >= 20)) v = 0;
-    if ((v == 3 || v == 4 || v == 12 || v == 17) && max_blen > kRegMaxBytes) v = 1;
+    if ((v == 3 || v == 4 || v == 12 || v == 17 || (v >= 34 && v <= 41)) && max_blen > kRegMaxBytes) v = 1;
     if ((v == 4 || v == 17) && !scratch) v = 1;
     dim3 grid(nwg), block(kBlockSumThreads);
 #define RSG_LAUNCH(KERNEL, GRID) \
@@ -1254,7 +1878,60 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
 #define RSG_STAGED(KK, MM, ...)                                                                                 \
     hipLaunchKernelGGL((block_sums_staged<KK, MM, ##__VA_ARGS__>), dim3((uint32_t)((total_blocks + 256u * KK - 1) / (256u * KK))), \
                        block, 0, stream, arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out)
+#define RSG_CRING(RR, SS, MM, WW)                                                                             \
+    hipLaunchKernelGGL((block_sums_cring<RR, SS, MM, WW>), dim3((uint32_t)((total_blocks + 255u) / 256u)), block, 0, \
+                       stream, arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out)
     switch (v) {
+        case 38:
+        case 39:
+        case 40:
+        case 41: {
+            int dev = 0, cus = 256;
+            if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            const uint64_t ntile = (total_blocks + 63) / 64;
+            const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus, ntile));
+            if (v == 38)
+                hipLaunchKernelGGL((block_sums_relay<2, 4>), dim3(g), dim3(kPkThreads), 0, stream, arena, arena_bytes,
+                                   files, wg_file, nwg, total_blocks, seed, out);
+            else if (v == 39)
+                hipLaunchKernelGGL((block_sums_relay<2, 2>), dim3(g), dim3(kPkThreads), 0, stream, arena, arena_bytes,
+                                   files, wg_file, nwg, total_blocks, seed, out);
+            else if (v == 40)
+                hipLaunchKernelGGL((block_sums_relay<2, 6>), dim3(g), dim3(kPkThreads), 0, stream, arena, arena_bytes,
+                                   files, wg_file, nwg, total_blocks, seed, out);
+            else
+                hipLaunchKernelGGL((block_sums_relay<2, 8>), dim3(g), dim3(kPkThreads), 0, stream, arena, arena_bytes,
+                                   files, wg_file, nwg, total_blocks, seed, out);
+            break;
+        }
+        case 34:
+        case 35:
+        case 36:
+        case 37: {
+            int dev = 0, cus = 256;
+            if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            const uint64_t ntile = (total_blocks + 63) / 64;
+            const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus, ntile));
+#define RSG_PARK(MM, AA, NN)                                                                                 \
+    hipLaunchKernelGGL((block_sums_park<MM, AA, NN>), dim3(g), dim3(kPkThreads), 0, stream, arena, arena_bytes, files, \
+                       wg_file, nwg, total_blocks, seed, out)
+            if (v == 34) RSG_PARK(0, 2, 2);
+            else if (v == 35) RSG_PARK(1, 2, 2);
+            else if (v == 36) RSG_PARK(0, 2, 1);
+            else RSG_PARK(1, 2, 1);
+#undef RSG_PARK
+            break;
+        }
+        case 24: RSG_CRING(1, 1, 0, 8); break;
+        case 25: RSG_CRING(2, 1, 0, 5); break;
+        case 26: RSG_CRING(3, 1, 0, 3); break;
+        case 27: RSG_CRING(1, 2, 0, 5); break;
+        case 28: RSG_CRING(2, 2, 0, 2); break;
+        case 29: RSG_CRING(1, 1, 1, 8); break;
+        case 30: RSG_CRING(1, 1, 2, 8); break;
+        case 31: RSG_CRING(2, 1, 1, 5); break;
+        case 32: RSG_CRING(2, 1, 2, 5); break;
+        case 33: RSG_CRING(1, 2, 1, 5); break;
         case 0:
             if (aligned) RSG_LAUNCH(block_sums_direct<true>, grid);
             else RSG_LAUNCH(block_sums_direct<false>, grid);
@@ -1328,6 +2005,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     }
 #undef RSG_LAUNCH
 #undef RSG_STAGED
+#undef RSG_CRING
     return hipGetLastError();
 }
 

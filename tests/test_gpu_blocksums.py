@@ -176,7 +176,7 @@ def test_generate_and_send_sums_wire(eng):
     assert bytes(conn.buf) == want
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 20, 21, 23])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 20, 21, 23, 24, 25, 26, 27, 28, 34, 38, 39, 40])
 @pytest.mark.parametrize("blen", [700, 64, 1773, 4096, 131072])
 def test_kernel_variants_match(eng, variant, blen):
     """Every kernel variant (direct / staged K=1 / staged K=4 / register-block /
@@ -200,7 +200,7 @@ def test_kernel_variants_match(eng, variant, blen):
     assert rec_dev == want
 
 
-@pytest.mark.parametrize("variant", [1, 4, 5, 6, 7, 8, 9, 20, 21, 23])
+@pytest.mark.parametrize("variant", [1, 4, 5, 6, 7, 8, 9, 20, 21, 23, 24, 25, 26, 27, 28, 34, 38, 39, 40])
 def test_variants_device_aligned_arena(eng, variant):
     """Aligned device arena (the staged / register-tile fast paths), files
     straddling waves, a file ending exactly at the arena end, blocks of
