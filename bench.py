@@ -124,17 +124,15 @@ def main():
     extra = {}
     if args.ab:
         from rsync_amd import _lib
-        names = {1: "staged_k1", 24: "cring_r1_s1_w8", 25: "cring_r2_s1_w5", 26: "cring_r3_s1_w3",
-                 27: "cring_r1_s2_w5", 28: "cring_r2_s2_w2", 29: "diag_cring_r1_s1_memory",
-                 30: "diag_cring_r1_s1_hash", 31: "diag_cring_r2_s1_memory", 32: "diag_cring_r2_s1_hash",
-                 33: "diag_cring_r1_s2_memory", 10: "diag_staged_memory_only", 11: "diag_staged_hash_only",
-                 14: "diag_linear_read_ldsdma"}
-        if os.environ.get("RSG_AB"):
-            names = {int(k): f"variant_{k}" for k in os.environ["RSG_AB"].split(",")}
+        # (product variant, diagnostic) pairs; diagnostics write meaningless records
+        names = {(1, 0): "staged", (2, 0): "park", (1, 1): "diag_staged_memory_only",
+                 (1, 2): "diag_staged_hash_only", (2, 3): "diag_park_memory_only",
+                 (1, 5): "diag_linear_read_ldsdma"}
         res = {v: [] for v in names}
         for _ in range(5):
             for v in names:
-                _lib.check(_lib.lib.rsg_set_block_sums_kernel(v))
+                _lib.check(_lib.lib.rsg_set_block_sums_kernel(v[0]))
+                _lib.check(_lib.lib.rsg_set_block_sums_diagnostic(v[1]))
                 for i in range(3):
                     step(i)
                 a0 = torch.cuda.Event(enable_timing=True)
@@ -146,6 +144,7 @@ def main():
                 eng.synchronize(sptr)
                 res[v].append(a0.elapsed_time(a1) / args.steps)
         _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+        _lib.check(_lib.lib.rsg_set_block_sums_diagnostic(0))
         step(0)  # the records hold the product kernel's output again (diagnostics write garbage)
         eng.synchronize(sptr)
         extra["ab_kernel_ms"] = {names[v]: [round(x, 4) for x in sorted(res[v])] for v in names}

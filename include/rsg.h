@@ -140,20 +140,26 @@ uint64_t rsg_plan_total_records(const rsg_plan *plan);
 rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void *d_arena,
                                   int32_t seed, void *d_records, void *stream);
 
-/* Tuning knob (process-wide): block-sum kernel variant.  -1 = automatic
- * (default: 1), 0 = direct per-lane loads, 1 = staged LDS-DMA slabs, 2 = staged
- * with 4 blocks per lane, 3 = whole block in registers (blocks <= 703 bytes),
- * 4 = register tiles (blocks <= 703 bytes), 5 = aligned line ring (each line
- * loaded once, realigned through LDS), 6 = line ring with each block's last
- * line taken from the next lane, 7/8 = variants 1/2 with each block's last
- * DMA segment cut at the block's end, 9 = deep per-lane prefetch for long
- * blocks (automatic for unaligned batches with blocks >= 8 KiB; otherwise
- * automatic = 1 for aligned batches, 0 for unaligned ones).  These give
- * identical results; only speed differs.  10..19 are timing diagnostics whose outputs are meaningless
- * (memory-only / hashing-only / plain reads).  Unaligned batches use
- * variant 0 or 9.  The environment variable RSG_BLOCKSUMS_KERNEL sets the initial
- * value. */
+/* Tuning knob (process-wide): block-sum kernel variant.  Every variant
+ * gives identical records; only speed differs.  -1 = automatic (default),
+ * 0 = direct per-lane loads, 1 = staged LDS-DMA slabs, 2 = park (one loader
+ * wave streams 64-block tiles through LDS, blocks parked in registers; blocks
+ * <= 703 bytes, otherwise 1 is used), 3 = deep per-lane prefetch for long
+ * blocks.  Automatic: aligned batches take 2 when 512 <= the largest block
+ * <= 703 bytes, else 1; unaligned batches (a block not 4-byte aligned) take 3
+ * for blocks >= 8 KiB, else 0 (1 and 2 fall back to 0 there).  The
+ * environment variable RSG_BLOCKSUMS_KERNEL sets the initial value.  Returns
+ * RSG_ERR_INVALID outside -1..3. */
 rsg_status rsg_set_block_sums_kernel(int32_t variant);
+
+/* Timing diagnostics for DESIGN.md's roofline analysis, NOT for use: while
+ * diag != 0 every aligned block-sum launch runs the diagnostic instead of the
+ * product kernel and the "records" it writes are meaningless.  1 = staged
+ * memory only, 2 = staged hashing only, 3 = park memory only, 4 = linear read
+ * of the arena (plain loads), 5 = linear read (LDS DMA).  0 = off (default;
+ * environment RSG_BLOCKSUMS_DIAG).  Kept apart from rsg_set_block_sums_kernel
+ * so the product knob can never select a diagnostic. */
+rsg_status rsg_set_block_sums_diagnostic(int32_t diag);
 
 /* One-shot device call: plan + launch + wait. */
 rsg_status rsg_block_sums_device(rsg_ctx *ctx, const void *d_arena, uint64_t arena_bytes,

@@ -82,6 +82,7 @@ _PROTOS = {
     "rsg_plan_total_records": (_u64, [_vp]),
     "rsg_block_sums_planned": (_st, [_vp, _vp, _vp, _i32, _vp, _vp]),
     "rsg_set_block_sums_kernel": (_st, [_i32]),
+    "rsg_set_block_sums_diagnostic": (_st, [_i32]),
     "rsg_block_sums_device": (_st, [_vp, _vp, _u64, ctypes.POINTER(File), _u64, _i32, _vp, _u64]),
     "rsg_block_sums_host": (_st, [_vp, ctypes.POINTER(File), _u64, _i32, _vp, _u64]),
     "rsg_hash_search_host": (_st, [_vp, _vp, _u64, ctypes.POINTER(SumHead), _vp, _vp, _vp, _i32,

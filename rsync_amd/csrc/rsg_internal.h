@@ -30,8 +30,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
 // Device scratch a block-sum launch needs: 4 + 4 * ceil(total_blocks / 64) bytes.
 inline uint64_t block_sums_scratch_bytes(uint64_t total_blocks) { return 8 + 4 * ((total_blocks + 63) / 64); }
 
-// 0 = direct (per-lane loads), 1 = staged (LDS DMA, default for aligned batches).
+// Product variants (-1 auto, 0 direct, 1 staged, 2 park, 3 long) and timing
+// diagnostics (0 off, 1..5; outputs meaningless), rsg_blocksums.hip.
 void set_block_sums_variant(int v);
+void set_block_sums_diagnostic(int d);
 
 // ---- sender search (rsg_match_kernels.hip)
 constexpr uint32_t kScanTile = 32768;                          // source bytes per tile

@@ -176,12 +176,12 @@ def test_generate_and_send_sums_wire(eng):
     assert bytes(conn.buf) == want
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 20, 21, 23, 24, 25, 26, 27, 28, 34, 38, 39, 40])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("blen", [700, 64, 1773, 4096, 131072])
 def test_kernel_variants_match(eng, variant, blen):
-    """Every kernel variant (direct / staged K=1 / staged K=4 / register-block /
-    register-tile / line ring / line ring sharing boundary lines) gives the
-    oracle's records, including waves that straddle files."""
+    """Every kernel variant (direct / staged / park / long) gives the oracle's
+    records, including waves and park tiles that straddle files; unaligned
+    arenas make the LDS-DMA variants fall back to direct."""
     from rsync_amd import _lib
     lens = [1 << 20, 700 * 64 * 3 + 5, 12345, 64, 1, 0, 300_001]
     files = [cases.splitmix64_bytes(4000 + i, n) for i, n in enumerate(lens)]
@@ -200,11 +200,12 @@ def test_kernel_variants_match(eng, variant, blen):
     assert rec_dev == want
 
 
-@pytest.mark.parametrize("variant", [1, 4, 5, 6, 7, 8, 9, 20, 21, 23, 24, 25, 26, 27, 28, 34, 38, 39, 40])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_variants_device_aligned_arena(eng, variant):
-    """Aligned device arena (the staged / register-tile fast paths), files
-    straddling waves, a file ending exactly at the arena end, blocks of
-    700/64/703 bytes."""
+    """Aligned device arena (the staged / park fast paths), files straddling
+    waves and tiles, a file ending exactly at the arena end (park's direct
+    tiles), blocks of 700/64/703 bytes (64: park with tiny blocks, ragged
+    tails hashed by the predicated path)."""
     from rsync_amd import _lib
     lens = [1 << 20, 700 * 64 * 3 + 5, 12344, 64, 4, 0, 300_000, 70_000 * 3]
     offs, o = [], 0

@@ -19,9 +19,9 @@ SEED = 0x1BADB002
 SHAPES = [  # (files, file bytes, block length, arenas)
     (1, 1 << 30, 131072, 2),      # one 1 GiB file, cfg5's block length
     (1, 32 << 30, 131072, 1),     # cfg5's per-GPU share: one 32 GiB file
-    (1024, 1 << 20, 700, 2),      # cfg2
+    (1024, 1 << 20, 700, 2),      # cfg2 (park applies to blocks <= 703 bytes only)
 ]
-VARIANTS = {1: "staged", 9: "long_deep_prefetch"}
+VARIANTS = {1: "staged", 2: "park", 3: "long_deep_prefetch"}
 
 
 def main():
