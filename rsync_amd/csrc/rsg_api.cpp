@@ -409,13 +409,13 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
 }
 
 rsg_status rsg_set_block_sums_kernel(int32_t variant) {
-    if (variant < -1 || variant > 3) return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..3");
+    if (variant < -1 || variant > 4) return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..4");
     rsg::set_block_sums_variant(variant);
     return RSG_OK;
 }
 
 rsg_status rsg_set_block_sums_diagnostic(int32_t diag) {
-    if (diag < 0 || diag > 5) return fail(nullptr, RSG_ERR_INVALID, "diagnostic must be 0..5");
+    if (diag < 0 || diag > 6) return fail(nullptr, RSG_ERR_INVALID, "diagnostic must be 0..6");
     rsg::set_block_sums_diagnostic(diag);
     return RSG_OK;
 }

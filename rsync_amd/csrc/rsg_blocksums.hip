@@ -670,9 +670,8 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
 
 // MODE 0 = product; 1 = memory only (diagnostic: DMA + copy, no hashing).
 // The tile DMA uses the nt cache policy (aux = 2): every byte is read once.
-// One loader wave: a second one (NL = 2, tried) convoys with the first on the
-// three slots and is slower.
-template <int MODE>
+// NL = loader waves (1 or 2); the other 8 - NL waves hash.
+template <int MODE, int NL>
 __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
@@ -689,8 +688,8 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint64_t ntiles = (total_blocks + 63) / 64;
     const uint32_t G = gridDim.x;  // one persistent workgroup per CU; tile t belongs to workgroup t % G
 
-    if (wave == 0) {
-        // ------------------------------------------------------------ loader
+    if (wave < NL) {
+        // ------------------------------------------------------------ loaders
         // DMA instruction i, lane l fills tile bytes [1024 i + 16 l, +16):
         // block j = (64 i + l) / 45, quad u = (64 i + l) % 45 (u = 44: pad,
         // marked by an offset no block length reaches).
@@ -702,12 +701,21 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             const uint32_t u = idx - 45u * jj[i];
             uu[i] = u < 44u ? 16u * u : 0x40000000u;  // the pad quad: no block length reaches it
         }
-        PkDesc cur;
+        // Loader L owns the slots s with s % NL == L and loads the tickets k
+        // whose slot k % 3 it owns (NL = 2: loader 0 slots 0 and 2, loader 1
+        // slot 1), so each loader's tiles sit in its own vmcnt.
+        auto owned = [&](uint32_t kk) { return (kk % kPkSlots) % NL == wave; };
+        constexpr uint32_t kOwned0 = (kPkSlots + NL - 1) / NL;  // slots of loader 0
+        const bool single = (wave == 0 ? kOwned0 : (kPkSlots - kOwned0)) == 1;
         uint32_t k = 0;
-        uint64_t t = blockIdx.x;
+        while (!owned(k)) k++;
+        PkDesc cur;
+        uint64_t t = blockIdx.x + (uint64_t)k * G;
         if (t < ntiles) pk_locate(t, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+        bool have_prev = false;
+        uint32_t prev = 0;
 #pragma unroll 1
-        for (; t < ntiles; t += G, k++) {
+        while (t < ntiles) {
             const uint32_t slot = k % kPkSlots;
             // the slot's previous tile must have been copied out by its hasher
             while (pk_load(&sh.freeq[slot]) != k) __builtin_amdgcn_s_sleep(1);
@@ -715,21 +723,34 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             if (lane == 0) sh.kind[slot] = cur.staged ? 1u : 0u;
             const bool staged = cur.staged;
             if (staged) pk_issue<2, true>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
+            uint32_t kn = k + 1;
+            while (!owned(kn)) kn++;
+            const uint64_t tn = blockIdx.x + (uint64_t)kn * G;
             // next tile's descriptor (scalar loads) while this one and the
             // previous one are in flight
-            if (t + G < ntiles) pk_locate(t + G, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
-            // publish the previous tile once its DMA has landed.  vmcnt is a
-            // 6-bit counter: a wave cannot have more than 63 DMA instructions
-            // (63 KiB) in flight, so waiting for tile k-2 instead (three tiles
-            // in flight) stalls the issue of tile k and measured slower.
-            if (k > 0) {
+            if (tn < ntiles) pk_locate(tn, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+            if (single) {
+                // one slot: publish this tile before waiting for the slot again
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) pk_store(&sh.full[slot], k);
+            } else if (have_prev) {
+                // publish the previous tile once its DMA has landed.  vmcnt is
+                // a 6-bit counter: a wave cannot have more than 63 DMA
+                // instructions (63 KiB) in flight, so waiting for an older
+                // tile instead stalls the issue of this one (measured slower).
                 if (staged) asm volatile("s_waitcnt vmcnt(45)" ::: "memory");
                 else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) pk_store(&sh.full[(k - 1) % kPkSlots], k - 1);
+                if (lane == 0) pk_store(&sh.full[prev % kPkSlots], prev);
             }
+            have_prev = true;
+            prev = k;
+            k = kn;
+            t = tn;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (k > 0 && lane == 0) pk_store(&sh.full[(k - 1) % kPkSlots], k - 1);
+        if (!single && have_prev) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) pk_store(&sh.full[prev % kPkSlots], prev);
+        }
         return;
     }
 
@@ -809,7 +830,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     if (g_variant == -2) {
         const char *e = getenv("RSG_BLOCKSUMS_KERNEL");
         g_variant = e ? atoi(e) : -1;
-        if (g_variant < -1 || g_variant > 3) g_variant = -1;
+        if (g_variant < -1 || g_variant > 4) g_variant = -1;
     }
     if (g_diag == -2) {
         const char *e = getenv("RSG_BLOCKSUMS_DIAG");
@@ -828,14 +849,19 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                 break;
             case 3:
                 if (max_blen <= kRegMaxBytes)
-                    hipLaunchKernelGGL(block_sums_park<1>, dim3(park_grid(total_blocks)), dim3(kPkThreads), 0, stream,
+                    hipLaunchKernelGGL((block_sums_park<1, 1>), dim3(park_grid(total_blocks)), dim3(kPkThreads), 0, stream,
+                                       arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+                break;
+            case 6:
+                if (max_blen <= kRegMaxBytes)
+                    hipLaunchKernelGGL((block_sums_park<1, 2>), dim3(park_grid(total_blocks)), dim3(kPkThreads), 0, stream,
                                        arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
                 break;
             case 4:
                 hipLaunchKernelGGL(diag_linear_read<false>, dim3(2048), dim3(256), 0, stream, arena, arena_bytes,
                                    (uint32_t *)out);
                 break;
-            default:
+            case 5:
                 hipLaunchKernelGGL(diag_linear_read<true>, dim3(2048), dim3(256), 0, stream, arena, arena_bytes,
                                    (uint32_t *)out);
                 break;
@@ -847,15 +873,20 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         v = aligned ? ((max_blen <= kRegMaxBytes && max_blen >= kParkMinBytes) ? 2 : 1)
                     : (max_blen >= kLongBlockBytes ? 3 : 0);
     if (!aligned && (v == 1 || v == 2)) v = 0;  // the LDS-DMA kernels need 4-byte aligned blocks
-    if (v == 2 && max_blen > kRegMaxBytes) v = 1;
+    if ((v == 2 || v == 4) && max_blen > kRegMaxBytes) v = 1;
+    if (v == 4 && !aligned) v = 0;
     switch (v) {
         case 1:
             hipLaunchKernelGGL(block_sums_staged<0>, grid, block, 0, stream, arena, arena_bytes, files, wg_file,
                                total_blocks, seed, out);
             break;
         case 2:
-            hipLaunchKernelGGL(block_sums_park<0>, dim3(park_grid(total_blocks)), dim3(kPkThreads), 0, stream, arena,
-                               arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+            hipLaunchKernelGGL((block_sums_park<0, 1>), dim3(park_grid(total_blocks)), dim3(kPkThreads), 0, stream,
+                               arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+            break;
+        case 4:  // experimental: two loader waves
+            hipLaunchKernelGGL((block_sums_park<0, 2>), dim3(park_grid(total_blocks)), dim3(kPkThreads), 0, stream,
+                               arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
             break;
         case 3: {
             const dim3 g64((uint32_t)((total_blocks + 63) / 64)), b64(64);
