@@ -125,10 +125,9 @@ def main():
     if args.ab:
         from rsync_amd import _lib
         # (product variant, diagnostic) pairs; diagnostics write meaningless records
-        names = {(1, 0): "staged", (2, 0): "park", (4, 0): "park_2_loaders", (1, 6): "diag_park_2_loaders_memory_only",
-                 (1, 1): "diag_staged_memory_only",
-                 (1, 2): "diag_staged_hash_only", (2, 3): "diag_park_memory_only",
-                 (1, 5): "diag_linear_read_ldsdma"}
+        names = {(1, 0): "staged", (2, 0): "park", (1, 1): "diag_staged_memory_only",
+                 (1, 2): "diag_staged_hash_only", (1, 3): "diag_park_memory_only", (1, 4): "diag_park_hash_only",
+                 (1, 6): "diag_linear_read_ldsdma"}
         res = {v: [] for v in names}
         for _ in range(5):
             for v in names:

@@ -142,10 +142,10 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
 
 /* Tuning knob (process-wide): block-sum kernel variant.  Every variant
  * gives identical records; only speed differs.  -1 = automatic (default),
- * 0 = direct per-lane loads, 1 = staged LDS-DMA slabs, 2 = park (one loader
- * wave streams 64-block tiles through LDS, blocks parked in registers; blocks
- * <= 703 bytes, otherwise 1 is used), 3 = deep per-lane prefetch for long
- * blocks.  Automatic: aligned batches take 2 when 512 <= the largest block
+ * 0 = direct per-lane loads, 1 = staged LDS-DMA slabs, 2 = park (three loader
+ * waves stream 64-block tiles through LDS, five hasher waves park the blocks
+ * in registers; blocks <= 703 bytes, otherwise 1 is used), 3 = deep per-lane
+ * prefetch for long blocks.  Automatic: aligned batches take 2 when 512 <= the largest block
  * <= 703 bytes, else 1; unaligned batches (a block not 4-byte aligned) take 3
  * for blocks >= 8 KiB, else 0 (1 and 2 fall back to 0 there).  The
  * environment variable RSG_BLOCKSUMS_KERNEL sets the initial value.  Returns
@@ -155,8 +155,9 @@ rsg_status rsg_set_block_sums_kernel(int32_t variant);
 /* Timing diagnostics for DESIGN.md's roofline analysis, NOT for use: while
  * diag != 0 every aligned block-sum launch runs the diagnostic instead of the
  * product kernel and the "records" it writes are meaningless.  1 = staged
- * memory only, 2 = staged hashing only, 3 = park memory only, 4 = linear read
- * of the arena (plain loads), 5 = linear read (LDS DMA).  0 = off (default;
+ * memory only, 2 = staged hashing only, 3 = park memory only, 4 = park
+ * hashing only, 5 = linear read of the arena (plain loads), 6 = linear read
+ * (LDS DMA).  0 = off (default;
  * environment RSG_BLOCKSUMS_DIAG).  Kept apart from rsg_set_block_sums_kernel
  * so the product knob can never select a diagnostic. */
 rsg_status rsg_set_block_sums_diagnostic(int32_t diag);

@@ -474,11 +474,14 @@ __global__ __launch_bounds__(256) void diag_linear_read(const uint8_t *__restric
 // blocks (45 KiB) is fetched as one near-linear LDS-DMA burst, and each
 // block then parks in its lane's VGPRs (176 registers) while it is hashed,
 // so LDS only holds tiles in transit.  One persistent 8-wave workgroup per CU:
-//   wave 0 (loader) locates the tiles of this workgroup (scalar loads, no
-//     vmcnt coupling with its DMA), writes their block lengths to LDS and
-//     keeps up to three tiles' DMA in flight in a 3-slot ring;
-//   waves 1..7 (hashers) take tiles in order by an LDS ticket, copy the slot
-//     into registers, free it, hash 64 blocks and store the records.
+//   waves 0..NL-1 (loaders; NL = 3: one per slot of the 3-slot ring) locate
+//     their tiles (scalar loads, no vmcnt coupling with the DMA), write the
+//     block lengths to LDS and DMA the tile.  A wave's vmcnt is a 6-bit
+//     counter (at most 63 DMA instructions = 63 KiB in flight per wave), so
+//     one loader cannot keep the ring full: three loaders keep up to three
+//     tiles (135 KiB) in flight per CU;
+//   the other waves (hashers) take tiles in order by an LDS ticket, copy the
+//     slot into registers, free it, hash 64 blocks and store the records.
 // LDS handshake per slot: full[s] = the ticket it holds (set by the loader
 // after its covering vmcnt), freeq[s] = the ticket it may take next (set by
 // the hasher once its ds_reads of the slot completed).  Tiles that cannot be
@@ -668,7 +671,8 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
     store_record(out, g, nn, s1, tw, h);
 }
 
-// MODE 0 = product; 1 = memory only (diagnostic: DMA + copy, no hashing).
+// MODE 0 = product; diagnostics: 1 = memory only (DMA + copy, no hashing),
+// 2 = hashing only (no DMA: the hashers hash whatever the slots hold).
 // The tile DMA uses the nt cache policy (aux = 2): every byte is read once.
 // NL = loader waves (1 or 2); the other 8 - NL waves hash.
 template <int MODE, int NL>
@@ -705,8 +709,9 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
         // whose slot k % 3 it owns (NL = 2: loader 0 slots 0 and 2, loader 1
         // slot 1), so each loader's tiles sit in its own vmcnt.
         auto owned = [&](uint32_t kk) { return (kk % kPkSlots) % NL == wave; };
-        constexpr uint32_t kOwned0 = (kPkSlots + NL - 1) / NL;  // slots of loader 0
-        const bool single = (wave == 0 ? kOwned0 : (kPkSlots - kOwned0)) == 1;
+        uint32_t nown = 0;  // slots this loader owns
+        for (uint32_t sl = 0; sl < kPkSlots; sl++) nown += (sl % NL == wave) ? 1u : 0u;
+        const bool single = nown == 1;
         uint32_t k = 0;
         while (!owned(k)) k++;
         PkDesc cur;
@@ -722,7 +727,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             sh.n[slot][lane] = cur.n;
             if (lane == 0) sh.kind[slot] = cur.staged ? 1u : 0u;
             const bool staged = cur.staged;
-            if (staged) pk_issue<2, true>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
+            if (staged && MODE != 2) pk_issue<2, true>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
             uint32_t kn = k + 1;
             while (!owned(kn)) kn++;
             const uint64_t tn = blockIdx.x + (uint64_t)kn * G;
@@ -803,15 +808,17 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
 
 // Kernel variants (rsg_set_block_sums_kernel; identical results, only speed
 // differs): -1 = automatic, 0 = direct per-lane loads, 1 = staged LDS-DMA
-// slabs, 2 = park (loader wave + register-parked blocks, blocks <= 703 bytes),
-// 3 = long blocks with deep per-lane prefetch.  Automatic: aligned batches
-// take park when 512 <= max block <= 703, else staged; unaligned batches take
-// long when blocks are >= 8 KiB, else direct.
+// slabs, 2 = park (three loader waves + five hashers with register-parked
+// blocks, blocks <= 703 bytes), 3 = long blocks with deep per-lane prefetch.
+// Automatic: aligned batches take park when 512 <= max block <= 703, else
+// staged; unaligned batches take long when blocks are >= 8 KiB, else direct.
 //
 // Timing diagnostics (rsg_set_block_sums_diagnostic, a separate knob so the
 // product knob can never select one; their "records" are meaningless):
 // 1 = staged memory only, 2 = staged hashing only, 3 = park memory only,
-// 4 = linear read with plain loads, 5 = linear read with LDS DMA.
+// 4 = park hashing only, 5 = linear read with plain loads, 6 = linear read
+// with LDS DMA.
+constexpr int kParkLoaders = 3;  // 1 / 2 / 3 loaders measured
 static int g_variant = -2;  // -2 = not yet read from RSG_BLOCKSUMS_KERNEL
 static int g_diag = -2;     // -2 = not yet read from RSG_BLOCKSUMS_DIAG
 
@@ -830,13 +837,14 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     if (g_variant == -2) {
         const char *e = getenv("RSG_BLOCKSUMS_KERNEL");
         g_variant = e ? atoi(e) : -1;
-        if (g_variant < -1 || g_variant > 4) g_variant = -1;
+        if (g_variant < -1 || g_variant > 3) g_variant = -1;
     }
     if (g_diag == -2) {
         const char *e = getenv("RSG_BLOCKSUMS_DIAG");
         g_diag = e ? atoi(e) : 0;
     }
     const dim3 block(kBlockSumThreads), grid(nwg);
+    const dim3 pgrid(park_grid(total_blocks)), pblock(kPkThreads);
     if (g_diag > 0 && aligned) {
         switch (g_diag) {
             case 1:
@@ -849,19 +857,19 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                 break;
             case 3:
                 if (max_blen <= kRegMaxBytes)
-                    hipLaunchKernelGGL((block_sums_park<1, 1>), dim3(park_grid(total_blocks)), dim3(kPkThreads), 0, stream,
-                                       arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
-                break;
-            case 6:
-                if (max_blen <= kRegMaxBytes)
-                    hipLaunchKernelGGL((block_sums_park<1, 2>), dim3(park_grid(total_blocks)), dim3(kPkThreads), 0, stream,
-                                       arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+                    hipLaunchKernelGGL((block_sums_park<1, kParkLoaders>), pgrid, pblock, 0, stream, arena, arena_bytes,
+                                       files, wg_file, nwg, total_blocks, seed, out);
                 break;
             case 4:
+                if (max_blen <= kRegMaxBytes)
+                    hipLaunchKernelGGL((block_sums_park<2, kParkLoaders>), pgrid, pblock, 0, stream, arena, arena_bytes,
+                                       files, wg_file, nwg, total_blocks, seed, out);
+                break;
+            case 5:
                 hipLaunchKernelGGL(diag_linear_read<false>, dim3(2048), dim3(256), 0, stream, arena, arena_bytes,
                                    (uint32_t *)out);
                 break;
-            case 5:
+            case 6:
                 hipLaunchKernelGGL(diag_linear_read<true>, dim3(2048), dim3(256), 0, stream, arena, arena_bytes,
                                    (uint32_t *)out);
                 break;
@@ -873,20 +881,15 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         v = aligned ? ((max_blen <= kRegMaxBytes && max_blen >= kParkMinBytes) ? 2 : 1)
                     : (max_blen >= kLongBlockBytes ? 3 : 0);
     if (!aligned && (v == 1 || v == 2)) v = 0;  // the LDS-DMA kernels need 4-byte aligned blocks
-    if ((v == 2 || v == 4) && max_blen > kRegMaxBytes) v = 1;
-    if (v == 4 && !aligned) v = 0;
+    if (v == 2 && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
             hipLaunchKernelGGL(block_sums_staged<0>, grid, block, 0, stream, arena, arena_bytes, files, wg_file,
                                total_blocks, seed, out);
             break;
         case 2:
-            hipLaunchKernelGGL((block_sums_park<0, 1>), dim3(park_grid(total_blocks)), dim3(kPkThreads), 0, stream,
-                               arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
-            break;
-        case 4:  // experimental: two loader waves
-            hipLaunchKernelGGL((block_sums_park<0, 2>), dim3(park_grid(total_blocks)), dim3(kPkThreads), 0, stream,
-                               arena, arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders>), pgrid, pblock, 0, stream, arena, arena_bytes, files,
+                               wg_file, nwg, total_blocks, seed, out);
             break;
         case 3: {
             const dim3 g64((uint32_t)((total_blocks + 63) / 64)), b64(64);

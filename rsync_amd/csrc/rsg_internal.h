@@ -39,7 +39,7 @@ void set_block_sums_diagnostic(int d);
 constexpr uint32_t kScanTile = 32768;                          // source bytes per tile
 constexpr uint32_t kRollThreads = 1024;                        // lanes per roll workgroup
 constexpr uint32_t kRollPerThread = kScanTile / kRollThreads;  // consecutive offsets per lane
-constexpr uint32_t kFilterBits = 1u << 19;                     // 64 KiB LDS bitmap
+constexpr uint32_t kFilterBits = 1u << 20;                     // 128 KiB LDS filter
 
 struct TileAgg {     // per tile: whole tile and its first r = B % kScanTile bytes
     uint32_t a1, a2;  // sum x, sum (i - tile_start) * x
@@ -49,9 +49,17 @@ struct TilePrefix {  // at a tile start: P = sum_{i<j} x_i, Q = sum_{i<j} i * x_
     uint32_t p, q;
 };
 
-// Bitmap slot of a 32-bit weak sum (low half s1, high half s2).
-__host__ __device__ inline uint32_t filter_index_host(uint32_t sum) {
-    return ((sum & 0xffffu) ^ ((sum >> 16) << 3)) & (kFilterBits - 1);
+// Blocked Bloom filter of the basis weak sums (low half s1, high half s2):
+// every sum sets two bits of ONE 32-bit word, so a probe is one LDS read.
+// Word = the top bits of a multiplicative hash, bits = two 5-bit fields of a
+// second one.  With the 32768 sums of a 1 GiB basis at B = 32 KiB about
+// 0.4 % of non-matching offsets pass (a one-bit 64 KiB bitmap passed 6 %).
+__host__ __device__ inline uint32_t filter_word(uint32_t sum) {
+    return (sum * 0x9E3779B1u) >> (32 - 15);  // kFilterBits / 32 = 2^15 words
+}
+__host__ __device__ inline uint32_t filter_mask(uint32_t sum) {
+    const uint32_t g = (sum ^ (sum >> 15)) * 0x85EBCA6Bu;
+    return (1u << (g >> 27)) | (1u << ((g >> 22) & 31u));
 }
 
 // Exact table of basis weak sums: buckets of kBucketWays u64 entries

@@ -266,10 +266,7 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
         else keys.push_back({S.groups[i].first, f});
     }
     std::vector<uint32_t> bitmap(rsg::kFilterBits / 32, 0);
-    for (auto &kv : keys) {
-        const uint32_t fi = rsg::filter_index_host(kv.first);
-        bitmap[fi >> 5] |= 1u << (fi & 31);
-    }
+    for (auto &kv : keys) bitmap[rsg::filter_word(kv.first)] |= rsg::filter_mask(kv.first);
     uint32_t nb = 16;
     while (nb < keys.size() / 2) nb <<= 1;
     std::vector<uint64_t> table;

@@ -13,7 +13,7 @@
 //   roll       per tile, 1024 lanes x 32 consecutive offsets: initial window
 //              from the prefixes plus a workgroup scan, then the reference's
 //              own rolling update; each offset is tested against an exact-
-//              equivalent filter (64 KiB LDS bitmap keyed on the full 32-bit
+//              equivalent filter (128 KiB LDS blocked Bloom filter keyed on the full 32-bit
 //              sum, then an L2-resident hash table of the basis sums with the
 //              block lengths present) and survivors are appended as
 //              candidates.  Candidates are confirmed on the host side of the
@@ -153,7 +153,6 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(const TileAgg *__restri
 }
 
 // --------------------------------------------------------------- roll
-__device__ __forceinline__ uint32_t filter_index(uint32_t sum) { return filter_index_host(sum); }
 
 // Exact membership of a weak sum in the basis: 2-choice table of buckets of
 // kBucketWays entries {sum1 << 32 | flags} (flags: bit0 used, bit1 = a block
@@ -181,7 +180,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     const uint32_t *__restrict__ bitmap_g, const uint64_t *__restrict__ table, uint32_t bmask,
     uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count) {
     constexpr uint32_t kWaves = kRollThreads / 64;
-    __shared__ uint32_t bitmap[kFilterBits / 32];       // 64 KiB
+    __shared__ uint32_t bitmap[kFilterBits / 32];       // 128 KiB
     __shared__ uint2 queue[kWaves][kQueueCap];           // (tile-local offset, sum)
     __shared__ uint4 wsum[2][kWaves];                     // scan partials, double-buffered per tile
     for (uint32_t i = threadIdx.x; i < kFilterBits / 32; i += kRollThreads) bitmap[i] = bitmap_g[i];
@@ -318,7 +317,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                 for (int jj = 0; jj < G; jj++) {
                     const int j = g0 + jj;
                     sum[jj] = __builtin_amdgcn_perm(W2, W1, 0x05040100u);  // (W1 & 0xffff) | W2 << 16, match.go:106
-                    word[jj] = bitmap[filter_index(sum[jj]) >> 5];
+                    word[jj] = bitmap[filter_word(sum[jj])];
                     const int32_t xo = sx8(O[j >> 2], j & 3);
                     const int32_t xi = sx8(S[j >> 2], j & 3);
                     W1 += (uint32_t)(xi - xo);
@@ -326,7 +325,8 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                 }
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
-                    const bool hit = (word[jj] >> (filter_index(sum[jj]) & 31)) & 1u;
+                    const uint32_t m = filter_mask(sum[jj]);
+                    const bool hit = (word[jj] & m) == m;
                     park(hit, (uint32_t)(g0 + jj), sum[jj]);
                 }
             }
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                     const int j = g0 + jj;
                     const uint32_t qr = lo + j;
                     sum[jj] = __builtin_amdgcn_perm(W2, W1, 0x05040100u);
-                    word[jj] = bitmap[filter_index(sum[jj]) >> 5];
+                    word[jj] = bitmap[filter_word(sum[jj])];
                     // rolling update, match.go:171-196
                     const int32_t xo = sx8(O[j >> 2], j & 3);
                     const bool more = qr + k < size_rel;
@@ -353,7 +353,8 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                 }
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
-                    const bool hit = ((word[jj] >> (filter_index(sum[jj]) & 31)) & 1u) && (lo + g0 + jj < end_rel);
+                    const uint32_t m = filter_mask(sum[jj]);
+                    const bool hit = ((word[jj] & m) == m) && (lo + g0 + jj < end_rel);
                     park(hit, (uint32_t)(g0 + jj), sum[jj]);
                 }
             }
