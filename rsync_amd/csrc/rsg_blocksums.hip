@@ -555,18 +555,28 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
         return;
     }
     const uint64_t gend = min(g0 + 64, total_blocks);
+    const uint32_t fmax = wg_file[nwg256];  // the batch's last block's file: no tile needs a later one
     uint64_t off = 0;
     uint32_t n = 0;
+    // Small files (cfg4: 4-64 KiB) put up to ~11 files in a tile: four
+    // descriptors per step, their scalar loads issued together.
+    bool done = false;
 #pragma unroll 1
-    for (uint32_t f = __builtin_amdgcn_readfirstlane(lo);; f++) {
-        const DevFile F = files[f];
-        if (g >= F.first_block && g < F.first_block + F.nblocks) {
-            const uint64_t boff = (g - F.first_block) * F.blen;
-            const uint64_t left = F.len - boff;
-            n = left < F.blen ? (uint32_t)left : F.blen;  // generator.go:334
-            off = F.offset + boff;
+    for (uint32_t f = __builtin_amdgcn_readfirstlane(lo); !done; f += 4) {
+        DevFile F[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) F[i] = files[min(f + i, fmax)];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) {
+            if (done) break;
+            if (g >= F[i].first_block && g < F[i].first_block + F[i].nblocks) {
+                const uint64_t boff = (g - F[i].first_block) * F[i].blen;
+                const uint64_t left = F[i].len - boff;
+                n = left < F[i].blen ? (uint32_t)left : F[i].blen;  // generator.go:334
+                off = F[i].offset + boff;
+            }
+            done = F[i].first_block + F[i].nblocks >= gend || f + i >= fmax;
         }
-        if (F.first_block + F.nblocks >= gend) break;
     }
     const uint64_t lo_v = wave_min_u64(n ? off : ~0ull);
     d.base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo_v >> 32)) << 32) |

@@ -51,15 +51,14 @@ struct TilePrefix {  // at a tile start: P = sum_{i<j} x_i, Q = sum_{i<j} i * x_
 
 // Blocked Bloom filter of the basis weak sums (low half s1, high half s2):
 // every sum sets two bits of ONE 32-bit word, so a probe is one LDS read.
-// Word = the top bits of a multiplicative hash, bits = two 5-bit fields of a
-// second one.  With the 32768 sums of a 1 GiB basis at B = 32 KiB about
-// 0.4 % of non-matching offsets pass (a one-bit 64 KiB bitmap passed 6 %).
-__host__ __device__ inline uint32_t filter_word(uint32_t sum) {
-    return (sum * 0x9E3779B1u) >> (32 - 15);  // kFilterBits / 32 = 2^15 words
-}
-__host__ __device__ inline uint32_t filter_mask(uint32_t sum) {
-    const uint32_t g = (sum ^ (sum >> 15)) * 0x85EBCA6Bu;
-    return (1u << (g >> 27)) | (1u << ((g >> 22) & 31u));
+// h = sum * golden ratio; word = h's top 15 bits, bits = h[5:9] and h[10:14]
+// (two bfe + one lshl_or on the GPU).  With the 32768 sums of a 1 GiB basis
+// at B = 32 KiB, 0.7 % of non-matching offsets pass (simulated on uniform
+// sums; a one-bit 64 KiB bitmap passed 6 %).
+__host__ __device__ inline uint32_t filter_hash(uint32_t sum) { return sum * 0x9E3779B1u; }
+__host__ __device__ inline uint32_t filter_word(uint32_t h) { return h >> (32 - 15); }  // 2^15 words
+__host__ __device__ inline uint32_t filter_mask(uint32_t h) {
+    return (1u << ((h >> 5) & 31u)) | (1u << ((h >> 10) & 31u));
 }
 
 // Exact table of basis weak sums: buckets of kBucketWays u64 entries

@@ -74,6 +74,26 @@ struct Search {
     }
 };
 
+// Candidate offsets arrive in atomic-append order: LSD radix sort on 16-bit
+// digits (as many passes as the largest offset needs), std::sort for few.
+void sort_offsets(std::vector<uint64_t> &C) {
+    if (C.size() < 4096) {
+        std::sort(C.begin(), C.end());
+        return;
+    }
+    uint64_t mx = 0;
+    for (uint64_t c : C) mx = std::max(mx, c);
+    std::vector<uint64_t> tmp(C.size());
+    std::vector<uint32_t> cnt(65537);
+    for (int shift = 0; shift < 64 && (mx >> shift) != 0; shift += 16) {
+        std::fill(cnt.begin(), cnt.end(), 0u);
+        for (uint64_t c : C) cnt[((c >> shift) & 0xffffu) + 1]++;
+        for (size_t h = 1; h < cnt.size(); h++) cnt[h] += cnt[h - 1];
+        for (uint64_t c : C) tmp[cnt[(c >> shift) & 0xffffu]++] = c;
+        C.swap(tmp);
+    }
+}
+
 // Confirm a batch of candidates (indices into C): Checksum1 + MD4(window ||
 // seed) on the GPU, then the first block in targets order whose sums and
 // length agree.  res[i]: -2 unknown, -1 no match, else the block index.
@@ -266,7 +286,10 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
         else keys.push_back({S.groups[i].first, f});
     }
     std::vector<uint32_t> bitmap(rsg::kFilterBits / 32, 0);
-    for (auto &kv : keys) bitmap[rsg::filter_word(kv.first)] |= rsg::filter_mask(kv.first);
+    for (auto &kv : keys) {
+        const uint32_t h = rsg::filter_hash(kv.first);
+        bitmap[rsg::filter_word(h)] |= rsg::filter_mask(h);
+    }
     uint32_t nb = 16;
     while (nb < keys.size() / 2) nb <<= 1;
     std::vector<uint64_t> table;
@@ -327,7 +350,7 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
             RSG_HIP(ctx, hipStreamSynchronize(S.st));
         }
         pt.mark("roll");
-        std::sort(C.begin(), C.end());
+        sort_offsets(C);
         C.erase(std::unique(C.begin(), C.end()), C.end());
         if ((s = walk(S, C, pos)) != RSG_OK) return s;
         pt.mark("walk");

@@ -206,7 +206,15 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         }
     };
 
-    for (uint32_t t = tile_lo + blockIdx.x; t < tile_hi; t += gridDim.x) {
+    // Each workgroup takes a contiguous run of tiles: the shifted window
+    // bytes [q + B, ...) it reads for tile t are tile t + B/32K's own bytes,
+    // which the same workgroup reads a few tiles later, so they come from its
+    // XCD's L2 instead of HBM (with tiles dealt round-robin the two reads
+    // land on different XCDs).
+    const uint32_t per = (tile_hi - tile_lo + gridDim.x - 1) / gridDim.x;
+    const uint32_t t_begin = tile_lo + blockIdx.x * per;
+    const uint32_t t_end = min(tile_hi, t_begin + per);
+    for (uint32_t t = t_begin; t < t_end; t++) {
         const uint64_t q0 = (uint64_t)t * kScanTile;
         if (q0 >= end) break;  // uniform
         const uint32_t lo = threadIdx.x * kRollPerThread;  // local offset of this lane's first offset
@@ -312,12 +320,13 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
             const int32_t B16 = (int32_t)(B & 0xffffu);
 #pragma unroll
             for (int g0 = 0; g0 < (int)kRollPerThread; g0 += G) {
-                uint32_t sum[G], word[G];
+                uint32_t sum[G], word[G], fh[G];
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
                     const int j = g0 + jj;
                     sum[jj] = __builtin_amdgcn_perm(W2, W1, 0x05040100u);  // (W1 & 0xffff) | W2 << 16, match.go:106
-                    word[jj] = bitmap[filter_word(sum[jj])];
+                    fh[jj] = filter_hash(sum[jj]);
+                    word[jj] = bitmap[filter_word(fh[jj])];
                     const int32_t xo = sx8(O[j >> 2], j & 3);
                     const int32_t xi = sx8(S[j >> 2], j & 3);
                     W1 += (uint32_t)(xi - xo);
@@ -325,7 +334,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                 }
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
-                    const uint32_t m = filter_mask(sum[jj]);
+                    const uint32_t m = filter_mask(fh[jj]);
                     const bool hit = (word[jj] & m) == m;
                     park(hit, (uint32_t)(g0 + jj), sum[jj]);
                 }
@@ -336,13 +345,14 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
             const uint32_t size_rel = (uint32_t)min<uint64_t>(size > q0 ? size - q0 : 0, 0xFFFFFFFFull);
 #pragma unroll
             for (int g0 = 0; g0 < (int)kRollPerThread; g0 += G) {
-                uint32_t sum[G], word[G];
+                uint32_t sum[G], word[G], fh[G];
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
                     const int j = g0 + jj;
                     const uint32_t qr = lo + j;
                     sum[jj] = __builtin_amdgcn_perm(W2, W1, 0x05040100u);
-                    word[jj] = bitmap[filter_word(sum[jj])];
+                    fh[jj] = filter_hash(sum[jj]);
+                    word[jj] = bitmap[filter_word(fh[jj])];
                     // rolling update, match.go:171-196
                     const int32_t xo = sx8(O[j >> 2], j & 3);
                     const bool more = qr + k < size_rel;
@@ -353,7 +363,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                 }
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
-                    const uint32_t m = filter_mask(sum[jj]);
+                    const uint32_t m = filter_mask(fh[jj]);
                     const bool hit = ((word[jj] & m) == m) && (lo + g0 + jj < end_rel);
                     park(hit, (uint32_t)(g0 + jj), sum[jj]);
                 }
