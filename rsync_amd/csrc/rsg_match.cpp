@@ -198,7 +198,7 @@ rsg_status walk(Search &S, const std::vector<uint64_t> &C, uint64_t &pos) {
         if (b >= 0) {
             S.out.push_back(rsg_match{(int64_t)c, b, 0});
             pos = c + (uint64_t)S.len_of(b);  // match.go:158 + the roll
-            i = std::lower_bound(C.begin() + i, C.end(), pos) - C.begin();
+            while (i < C.size() && C[i] < pos) i++;  // each candidate is stepped over once
         } else {
             pos = c + 1;
             i++;

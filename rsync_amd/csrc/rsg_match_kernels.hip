@@ -214,26 +214,50 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     const uint32_t per = (tile_hi - tile_lo + gridDim.x - 1) / gridDim.x;
     const uint32_t t_begin = tile_lo + blockIdx.x * per;
     const uint32_t t_end = min(tile_hi, t_begin + per);
+    const uint32_t lo = threadIdx.x * kRollPerThread;  // local offset of this lane's first offset
+    const uint32_t sh = B & 3u;  // (q0 + lo + B) & 3: q0, lo are multiples of 32
+    // own bytes [qt, qt+32) and the 4-byte aligned shifted bytes around
+    // [qt+B, qt+B+32) of tile t; the next tile's are loaded while this one
+    // is scanned (one workgroup per CU: nothing else would hide the latency)
+    uint32_t O[8], A[12], On[8];
+    // Plain 16-byte loads (no end-of-source guards): for tiles whose own and
+    // shifted bytes lie inside the source.
+    auto fetch_plain = [&](uint32_t tt, uint32_t *o, uint32_t *a) {
+        const uint8_t *p = src + (uint64_t)tt * kScanTile + lo;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const u32x4a4m v = *reinterpret_cast<const u32x4a4m *>(p + 16 * q);
+            o[4 * q] = v.x; o[4 * q + 1] = v.y; o[4 * q + 2] = v.z; o[4 * q + 3] = v.w;
+        }
+        const uint8_t *pa = p + B - sh;
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            const u32x4a4m v = *reinterpret_cast<const u32x4a4m *>(pa + 16 * q);
+            a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
+        }
+    };
+    auto interior = [&](uint32_t tt) { return (uint64_t)(tt + 1) * kScanTile + B + 48 <= size; };
+    bool have = false;  // O, A already hold tile t's bytes (prefetched)
     for (uint32_t t = t_begin; t < t_end; t++) {
         const uint64_t q0 = (uint64_t)t * kScanTile;
         if (q0 >= end) break;  // uniform
-        const uint32_t lo = threadIdx.x * kRollPerThread;  // local offset of this lane's first offset
         const uint64_t qt = q0 + lo;
-        // own bytes [qt, qt+32) and shifted bytes [qt+B, qt+B+32)
-        uint32_t O[8], S[8];
-        load_vec(src, size, qt, O);
-        load_vec(src, size, qt + 16, O + 4);
-        {
-            const uint64_t ps = qt + B;
-            const uint32_t sh = (uint32_t)(ps & 3u);  // uniform across the workgroup
-            const uint64_t pa = ps - sh;
-            uint32_t A[12];
+        if (!have) {
+            load_vec(src, size, qt, O);
+            load_vec(src, size, qt + 16, O + 4);
+            const uint64_t pa = qt + B - sh;
             load_vec(src, size, pa, A);
             load_vec(src, size, pa + 16, A + 4);
             load_vec(src, size, pa + 32, A + 8);
-#pragma unroll
-            for (int k = 0; k < 8; k++) S[k] = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sh);
         }
+        uint32_t S[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) S[k] = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sh);
+        // the next tile's bytes load while this one is scanned (one workgroup
+        // per CU: nothing else would hide the latency); A is dead once S is
+        // built, so it takes the next tile's shifted bytes
+        const bool next = t + 1 < t_end && (uint64_t)(t + 1) * kScanTile < end && interior(t + 1);
+        if (next) fetch_plain(t + 1, On, A);
         int32_t o1, o2, s1, s2, v1, v2;
         vec_sums(O, o1, o2);
         vec_sums(O + 4, v1, v2);
@@ -258,10 +282,12 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         }
         if (lane == 63) wsum[parity][wave] = make_uint4(incl[0], incl[1], incl[2], incl[3]);
         __syncthreads();
+        // all 16 partials at once (broadcast reads, no dependent chain)
         uint4 add = make_uint4(0, 0, 0, 0);
-        for (uint32_t w = 0; w < wave; w++) {
+#pragma unroll
+        for (uint32_t w = 0; w < kWaves; w++) {
             const uint4 p = wsum[parity][w];
-            add.x += p.x; add.y += p.y; add.z += p.z; add.w += p.w;
+            if (w < wave) { add.x += p.x; add.y += p.y; add.z += p.z; add.w += p.w; }
         }
         const uint32_t ex[4] = {incl[0] - v[0] + add.x, incl[1] - v[1] + add.y, incl[2] - v[2] + add.z,
                                 incl[3] - v[3] + add.w};
@@ -287,6 +313,10 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
             W2 = (uint32_t)size * W1 - (tot.q - Qq);
             k = qt < size ? (uint32_t)(size - qt) : 0u;
         }
+        // An opaque copy of lo: without it the compiler hoists lo + j for all
+        // 32 offsets out of the tile loop (64 live registers, spilled).
+        uint32_t lol = lo;
+        asm volatile("" : "+v"(lol));
         uint32_t nq = 0;  // wave-uniform queue fill
         // Park one offset's filter hit in the wave's LDS queue (wave-uniform
         // branch on the ballot).  When the queue is full (repetitive data: most
@@ -300,12 +330,12 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                     if (hit) {
                         const uint32_t below = __builtin_amdgcn_mbcnt_hi(
                             (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                        queue[wave][nq + below] = make_uint2(lo + j, sum);
+                        queue[wave][nq + below] = make_uint2(lol + j, sum);
                     }
                     nq += nb;
                 } else if (hit) {
                     const uint32_t at = atomicAdd(count, 1u);
-                    if (at < cap) cand[at] = q0 + lo + j;
+                    if (at < cap) cand[at] = q0 + lol + j;
                 }
             }
         };
@@ -338,6 +368,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                     const bool hit = (word[jj] & m) == m;
                     park(hit, (uint32_t)(g0 + jj), sum[jj]);
                 }
+                __builtin_amdgcn_sched_barrier(0);  // groups stay apart: registers for the next tile's bytes
             }
         } else {
             // Edge tile (the file's end is near): 32-bit offsets relative to q0.
@@ -349,7 +380,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
                     const int j = g0 + jj;
-                    const uint32_t qr = lo + j;
+                    const uint32_t qr = lol + j;
                     sum[jj] = __builtin_amdgcn_perm(W2, W1, 0x05040100u);
                     fh[jj] = filter_hash(sum[jj]);
                     word[jj] = bitmap[filter_word(fh[jj])];
@@ -364,12 +395,18 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
                     const uint32_t m = filter_mask(fh[jj]);
-                    const bool hit = ((word[jj] & m) == m) && (lo + g0 + jj < end_rel);
+                    const bool hit = ((word[jj] & m) == m) && (lol + g0 + jj < end_rel);
                     park(hit, (uint32_t)(g0 + jj), sum[jj]);
                 }
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
         drain(q0, nq);
+        if (next) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) O[k] = On[k];
+        }
+        have = next;
     }
 }
 
