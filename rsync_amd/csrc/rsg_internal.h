@@ -51,15 +51,14 @@ struct TilePrefix {  // at a tile start: P = sum_{i<j} x_i, Q = sum_{i<j} i * x_
 
 // Blocked Bloom filter of the basis weak sums (low half s1, high half s2):
 // every sum sets two bits of ONE 32-bit word, so a probe is one LDS read.
-// h = sum * golden ratio; word = h's top 15 bits, bits = h[5:9] and h[10:14]
-// (two bfe + one lshl_or on the GPU).  With the 32768 sums of a 1 GiB basis
-// at B = 32 KiB, 0.7 % of non-matching offsets pass (simulated on uniform
-// sums; a one-bit 64 KiB bitmap passed 6 %).
-__host__ __device__ inline uint32_t filter_hash(uint32_t sum) { return sum * 0x9E3779B1u; }
-__host__ __device__ inline uint32_t filter_word(uint32_t h) { return h >> (32 - 15); }  // 2^15 words
-__host__ __device__ inline uint32_t filter_mask(uint32_t h) {
-    return (1u << ((h >> 5) & 31u)) | (1u << ((h >> 10) & 31u));
-}
+// h = rotl(sum, 13) ^ sum (two VALU: no multiply); word = h[2:16] (the LDS
+// byte address is h & 0x1fffc), bits = h[22:26] and h[27:31].  With the
+// 32768 sums of a 1 GiB basis at B = 32 KiB, 0.7 % of non-matching offsets
+// pass (simulated on uniform sums, as a multiplicative hash; a one-bit 64 KiB
+// bitmap passed 6 %).
+__host__ __device__ inline uint32_t filter_hash(uint32_t sum) { return ((sum << 13) | (sum >> 19)) ^ sum; }
+__host__ __device__ inline uint32_t filter_word(uint32_t h) { return (h >> 2) & 0x7fffu; }  // 2^15 words
+__host__ __device__ inline uint32_t filter_mask(uint32_t h) { return (1u << ((h >> 22) & 31u)) | (1u << (h >> 27)); }
 
 // Exact table of basis weak sums: buckets of kBucketWays u64 entries
 // {sum1 << 32 | flags}; a sum lives in bucket hash1 or hash2.

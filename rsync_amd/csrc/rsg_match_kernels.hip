@@ -32,6 +32,31 @@ __device__ __forceinline__ int32_t sx8(uint32_t w, int b) {
     return (int32_t)(w << (24 - 8 * b)) >> 24;  // SignExtend of byte b of w
 }
 
+// sx8(a, b) - sx8(c, b) and k * sx8(c, b) (k a 24-bit signed value) in one
+// VALU instruction each: SDWA operand byte selects with sign extension
+// (SignExtend, rsyncchecksum.go:24-27).  b must fold to a constant.
+__device__ __forceinline__ int32_t sub_sx8(uint32_t a, uint32_t c, int b) {
+    int32_t d;
+    switch (b) {
+        case 0: asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0" : "=v"(d) : "v"(a), "v"(c)); break;
+        case 1: asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_1" : "=v"(d) : "v"(a), "v"(c)); break;
+        case 2: asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:BYTE_2" : "=v"(d) : "v"(a), "v"(c)); break;
+        default: asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3" : "=v"(d) : "v"(a), "v"(c)); break;
+    }
+    return d;
+}
+__device__ __forceinline__ int32_t mul_sx8(int32_t k, uint32_t c, int b) {
+    int32_t m;
+    switch (b) {
+        case 0: asm("v_mul_i32_i24_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(m) : "v"(k), "v"(c)); break;
+        case 1: asm("v_mul_i32_i24_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(m) : "v"(k), "v"(c)); break;
+        case 2: asm("v_mul_i32_i24_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(m) : "v"(k), "v"(c)); break;
+        default: asm("v_mul_i32_i24_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(m) : "v"(k), "v"(c)); break;
+    }
+    return m;
+}
+
+
 // Four little-endian words of src[pos, pos+16); bytes at or past `size` read 0.
 // The fast path needs pos 4-byte aligned (the caller guarantees it).
 __device__ __forceinline__ void load_vec(const uint8_t *src, uint64_t size, uint64_t pos, uint32_t w[4]) {
@@ -172,7 +197,7 @@ __device__ __forceinline__ uint32_t table_flags(const uint64_t *__restrict__ tab
     return fl;
 }
 
-constexpr uint32_t kQueueCap = 192;  // bitmap hits parked per wave before the exact probes
+constexpr uint32_t kQueueCap = 96;  // bitmap hits parked per wave and tile before the exact probes
 
 __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
@@ -181,7 +206,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count) {
     constexpr uint32_t kWaves = kRollThreads / 64;
     __shared__ uint32_t bitmap[kFilterBits / 32];       // 128 KiB
-    __shared__ uint2 queue[kWaves][kQueueCap];           // (tile-local offset, sum)
+    __shared__ uint2 queue[kWaves][2][kQueueCap];        // (tile-local offset, sum), per tile parity
     __shared__ uint4 wsum[2][kWaves];                     // scan partials, double-buffered per tile
     for (uint32_t i = threadIdx.x; i < kFilterBits / 32; i += kRollThreads) bitmap[i] = bitmap_g[i];
     __syncthreads();
@@ -192,20 +217,26 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     const uint32_t rem_flag = (rem != 0 && rem != B) ? 4u : 2u;
     uint32_t parity = 0;
 
-    // exact probes of this wave's parked hits; true candidates go to `cand`
-    auto drain = [&](uint64_t q0, uint32_t n) {
-        for (uint32_t i = lane; i < n; i += 64) {
-            const uint2 e = queue[wave][i];
-            const uint64_t q = q0 + e.x;
-            const uint32_t k = (uint32_t)min<uint64_t>((uint64_t)B, size - q);
-            const uint32_t need = (k == B) ? 2u : ((k == rem) ? rem_flag : 0u);
-            if (table_flags(table, bmask, e.y) & need) {
-                const uint32_t at = atomicAdd(count, 1u);
-                if (at < cap) cand[at] = q;
-            }
+    // Exact probes of a wave's parked hits (one queue half = one tile); true
+    // candidates go to `cand`.  The probes of tile t are issued while tile
+    // t+1 is scanned (their L2 latency hides under the offset loop): one
+    // entry per lane is prefetched, any further ones are probed in place.
+    auto probe = [&](uint64_t q, uint32_t sum, uint32_t fl) {
+        const uint32_t k = (uint32_t)min<uint64_t>((uint64_t)B, size - q);
+        const uint32_t need = (k == B) ? 2u : ((k == rem) ? rem_flag : 0u);
+        if (fl & need) {
+            const uint32_t at = atomicAdd(count, 1u);
+            if (at < cap) cand[at] = q;
         }
     };
-
+    auto drain_rest = [&](uint32_t qh, uint64_t q0, uint32_t from, uint32_t n) {
+        for (uint32_t i = from + lane; i < n; i += 64) {
+            const uint2 e = queue[wave][qh][i];
+            probe(q0 + e.x, e.y, table_flags(table, bmask, e.y));
+        }
+    };
+    uint32_t prev_n = 0, qh = 0;  // entries parked by the previous tile, in queue half qh ^ 1
+    uint64_t prev_q0 = 0;
     // Each workgroup takes a contiguous run of tiles: the shifted window
     // bytes [q + B, ...) it reads for tile t are tile t + B/32K's own bytes,
     // which the same workgroup reads a few tiles later, so they come from its
@@ -258,6 +289,17 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         // built, so it takes the next tile's shifted bytes
         const bool next = t + 1 < t_end && (uint64_t)(t + 1) * kScanTile < end && interior(t + 1);
         if (next) fetch_plain(t + 1, On, A);
+        // the previous tile's first 64 parked hits: entry and bucket loads now
+        uint2 pe = make_uint2(0, 0);
+        uint64_t pb[2 * kBucketWays];
+        const bool pv = lane < prev_n;
+        if (pv) {
+            pe = queue[wave][qh ^ 1][lane];
+            const uint64_t *b1 = table + (uint64_t)(bucket_hash1(pe.y) & bmask) * kBucketWays;
+            const uint64_t *b2 = table + (uint64_t)(bucket_hash2(pe.y) & bmask) * kBucketWays;
+#pragma unroll
+            for (uint32_t i = 0; i < kBucketWays; i++) { pb[i] = b1[i]; pb[kBucketWays + i] = b2[i]; }
+        }
         int32_t o1, o2, s1, s2, v1, v2;
         vec_sums(O, o1, o2);
         vec_sums(O + 4, v1, v2);
@@ -292,7 +334,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         const uint32_t ex[4] = {incl[0] - v[0] + add.x, incl[1] - v[1] + add.y, incl[2] - v[2] + add.z,
                                 incl[3] - v[3] + add.w};
         parity ^= 1u;
-        // Lanes past `end` stay in the loop (they never hit): drain() spreads the
+        // Lanes past `end` stay in the loop (they never hit): the probes spread the
         // wave's parked hits over all 64 lanes.
         // P, Q at qt
         const uint32_t Pq = pre[t].p + ex[0];
@@ -330,7 +372,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                     if (hit) {
                         const uint32_t below = __builtin_amdgcn_mbcnt_hi(
                             (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                        queue[wave][nq + below] = make_uint2(lol + j, sum);
+                        queue[wave][qh][nq + below] = make_uint2(lol + j, sum);
                     }
                     nq += nb;
                 } else if (hit) {
@@ -347,7 +389,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
             // Interior tile: every offset is visited and every window has its
             // full length B and a byte entering (match.go:175-191 "more").
             // S2 only matters mod 2^16, so B*x uses B mod 2^16 (24-bit mul).
-            const int32_t B16 = (int32_t)(B & 0xffffu);
+            const int32_t negB16 = -(int32_t)(B & 0xffffu);
 #pragma unroll
             for (int g0 = 0; g0 < (int)kRollPerThread; g0 += G) {
                 uint32_t sum[G], word[G], fh[G];
@@ -357,10 +399,9 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                     sum[jj] = __builtin_amdgcn_perm(W2, W1, 0x05040100u);  // (W1 & 0xffff) | W2 << 16, match.go:106
                     fh[jj] = filter_hash(sum[jj]);
                     word[jj] = bitmap[filter_word(fh[jj])];
-                    const int32_t xo = sx8(O[j >> 2], j & 3);
-                    const int32_t xi = sx8(S[j >> 2], j & 3);
-                    W1 += (uint32_t)(xi - xo);
-                    W2 = W2 + (uint32_t)__mul24(-B16, xo) + W1;
+                    // W1 += xi - xo; W2 += W1 - B * xo (4 VALU, SDWA byte selects)
+                    W1 += (uint32_t)sub_sx8(S[j >> 2], O[j >> 2], j & 3);
+                    W2 = W2 + (uint32_t)mul_sx8(negB16, O[j >> 2], j & 3) + W1;
                 }
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
@@ -401,13 +442,24 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        drain(q0, nq);
+        if (pv) {
+            uint32_t fl = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 2 * kBucketWays; i++)
+                if ((uint32_t)(pb[i] >> 32) == pe.y && (uint32_t)pb[i] != 0) fl |= (uint32_t)pb[i];
+            probe(prev_q0 + pe.x, pe.y, fl);
+        }
+        if (prev_n > 64) drain_rest(qh ^ 1, prev_q0, 64, prev_n);
+        prev_n = nq;
+        prev_q0 = q0;
+        qh ^= 1u;
         if (next) {
 #pragma unroll
             for (int k = 0; k < 8; k++) O[k] = On[k];
         }
         have = next;
     }
+    drain_rest(qh ^ 1, prev_q0, 0, prev_n);  // the last tile's hits
 }
 
 // --------------------------------------------------------------- resolve
