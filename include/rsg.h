@@ -196,6 +196,32 @@ rsg_status rsg_hash_search_device(rsg_ctx *ctx, const void *d_src, uint64_t src_
                                   const uint8_t *sum2, const int32_t *targets, int32_t seed,
                                   rsg_match *matches, uint64_t match_cap, uint64_t *n_matches);
 
+/* Batched search over the files of a transfer: replaces SendFiles' per-file
+ * loop (sender.go:19-115) once their sums have been read, i.e. one
+ * hashSearch (sender.go:90) per job, in job order.  Jobs are pipelined: job
+ * i+1's basis tables and weak-sum scan run on the GPU while job i is walked
+ * and confirmed.  Each job's result equals the single-file call's.
+ * Every job's n_matches and status are set: RSG_OK, RSG_ERR_INVALID for its
+ * own bad arguments, RSG_ERR_TRUNCATED beyond match_cap (n_matches is the
+ * full count).  A HIP or allocation failure stops the batch: that job and
+ * the later ones get its status.  The call returns RSG_OK, or the first
+ * failing job's status with that job's message in rsg_last_error. */
+typedef struct rsg_search_job {
+    const void *src;         /* device pointer (_device) or host pointer (_host) */
+    uint64_t src_len;
+    rsg_sum_head head;
+    const uint32_t *sum1;    /* as rsg_hash_search_*                          */
+    const uint8_t *sum2;
+    const int32_t *targets;
+    rsg_match *matches;
+    uint64_t match_cap;
+    uint64_t n_matches;      /* out */
+    int32_t status;          /* out */
+    int32_t reserved;
+} rsg_search_job;
+rsg_status rsg_hash_search_batch_device(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed);
+rsg_status rsg_hash_search_batch_host(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed);
+
 /* Token stream of simpleSendToken (token.go:4-31) as matched() emits it
  * (match.go:233-282): literal runs in <= 256 KiB pieces (int32 LE n + n bytes),
  * a match as int32 -(i+1), terminated by int32 0 (match.go:212).  Host byte

@@ -54,6 +54,14 @@ class Match(ctypes.Structure):
     _fields_ = [("offset", ctypes.c_int64), ("index", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+class SearchJob(ctypes.Structure):
+    """rsg_search_job: one file of rsg_hash_search_batch_* (n_matches, status out)."""
+    _fields_ = [("src", ctypes.c_void_p), ("src_len", ctypes.c_uint64), ("head", SumHead),
+                ("sum1", ctypes.c_void_p), ("sum2", ctypes.c_void_p), ("targets", ctypes.c_void_p),
+                ("matches", ctypes.POINTER(Match)), ("match_cap", ctypes.c_uint64),
+                ("n_matches", ctypes.c_uint64), ("status", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
 _vp = ctypes.c_void_p
 _u64 = ctypes.c_uint64
 _i32 = ctypes.c_int32
@@ -89,6 +97,8 @@ _PROTOS = {
                                    ctypes.POINTER(Match), _u64, ctypes.POINTER(_u64)]),
     "rsg_hash_search_device": (_st, [_vp, _vp, _u64, ctypes.POINTER(SumHead), _vp, _vp, _vp, _i32,
                                      ctypes.POINTER(Match), _u64, ctypes.POINTER(_u64)]),
+    "rsg_hash_search_batch_device": (_st, [_vp, ctypes.POINTER(SearchJob), _u64, _i32]),
+    "rsg_hash_search_batch_host": (_st, [_vp, ctypes.POINTER(SearchJob), _u64, _i32]),
     "rsg_encode_tokens": (_st, [_vp, _u64, ctypes.POINTER(SumHead), ctypes.POINTER(Match), _u64,
                                 _vp, _u64, ctypes.POINTER(_u64)]),
     "rsg_apply_tokens": (_st, [_vp, _u64, ctypes.POINTER(SumHead), _vp, _u64, _vp, _u64,

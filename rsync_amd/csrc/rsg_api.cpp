@@ -259,12 +259,20 @@ void rsg_ctx_destroy(rsg_ctx *c) {
     for (int i = 0; i < 2; i++)
         if (c->side[i]) hipStreamSynchronize(c->side[i]);
     DevBuf *dbs[] = {&c->d_files, &c->d_wg, &c->d_in[0], &c->d_in[1], &c->d_out[0], &c->d_out[1],
-                     &c->d_desc[0], &c->d_desc[1], &c->d_fb[0], &c->d_fb[1], &c->d_agg, &c->d_prefix, &c->d_bits, &c->d_counts,
-                     &c->d_list, &c->d_table, &c->d_filter, &c->d_misc, &c->d_groups, &c->d_hi16, &c->d_sum2,
-                     &c->d_res};
+                     &c->d_desc[0], &c->d_desc[1], &c->d_fb[0], &c->d_fb[1], &c->d_res};
     for (DevBuf *b : dbs)
         if (b->p) hipFree(b->p);
-    PinBuf *pbs[] = {&c->h_in[0], &c->h_in[1], &c->h_out[0], &c->h_out[1], &c->h_desc[0], &c->h_desc[1], &c->h_misc};
+    for (SearchSlot &sl : c->search) {
+        DevBuf *sbs[] = {&sl.agg, &sl.prefix, &sl.counts, &sl.list, &sl.blob, &sl.src};
+        for (DevBuf *b : sbs)
+            if (b->p) hipFree(b->p);
+        if (sl.count.p) hipHostFree(sl.count.p);
+        if (sl.stage.p) hipHostFree(sl.stage.p);
+        if (sl.scanned) hipEventDestroy(sl.scanned);
+        if (sl.rolled) hipEventDestroy(sl.rolled);
+        if (sl.confirmed) hipEventDestroy(sl.confirmed);
+    }
+    PinBuf *pbs[] = {&c->h_in[0], &c->h_in[1], &c->h_out[0], &c->h_out[1], &c->h_desc[0], &c->h_desc[1]};
     for (PinBuf *b : pbs)
         if (b->p) hipHostFree(b->p);
     if (c->comm) ncclCommDestroy(c->comm);

@@ -23,10 +23,24 @@ struct PinBuf {
     uint64_t cap = 0;
 };
 
+// Sender scratch of one search in flight; a batch rotates three of them so
+// later files' tables and kernels overlap file i's walk (rsg_match.cpp).
+struct SearchSlot {
+    DevBuf agg, prefix, counts, list;  // tile sums, tile prefixes, candidate count and list
+    DevBuf blob;                       // basis tables, one upload: groups | hi16 | sum2 | filter | table
+    DevBuf src;                        // realigned or uploaded source
+    PinBuf stage;                      // pinned staging of the blob
+    PinBuf count;                      // candidate count read back
+    hipEvent_t scanned = nullptr;      // prefix pass done (side stream)
+    hipEvent_t rolled = nullptr;       // roll kernel + count read-back done
+    hipEvent_t confirmed = nullptr;    // confirmation batch + result read-back done
+};
+constexpr int kSearchSlots = 3;  // jobs i (walking), i+1 (rolled or rolling), i+2 (being issued)
+
 struct rsg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t side[2] = {nullptr, nullptr};  // host-path pipeline streams
+    hipStream_t side[2] = {nullptr, nullptr};  // host-path pipeline streams; sender search slots
     hipEvent_t side_done[2] = {nullptr, nullptr};
     std::recursive_mutex mu;
     std::string err;
@@ -35,9 +49,8 @@ struct rsg_ctx {
     DevBuf d_in[2], d_out[2], d_desc[2], d_fb[2];
     PinBuf h_in[2], h_out[2], h_desc[2];
     // sender scratch
-    DevBuf d_agg, d_prefix, d_bits, d_counts, d_list, d_table, d_filter, d_misc;
-    DevBuf d_groups, d_hi16, d_sum2, d_res;  // resolve tables (basis sums grouped by Sum1)
-    PinBuf h_misc;
+    SearchSlot search[kSearchSlots];
+    DevBuf d_res;
     // multi-GPU
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;

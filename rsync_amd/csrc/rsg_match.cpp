@@ -20,6 +20,9 @@
 #include <algorithm>
 #include <chrono>
 #include <climits>
+#include <functional>
+#include <memory>
+#include <string>
 #include <unordered_map>
 #include <vector>
 
@@ -51,13 +54,13 @@ struct PhaseTimer {
 };
 
 struct Search {
-    PhaseTimer *pt;
+    PhaseTimer pt;
     rsg_ctx *ctx;
+    SearchSlot *sl;
     hipStream_t st;
     const uint8_t *d_src;
     uint64_t size;
     rsg_sum_head head;
-    const uint8_t *sum2;
     int32_t seed;
     int64_t end;  // visited offsets are q < end (end >= 1: offset 0 is always visited)
     // (sum1, block) in targets order, stably sorted by sum1: each sum's blocks
@@ -65,6 +68,19 @@ struct Search {
     std::vector<std::pair<uint32_t, int32_t>> groups;
     std::vector<uint32_t> hi16;  // groups index of the first sum with a given high half (65537 entries)
     std::vector<rsg_match> out;
+    hipStream_t side = nullptr;  // prefix pass (beside the previous file's roll)
+    hipStream_t copy = nullptr;  // candidate read-back
+    // Called once, right after the first confirmation batch is issued (or at
+    // the end of finish() if none is): the batch issues a later job there.
+    std::function<rsg_status()> hook;
+    // device tables inside the slot's blob
+    uint64_t off_hi16 = 0, off_sum2 = 0, off_filter = 0, off_table = 0, blob_bytes = 0;
+    const uint2 *d_groups = nullptr;
+    const uint32_t *d_hi16 = nullptr, *d_filter = nullptr;
+    const uint8_t *d_sum2 = nullptr;
+    const uint64_t *d_table = nullptr;
+    uint32_t ntiles = 0, tile_end = 0, bmask = 0, cus = 256;
+    bool pending = false;  // prepare() launched the roll of [0, tile_end) and its count read-back
 
     int64_t len_of(int32_t i) const {
         return (i == head.count - 1 && head.rem != 0) ? head.rem : head.block_len;  // sender.go:135-139
@@ -121,7 +137,7 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
     for (uint32_t w = 0; w <= plan.nwg; w++)
         plan.wg_file[w] = (uint32_t)std::min<uint64_t>((uint64_t)w * rsg::kBlockSumThreads, idx.size() - 1);
     rsg_status s;
-    S.pt->mark("v.plan");
+    S.pt.mark("v.plan");
     if ((s = ensure_dev(ctx, ctx->d_files, plan.files.size() * sizeof(DevFile) + 32)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, ctx->d_wg, plan.wg_file.size() * sizeof(uint32_t) + 4)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, ctx->d_out[0], plan.total_blocks * kRecordBytes)) != RSG_OK) return s;
@@ -138,17 +154,23 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
     // indices come back.
     if ((s = ensure_dev(ctx, ctx->d_res, plan.total_blocks * 4)) != RSG_OK) return s;
     RSG_HIP(ctx, rsg::launch_resolve((const uint8_t *)ctx->d_out[0].p, (const DevFile *)ctx->d_files.p,
-                                     plan.total_blocks, (const uint2 *)ctx->d_groups.p,
-                                     (const uint32_t *)ctx->d_hi16.p, (const uint8_t *)ctx->d_sum2.p,
+                                     plan.total_blocks, S.d_groups, S.d_hi16, S.d_sum2,
                                      S.head.count, S.head.block_len, S.head.rem, S.head.s2len,
                                      (int32_t *)ctx->d_res.p, S.st));
     if ((s = ensure_pin(ctx, ctx->h_out[0], plan.total_blocks * 4)) != RSG_OK) return s;
     const int32_t *found = (const int32_t *)ctx->h_out[0].p;
     RSG_HIP(ctx, hipMemcpyAsync(ctx->h_out[0].p, ctx->d_res.p, plan.total_blocks * 4, hipMemcpyDeviceToHost, S.st));
-    RSG_HIP(ctx, hipStreamSynchronize(S.st));
-    S.pt->mark("v.kernel");
+    if (!S.sl->confirmed) RSG_HIP(ctx, hipEventCreateWithFlags(&S.sl->confirmed, hipEventDisableTiming));
+    RSG_HIP(ctx, hipEventRecord(S.sl->confirmed, S.st));
+    if (S.hook) {  // the next job's work queues behind this batch, and the host builds its tables meanwhile
+        const std::function<rsg_status()> h = std::move(S.hook);
+        S.hook = nullptr;
+        if ((s = h()) != RSG_OK) return s;
+    }
+    RSG_HIP(ctx, hipEventSynchronize(S.sl->confirmed));
+    S.pt.mark("v.kernel");
     for (size_t i = 0; i < idx.size(); i++) res[idx[i]] = found[i];
-    S.pt->mark("v.resolve");
+    S.pt.mark("v.resolve");
     return RSG_OK;
 }
 
@@ -207,43 +229,22 @@ rsg_status walk(Search &S, const std::vector<uint64_t> &C, uint64_t &pos) {
     return RSG_OK;
 }
 
-rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_sum_head *head, const uint32_t *sum1,
-                  const uint8_t *sum2, const int32_t *targets, int32_t seed, rsg_match *matches, uint64_t match_cap,
-                  uint64_t *n_matches) {
-    PhaseTimer pt;
-    Search S;
-    S.pt = &pt;
-    S.seed = seed;
-    S.ctx = ctx;
-    S.st = ctx->stream;
-    S.d_src = d_src;
-    S.size = size;
-    S.head = *head;
-    S.sum2 = sum2;
-    const int64_t B = head->block_len;
-    const int32_t count = head->count;
-    const int64_t last_len = (head->rem != 0) ? head->rem : B;
-    S.end = std::max<int64_t>((int64_t)size + 1 - last_len, 1);  // match.go:70 (offset 0 always visited)
+rsg_status launch_range(Search &S, uint32_t lo, uint32_t hi);
 
-    // The prefix pass over the source needs only B: it runs on the GPU while
-    // the host builds the filter tables below.
-    const uint64_t ntiles64 = (size + kScanTile - 1) / kScanTile;
+// Stage 1 of a search, host part: the basis tables, packed into the slot's
+// pinned staging blob.  Basis sums grouped by Sum1 in targets order (resolve
+// tables); Bloom filter of every Sum1 + a 2-choice bucketed table {Sum1,
+// flags: bit1 = a block of length B, bit2 = the remainder block}.
+rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets) {
+    rsg_ctx *ctx = S.ctx;
+    SearchSlot &sl = *S.sl;
+    const int64_t B = S.head.block_len;
+    const int32_t count = S.head.count;
+    const int64_t last_len = (S.head.rem != 0) ? S.head.rem : B;
+    S.end = std::max<int64_t>((int64_t)S.size + 1 - last_len, 1);  // match.go:70 (offset 0 always visited)
+    const uint64_t ntiles64 = (S.size + kScanTile - 1) / kScanTile;
     if (ntiles64 >= 0xFFFFFFF0ull) return fail(ctx, RSG_ERR_INVALID, "source too large");
-    const uint32_t ntiles = (uint32_t)ntiles64;
-    rsg_status s;
-    if ((s = ensure_dev(ctx, ctx->d_agg, (uint64_t)ntiles * sizeof(TileAgg) + 64)) != RSG_OK) return s;
-    if ((s = ensure_dev(ctx, ctx->d_prefix, ((uint64_t)ntiles + 1) * sizeof(TilePrefix) + 64)) != RSG_OK) return s;
-    if ((s = ensure_dev(ctx, ctx->d_list, (uint64_t)kCandCap * 8)) != RSG_OK) return s;
-    if ((s = ensure_dev(ctx, ctx->d_counts, 64)) != RSG_OK) return s;
-    {
-        const uint32_t r = (uint32_t)(B % kScanTile);
-        RSG_HIP(ctx, rsg::launch_tile_agg(d_src, size, r, (TileAgg *)ctx->d_agg.p, ntiles, S.st));
-        RSG_HIP(ctx, rsg::launch_tile_scan((const TileAgg *)ctx->d_agg.p, ntiles, (TilePrefix *)ctx->d_prefix.p, S.st));
-    }
-
-    // Basis sums grouped by Sum1 in targets order; device filter = bitmap of
-    // every Sum1 + a 2-choice bucketed table {Sum1, flags: bit1 = a block of
-    // length B, bit2 = the remainder block}.
+    S.ntiles = (uint32_t)ntiles64;
     {
         // Stable LSD radix sort (two 16-bit passes) of the targets-ordered
         // (sum1, block) list: equal sums keep their targets order.
@@ -265,20 +266,7 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
         for (auto &e : S.groups) S.hi16[(e.first >> 16) + 1]++;
         for (size_t h = 1; h < S.hi16.size(); h++) S.hi16[h] += S.hi16[h - 1];
     }
-    pt.mark("groups");
-    {
-        // device copies for the resolve kernel: (sum1, block) pairs, hi16 index, sum2
-        const uint64_t ng = S.groups.size();
-        if ((s = ensure_dev(ctx, ctx->d_groups, ng * 8 + 8)) != RSG_OK) return s;
-        if ((s = ensure_dev(ctx, ctx->d_hi16, S.hi16.size() * 4)) != RSG_OK) return s;
-        if ((s = ensure_dev(ctx, ctx->d_sum2, (uint64_t)count * 16 + 16)) != RSG_OK) return s;
-        static_assert(sizeof(S.groups[0]) == 8, "(sum1, block) pair must be 8 bytes");
-        if (ng) {
-            RSG_HIP(ctx, hipMemcpyAsync(ctx->d_groups.p, S.groups.data(), ng * 8, hipMemcpyHostToDevice, S.st));
-            RSG_HIP(ctx, hipMemcpyAsync(ctx->d_sum2.p, sum2, (uint64_t)count * 16, hipMemcpyHostToDevice, S.st));
-        }
-        RSG_HIP(ctx, hipMemcpyAsync(ctx->d_hi16.p, S.hi16.data(), S.hi16.size() * 4, hipMemcpyHostToDevice, S.st));
-    }
+    S.pt.mark("groups");
     std::vector<std::pair<uint32_t, uint32_t>> keys;  // distinct sum1 -> flags
     for (size_t i = 0; i < S.groups.size(); i++) {
         const uint32_t f = 1u | ((S.len_of(S.groups[i].second) == B) ? 2u : 4u);
@@ -293,9 +281,10 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
     uint32_t nb = 16;
     while (nb < keys.size() / 2) nb <<= 1;
     std::vector<uint64_t> table;
+    std::vector<uint8_t> fill;
     for (;;) {
         table.assign((size_t)nb * rsg::kBucketWays, 0);
-        std::vector<uint8_t> fill(nb, 0);
+        fill.assign(nb, 0);
         bool ok = true;
         for (auto &kv : keys) {
             const uint32_t h1 = rsg::bucket_hash1(kv.first) & (nb - 1), h2 = rsg::bucket_hash2(kv.first) & (nb - 1);
@@ -306,39 +295,112 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
         if (ok) break;
         nb <<= 1;
     }
-    pt.mark("tables");
-    if ((s = ensure_dev(ctx, ctx->d_filter, bitmap.size() * 4)) != RSG_OK) return s;
-    if ((s = ensure_dev(ctx, ctx->d_table, table.size() * 8)) != RSG_OK) return s;
-    const uint32_t bmask = nb - 1;
-    RSG_HIP(ctx, hipMemcpyAsync(ctx->d_filter.p, bitmap.data(), bitmap.size() * 4, hipMemcpyHostToDevice, S.st));
-    RSG_HIP(ctx, hipMemcpyAsync(ctx->d_table.p, table.data(), table.size() * 8, hipMemcpyHostToDevice, S.st));
+    S.bmask = nb - 1;
+    // blob layout, 256-byte aligned parts
+    static_assert(sizeof(S.groups[0]) == 8, "(sum1, block) pair must be 8 bytes");
+    auto up = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
+    const uint64_t n_groups = S.groups.size() * 8, n_hi16 = S.hi16.size() * 4, n_sum2 = (uint64_t)count * 16;
+    const uint64_t n_filter = bitmap.size() * 4, n_table = table.size() * 8;
+    S.off_hi16 = up(n_groups);
+    S.off_sum2 = S.off_hi16 + up(n_hi16);
+    S.off_filter = S.off_sum2 + up(n_sum2);
+    S.off_table = S.off_filter + up(n_filter);
+    S.blob_bytes = S.off_table + up(n_table);
+    rsg_status s;
+    if ((s = ensure_pin(ctx, sl.stage, S.blob_bytes)) != RSG_OK) return s;
+    uint8_t *st = (uint8_t *)sl.stage.p;
+    if (n_groups) memcpy(st, S.groups.data(), n_groups);
+    memcpy(st + S.off_hi16, S.hi16.data(), n_hi16);
+    if (n_sum2) memcpy(st + S.off_sum2, sum2, n_sum2);
+    memcpy(st + S.off_filter, bitmap.data(), n_filter);
+    memcpy(st + S.off_table, table.data(), n_table);
+    S.pt.mark("tables");
+    return RSG_OK;
+}
 
-    if (pt.on) {
-        RSG_HIP(ctx, hipStreamSynchronize(S.st));
-        pt.mark("agg+scan");
+// Stage 1, GPU part.  Side stream: (realigning copy,) prefix pass; compute
+// stream: blob upload, then after the prefix pass the roll over the whole
+// scan range and its candidate count read-back (event `rolled`).  The roll
+// queues behind whatever the compute stream holds (the previous file's roll),
+// never beside it.
+rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
+    rsg_ctx *ctx = S.ctx;
+    SearchSlot &sl = *S.sl;
+    rsg_status s;
+    if (!sl.scanned) RSG_HIP(ctx, hipEventCreateWithFlags(&sl.scanned, hipEventDisableTiming));
+    if (!sl.rolled) RSG_HIP(ctx, hipEventCreateWithFlags(&sl.rolled, hipEventDisableTiming));
+    if ((s = ensure_dev(ctx, sl.agg, (uint64_t)S.ntiles * sizeof(TileAgg) + 64)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, sl.prefix, ((uint64_t)S.ntiles + 1) * sizeof(TilePrefix) + 64)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, sl.list, (uint64_t)kCandCap * 8)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, sl.counts, 64)) != RSG_OK) return s;
+    if ((s = ensure_pin(ctx, sl.count, 64)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, sl.blob, S.blob_bytes)) != RSG_OK) return s;
+    if (host_src || ((uintptr_t)src & 15u)) {  // the scan kernels read 16-byte vectors at 16-byte strides
+        if ((s = ensure_dev(ctx, sl.src, S.size + 64)) != RSG_OK) return s;
+        RSG_HIP(ctx, hipMemcpyAsync(sl.src.p, src, S.size, host_src ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice,
+                                    S.side));
+        src = (const uint8_t *)sl.src.p;
     }
+    S.d_src = src;
+    const uint32_t r = (uint32_t)(S.head.block_len % kScanTile);
+    RSG_HIP(ctx, rsg::launch_tile_agg(S.d_src, S.size, r, (TileAgg *)sl.agg.p, S.ntiles, S.side));
+    RSG_HIP(ctx, rsg::launch_tile_scan((const TileAgg *)sl.agg.p, S.ntiles, (TilePrefix *)sl.prefix.p, S.side));
+    RSG_HIP(ctx, hipEventRecord(sl.scanned, S.side));
+
+    RSG_HIP(ctx, hipMemcpyAsync(sl.blob.p, sl.stage.p, S.blob_bytes, hipMemcpyHostToDevice, S.st));
+    const uint8_t *blob = (const uint8_t *)sl.blob.p;
+    S.d_groups = (const uint2 *)blob;
+    S.d_hi16 = (const uint32_t *)(blob + S.off_hi16);
+    S.d_sum2 = blob + S.off_sum2;
+    S.d_filter = (const uint32_t *)(blob + S.off_filter);
+    S.d_table = (const uint64_t *)(blob + S.off_table);
+    RSG_HIP(ctx, hipStreamWaitEvent(S.st, sl.scanned, 0));
+
     int dev_cus = 256;
     hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    const uint64_t scan_end = std::min<uint64_t>((uint64_t)S.end, size);
-    const uint32_t tile_end = (uint32_t)((scan_end + kScanTile - 1) / kScanTile);
-    uint32_t lo = 0, span = tile_end;
+    S.cus = (uint32_t)dev_cus;
+    const uint64_t scan_end = std::min<uint64_t>((uint64_t)S.end, S.size);
+    S.tile_end = (uint32_t)((scan_end + kScanTile - 1) / kScanTile);
+    if ((s = launch_range(S, 0, S.tile_end)) != RSG_OK) return s;
+    S.pending = true;
+    return RSG_OK;
+}
+
+// Roll kernel over tiles [lo, hi) + asynchronous read-back of its candidate
+// count, on the compute stream; event `rolled` marks both done.
+rsg_status launch_range(Search &S, uint32_t lo, uint32_t hi) {
+    rsg_ctx *ctx = S.ctx;
+    SearchSlot &sl = *S.sl;
+    RSG_HIP(ctx, hipMemsetAsync(sl.counts.p, 0, 4, S.st));
+    RSG_HIP(ctx, rsg::launch_roll(S.d_src, S.size, (uint32_t)S.head.block_len, (uint32_t)S.head.rem, (uint64_t)S.end,
+                                  lo, hi, (const TileAgg *)sl.agg.p, (const TilePrefix *)sl.prefix.p, S.ntiles,
+                                  S.d_filter, S.d_table, S.bmask, (uint64_t *)sl.list.p, kCandCap,
+                                  (uint32_t *)sl.counts.p, S.cus, S.st));
+    RSG_HIP(ctx, hipMemcpyAsync(sl.count.p, sl.counts.p, 4, hipMemcpyDeviceToHost, S.st));
+    RSG_HIP(ctx, hipEventRecord(sl.rolled, S.st));
+    return RSG_OK;
+}
+
+// Stage 2: candidates of each scan range back to the host (copy stream),
+// sorted, walked in match.go's greedy order with GPU confirmation on the
+// compute stream.  Synchronous.
+rsg_status finish(Search &S) {
+    rsg_ctx *ctx = S.ctx;
+    SearchSlot &sl = *S.sl;
+    uint32_t lo = 0, span = S.tile_end;
     uint64_t pos = 0;
     std::vector<uint64_t> C;
-    while (lo < tile_end) {
-        const uint32_t hi = std::min(tile_end, lo + span);
+    rsg_status s;
+    while (lo < S.tile_end) {
+        const uint32_t hi = std::min(S.tile_end, lo + span);
         if ((uint64_t)hi * kScanTile <= pos) {  // the walk already jumped past this range
             lo = hi;
             continue;
         }
-        RSG_HIP(ctx, hipMemsetAsync(ctx->d_counts.p, 0, 4, S.st));
-        RSG_HIP(ctx, rsg::launch_roll(d_src, size, (uint32_t)B, (uint32_t)head->rem, (uint64_t)S.end, lo, hi,
-                                      (const TileAgg *)ctx->d_agg.p, (const TilePrefix *)ctx->d_prefix.p, ntiles,
-                                      (const uint32_t *)ctx->d_filter.p, (const uint64_t *)ctx->d_table.p, bmask,
-                                      (uint64_t *)ctx->d_list.p, kCandCap, (uint32_t *)ctx->d_counts.p,
-                                      (uint32_t)dev_cus, S.st));
-        uint32_t n = 0;
-        RSG_HIP(ctx, hipMemcpyAsync(&n, ctx->d_counts.p, 4, hipMemcpyDeviceToHost, S.st));
-        RSG_HIP(ctx, hipStreamSynchronize(S.st));
+        if (!S.pending && (s = launch_range(S, lo, hi)) != RSG_OK) return s;
+        S.pending = false;
+        RSG_HIP(ctx, hipEventSynchronize(sl.rolled));
+        const uint32_t n = *(const volatile uint32_t *)sl.count.p;
         if (n > kCandCap) {  // dense range (repetitive data): halve it and retry
             if (hi - lo == 1) return fail(ctx, RSG_ERR_INVALID, "internal: candidate overflow in one tile");
             span = std::max<uint32_t>(1, (hi - lo) / 2);
@@ -346,22 +408,21 @@ rsg_status search(rsg_ctx *ctx, const uint8_t *d_src, uint64_t size, const rsg_s
         }
         C.resize(n);
         if (n) {
-            RSG_HIP(ctx, hipMemcpyAsync(C.data(), ctx->d_list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, S.st));
-            RSG_HIP(ctx, hipStreamSynchronize(S.st));
+            RSG_HIP(ctx, hipMemcpyAsync(C.data(), sl.list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, S.copy));
+            RSG_HIP(ctx, hipStreamSynchronize(S.copy));
         }
-        pt.mark("roll");
+        S.pt.mark("roll");
         sort_offsets(C);
         C.erase(std::unique(C.begin(), C.end()), C.end());
         if ((s = walk(S, C, pos)) != RSG_OK) return s;
-        pt.mark("walk");
+        S.pt.mark("walk");
         lo = hi;
     }
-    *n_matches = S.out.size();
-    const uint64_t ncopy = std::min<uint64_t>(S.out.size(), match_cap);
-    if (ncopy) memcpy(matches, S.out.data(), ncopy * sizeof(rsg_match));
-    if (S.out.size() > match_cap)
-        return fail(ctx, RSG_ERR_TRUNCATED, "%llu matches, capacity %llu", (unsigned long long)S.out.size(),
-                    (unsigned long long)match_cap);
+    if (S.hook) {
+        const std::function<rsg_status()> h = std::move(S.hook);
+        S.hook = nullptr;
+        return h();
+    }
     return RSG_OK;
 }
 
@@ -387,45 +448,169 @@ rsg_status check_args(rsg_ctx *ctx, const rsg_sum_head *head, const uint32_t *su
     return RSG_OK;
 }
 
+// Bad arguments and truncation belong to one job; anything else (HIP,
+// allocation) stops the batch.
+bool job_local(rsg_status s) { return s == RSG_ERR_INVALID || s == RSG_ERR_TRUNCATED; }
+
+// The jobs in order, three in flight (scratch slot i % 3).  Job i+1 is issued
+// before job i is finished, and job i+2 is issued from inside job i's
+// finish() as soon as its confirmation batch is queued, so on the GPU
+//   compute stream (side[0]):  roll(i+1) | confirm(i) | roll(i+2) | confirm(i+1) ...
+//   side stream (side[1]):     prefix pass(i+2) beside roll(i+1) / confirm(i)
+//   copy stream (ctx->stream): candidate read-back
+// while the host sorts and walks job i's candidates during roll(i+1) and
+// builds job i+2's tables during confirm(i).  Two files' kernels never share
+// the CUs except the memory-bound prefix pass: a confirmation kernel (few
+// lanes, serial MD4 chains) beside a roll kernel ran 3x slower.
+rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed, bool host_src) {
+    if (njobs && !jobs) return fail(ctx, RSG_ERR_INVALID, "NULL jobs");
+    for (uint64_t i = 0; i < njobs; i++) {
+        jobs[i].n_matches = 0;
+        jobs[i].status = RSG_OK;
+    }
+    rsg_status first = RSG_OK;
+    std::string first_err;
+    auto note = [&](uint64_t i, rsg_status st) {
+        jobs[i].status = st;
+        if (st != RSG_OK && first == RSG_OK) {
+            first = st;
+            first_err = ctx->err;
+        }
+    };
+    // Sources written on the context's stream (fills, copies) come first.
+    RSG_HIP(ctx, hipEventRecord(ctx->side_done[0], ctx->stream));
+    for (int k = 0; k < 2; k++) RSG_HIP(ctx, hipStreamWaitEvent(ctx->side[k], ctx->side_done[0], 0));
+
+    std::unique_ptr<Search> live[kSearchSlots];
+    // Validate job i and issue its stage 1.  Returns only fatal statuses; a
+    // job-local failure is recorded on the job, which then holds no search.
+    auto start = [&](uint64_t i) -> rsg_status {
+        rsg_search_job &j = jobs[i];
+        const int slot = (int)(i % kSearchSlots);
+        live[slot].reset();  // job i - 3 of this slot was finished, its GPU work waited for
+        rsg_status s = check_args(ctx, &j.head, j.sum1, j.sum2, j.targets, j.matches, j.match_cap, &j.n_matches);
+        if (s != RSG_OK) return note(i, s), RSG_OK;
+        if (j.head.count == 0 || j.src_len == 0) return RSG_OK;  // sendFile path / empty source: no matches
+        if (!j.src) return note(i, fail(ctx, RSG_ERR_INVALID, "NULL source")), RSG_OK;
+        std::unique_ptr<Search> S(new Search());
+        S->ctx = ctx;
+        S->sl = &ctx->search[slot];
+        S->st = ctx->side[0];
+        S->side = ctx->side[1];
+        S->copy = ctx->stream;
+        S->size = j.src_len;
+        S->head = j.head;
+        S->seed = seed;
+        if ((s = tables(*S, j.sum1, j.sum2, j.targets)) == RSG_OK) s = enqueue_scan(*S, (const uint8_t *)j.src, host_src);
+        if (s != RSG_OK) {
+            if (!job_local(s)) return s;
+            note(i, s);
+            return RSG_OK;
+        }
+        live[slot] = std::move(S);
+        return RSG_OK;
+    };
+    // RSG_SEARCH_OVERLAP=0: issue job i+1 only after job i is finished (A/B measurement)
+    const char *ov = getenv("RSG_SEARCH_OVERLAP");
+    const bool overlap = !(ov && ov[0] == '0');
+    rsg_status fatal = RSG_OK;
+    uint64_t i = 0;
+    if (njobs) fatal = start(0);
+    if (fatal == RSG_OK && overlap && njobs > 1) fatal = start(1);
+    for (; fatal == RSG_OK && i < njobs; i++) {
+        const uint64_t ahead = overlap ? i + 2 : i + 1;
+        auto next = [&, ahead]() -> rsg_status { return ahead < njobs ? start(ahead) : RSG_OK; };
+        Search *S = live[i % kSearchSlots].get();
+        if (!S) {
+            if ((fatal = next()) != RSG_OK) break;
+            continue;
+        }
+        S->hook = next;
+        rsg_status s = finish(*S);
+        if (s == RSG_OK) {
+            rsg_search_job &j = jobs[i];
+            j.n_matches = S->out.size();
+            const uint64_t ncopy = std::min<uint64_t>(S->out.size(), j.match_cap);
+            if (ncopy) memcpy(j.matches, S->out.data(), ncopy * sizeof(rsg_match));
+            if (S->out.size() > j.match_cap)
+                note(i, fail(ctx, RSG_ERR_TRUNCATED, "%llu matches, capacity %llu",
+                             (unsigned long long)S->out.size(), (unsigned long long)j.match_cap));
+        } else if (job_local(s)) {
+            note(i, s);
+        } else {
+            fatal = s;
+            break;
+        }
+        if (S->hook && (fatal = S->hook()) != RSG_OK) {  // finish() stopped early on a job-local error
+            i++;
+            break;
+        }
+        live[i % kSearchSlots].reset();
+    }
+    if (fatal != RSG_OK) {
+        const std::string msg = ctx->err;
+        for (uint64_t k = i; k < njobs; k++) jobs[k].status = fatal;
+        if (first == RSG_OK) {
+            first = fatal;
+            first_err = msg;
+        }
+    }
+    for (int k = 0; k < 2; k++) (void)hipStreamSynchronize(ctx->side[k]);  // nothing outlives the call
+    (void)hipStreamSynchronize(ctx->stream);
+    if (first != RSG_OK) ctx->err = first_err;
+    return first;
+}
+
 }  // namespace
 
 extern "C" {
 
-rsg_status rsg_hash_search_device(rsg_ctx *ctx, const void *d_src, uint64_t src_len, const rsg_sum_head *head,
-                                  const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets, int32_t seed,
-                                  rsg_match *matches, uint64_t match_cap, uint64_t *n_matches) {
+rsg_status rsg_hash_search_batch_device(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed) {
     if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
     std::lock_guard<std::recursive_mutex> lock(ctx->mu);
     RSG_HIP(ctx, hipSetDevice(ctx->device));
-    rsg_status s = check_args(ctx, head, sum1, sum2, targets, matches, match_cap, n_matches);
-    if (s != RSG_OK) return s;
-    *n_matches = 0;
-    if (head->count == 0 || src_len == 0) return RSG_OK;  // sendFile path / empty source: no matches
-    if (!d_src) return fail(ctx, RSG_ERR_INVALID, "NULL source");
-    const uint8_t *src = (const uint8_t *)d_src;
-    if ((uintptr_t)src & 15u) {  // the scan kernels read 16-byte vectors at 16-byte strides
-        if ((s = ensure_dev(ctx, ctx->d_misc, src_len + 64)) != RSG_OK) return s;
-        RSG_HIP(ctx, hipMemcpyAsync(ctx->d_misc.p, src, src_len, hipMemcpyDeviceToDevice, ctx->stream));
-        src = (const uint8_t *)ctx->d_misc.p;
-    }
-    return search(ctx, src, src_len, head, sum1, sum2, targets, seed, matches, match_cap, n_matches);
+    return search_batch(ctx, jobs, njobs, seed, false);
+}
+
+rsg_status rsg_hash_search_batch_host(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed) {
+    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    RSG_HIP(ctx, hipSetDevice(ctx->device));
+    return search_batch(ctx, jobs, njobs, seed, true);
+}
+
+// The single-file calls are batches of one.
+static rsg_status search_one(rsg_ctx *ctx, const void *src, uint64_t src_len, const rsg_sum_head *head,
+                             const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets, int32_t seed,
+                             rsg_match *matches, uint64_t match_cap, uint64_t *n_matches, bool host_src) {
+    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    RSG_HIP(ctx, hipSetDevice(ctx->device));
+    if (!head || !n_matches) return fail(ctx, RSG_ERR_INVALID, "NULL head or n_matches");
+    rsg_search_job j{};
+    j.src = src;
+    j.src_len = src_len;
+    j.head = *head;
+    j.sum1 = sum1;
+    j.sum2 = sum2;
+    j.targets = targets;
+    j.matches = matches;
+    j.match_cap = match_cap;
+    const rsg_status s = search_batch(ctx, &j, 1, seed, host_src);
+    *n_matches = j.n_matches;
+    return s;
+}
+
+rsg_status rsg_hash_search_device(rsg_ctx *ctx, const void *d_src, uint64_t src_len, const rsg_sum_head *head,
+                                  const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets, int32_t seed,
+                                  rsg_match *matches, uint64_t match_cap, uint64_t *n_matches) {
+    return search_one(ctx, d_src, src_len, head, sum1, sum2, targets, seed, matches, match_cap, n_matches, false);
 }
 
 rsg_status rsg_hash_search_host(rsg_ctx *ctx, const uint8_t *src, uint64_t src_len, const rsg_sum_head *head,
                                 const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets, int32_t seed,
                                 rsg_match *matches, uint64_t match_cap, uint64_t *n_matches) {
-    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
-    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
-    RSG_HIP(ctx, hipSetDevice(ctx->device));
-    rsg_status s = check_args(ctx, head, sum1, sum2, targets, matches, match_cap, n_matches);
-    if (s != RSG_OK) return s;
-    *n_matches = 0;
-    if (head->count == 0 || src_len == 0) return RSG_OK;
-    if (!src) return fail(ctx, RSG_ERR_INVALID, "NULL source");
-    if ((s = ensure_dev(ctx, ctx->d_misc, src_len + 64)) != RSG_OK) return s;
-    RSG_HIP(ctx, hipMemcpyAsync(ctx->d_misc.p, src, src_len, hipMemcpyHostToDevice, ctx->stream));
-    return search(ctx, (const uint8_t *)ctx->d_misc.p, src_len, head, sum1, sum2, targets, seed, matches,
-                  match_cap, n_matches);
+    return search_one(ctx, src, src_len, head, sum1, sum2, targets, seed, matches, match_cap, n_matches, true);
 }
 
 }  // extern "C"

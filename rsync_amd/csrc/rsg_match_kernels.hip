@@ -145,36 +145,60 @@ __global__ __launch_bounds__(256) void tile_agg_kernel(const uint8_t *__restrict
 
 // --------------------------------------------------------------- tile_scan
 // One workgroup: pre[t] = (P, Q) at the start of tile t (global byte index in
-// Q), pre[ntiles] = totals.  Tile t contributes (a1, a2 + t*T*a1).
+// Q), pre[ntiles] = totals.  Tile t contributes (a1, a2 + t*T*a1).  Rounds of
+// 1024 x 32 tiles; a thread owns 32 consecutive tiles of a round, loads them
+// all at once (independent loads: one memory latency per round, not one per
+// tile) and keeps them in registers for the write-out.
+constexpr uint32_t kScanPer = 32;
 __global__ __launch_bounds__(1024) void tile_scan_kernel(const TileAgg *__restrict__ agg, uint32_t ntiles,
                                                          TilePrefix *__restrict__ pre) {
-    __shared__ uint32_t sp[1024], sq[1024];
-    const uint32_t per = (ntiles + 1023) / 1024;
-    const uint32_t b = threadIdx.x * per, e = min(b + per, ntiles);
-    uint32_t p = 0, q = 0;
-    for (uint32_t t = b; t < e; t++) {
-        p += agg[t].a1;
-        q += agg[t].a2 + t * kScanTile * agg[t].a1;
-    }
-    sp[threadIdx.x] = p;
-    sq[threadIdx.x] = q;
-    __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
-        uint32_t vp = 0, vq = 0;
-        if (threadIdx.x >= d) { vp = sp[threadIdx.x - d]; vq = sq[threadIdx.x - d]; }
+    __shared__ uint32_t sp[16], sq[16];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t carry_p = 0, carry_q = 0;
+    for (uint64_t base = 0; base < ntiles; base += 1024ull * kScanPer) {
+        const uint64_t b = base + (uint64_t)threadIdx.x * kScanPer;
+        uint32_t c1[kScanPer], c2[kScanPer];
+#pragma unroll
+        for (uint32_t k = 0; k < kScanPer; k++) {
+            // branch-free: clamped loads, out-of-range tiles contribute 0
+            const uint64_t t = b + k;
+            const uint2 v = *reinterpret_cast<const uint2 *>(&agg[t < ntiles ? t : ntiles - 1]);
+            const uint32_t a1 = t < ntiles ? v.x : 0u, a2 = t < ntiles ? v.y : 0u;
+            c1[k] = a1;
+            c2[k] = a2 + (uint32_t)t * kScanTile * a1;
+        }
+        uint32_t p = 0, q = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kScanPer; k++) { p += c1[k]; q += c2[k]; }
+        // inclusive wave scan, then across the 16 waves
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t vp = __shfl_up(p, d, 64), vq = __shfl_up(q, d, 64);
+            if (lane >= d) { p += vp; q += vq; }
+        }
+        if (lane == 63) { sp[wave] = p; sq[wave] = q; }
         __syncthreads();
-        sp[threadIdx.x] += vp;
-        sq[threadIdx.x] += vq;
+        uint32_t wp = carry_p, wq = carry_q, tp = carry_p, tq = carry_q;
+        for (uint32_t w = 0; w < 16; w++) {
+            if (w < wave) { wp += sp[w]; wq += sq[w]; }
+            tp += sp[w];
+            tq += sq[w];
+        }
         __syncthreads();
+        // exclusive prefix of this thread's first tile
+        uint32_t xp = wp + __shfl_up(p, 1, 64), xq = wq + __shfl_up(q, 1, 64);
+        if (lane == 0) { xp = wp; xq = wq; }
+#pragma unroll
+        for (uint32_t k = 0; k < kScanPer; k++) {
+            const uint64_t t = b + k;
+            if (t < ntiles) pre[t] = TilePrefix{xp, xq};
+            xp += c1[k];
+            xq += c2[k];
+        }
+        carry_p = tp;
+        carry_q = tq;
     }
-    p = threadIdx.x ? sp[threadIdx.x - 1] : 0;
-    q = threadIdx.x ? sq[threadIdx.x - 1] : 0;
-    for (uint32_t t = b; t < e; t++) {
-        pre[t] = TilePrefix{p, q};
-        p += agg[t].a1;
-        q += agg[t].a2 + t * kScanTile * agg[t].a1;
-    }
-    if (threadIdx.x == 1023) pre[ntiles] = TilePrefix{sp[1023], sq[1023]};
+    if (threadIdx.x == 0) pre[ntiles] = TilePrefix{carry_p, carry_q};
 }
 
 // --------------------------------------------------------------- roll

@@ -352,6 +352,47 @@ class Engine:
                                          _ptr(s2), _ptr(tg), _i32(seed), out, cap, ctypes.byref(nm)), self.ctx)
         return _matches_list(out, nm.value)
 
+    def hash_search_batch(self, jobs, seed: int, device: bool = True, raise_on_error: bool = True,
+                          as_arrays: bool = False):
+        """SendFiles' per-file hashSearch loop (sender.go:19-115) in one
+        pipelined call.  jobs = [(src, src_len, head, sum1, sum2, targets)]:
+        src is a DeviceBuffer when device, else host bytes / a uint8 array
+        (src_len None = its length).  Returns one match list per job, or with
+        raise_on_error=False a list of (status, matches) pairs.  as_arrays:
+        matches stay the C-ABI's rsg_match records (numpy structured arrays
+        with fields offset / index), as a Go caller would read them."""
+        n = len(jobs)
+        arr = (_lib.SearchJob * max(n, 1))()
+        keep, outs = [], []
+        for k, (src, src_len, head, sum1, sum2, targets) in enumerate(jobs):
+            j = arr[k]
+            if device:
+                j.src, j.src_len = src.ptr, src_len
+            else:
+                a = _u8(src)
+                keep.append(a)
+                j.src, j.src_len = _ptr(a).value, a.size if src_len is None else src_len
+            j.head = head if isinstance(head, SumHead) else SumHead(*head)
+            s1 = np.ascontiguousarray(sum1, dtype=np.uint32)
+            s2 = np.ascontiguousarray(sum2, dtype=np.uint8).reshape(-1)
+            tg = np.ascontiguousarray(targets, dtype=np.int32)
+            keep += [s1, s2, tg]
+            j.sum1, j.sum2, j.targets = _ptr(s1).value, _ptr(s2).value, _ptr(tg).value
+            cap = j.src_len // max(j.head.block_len, 1) + 2
+            out = np.empty(cap, dtype=_MATCH_DT)
+            outs.append(out)
+            j.matches, j.match_cap = ctypes.cast(out.ctypes.data, ctypes.POINTER(Match)), cap
+        fn = lib.rsg_hash_search_batch_device if device else lib.rsg_hash_search_batch_host
+        st = fn(self.ctx, arr, n, _i32(seed))
+
+        def res(k):
+            m = outs[k][: arr[k].n_matches]
+            return m if as_arrays else _matches_list(m, len(m))
+        if raise_on_error:
+            check(st, self.ctx)
+            return [res(k) for k in range(n)]
+        return [(arr[k].status, res(k) if arr[k].status == _lib.OK else []) for k in range(n)]
+
     # ------------------------------------------------------------ multi-GPU
     @staticmethod
     def comm_unique_id() -> bytes:

@@ -141,3 +141,70 @@ def test_delta_round_trip_on_gpu(eng, seed_case):
     with pytest.raises(rsync_amd.RsgError) as e:
         eng.receive_data(bytes(bad), head, basis, seed)
     assert e.value.status == rsync_amd._lib.ERR_CORRUPT
+
+
+def _random_job(k, seed):
+    rng = np.random.default_rng(500 + k)
+    n = int(rng.integers(1, 400_000))
+    basis = cases.splitmix64_bytes(510 + k, n)
+    src = cases.mutate(basis, 520 + k, float(rng.uniform(0, 0.6)), 1, 3000,
+                       n_ins=int(rng.integers(0, 4)), n_del=int(rng.integers(0, 4)))
+    blen = int(rng.choice([0, 7, 333, 700, 4096, 40000]))
+    head, s1, s2 = basis_sums(basis, blen, seed)
+    return src, head, s1, s2, orc.stable_targets(s1)
+
+
+def test_batch_host_vs_oracle(eng):
+    """rsg_hash_search_batch_host: several files of one transfer in one
+    pipelined call equal the oracle file by file; an empty source, a count-0
+    head (sendFile path) and a job with bad targets in the middle are settled
+    on their own job without disturbing the others."""
+    import rsync_amd
+    seed = 0x1BADB002
+    jobs, want = [], []
+    for k in range(6):
+        src, head, s1, s2, tg = _random_job(k, seed)
+        jobs.append((src, None, head, s1, s2, tg))
+        want.append(orc.hash_search(src, head, s1, s2, tg, seed)[0])
+    src, head, s1, s2, tg = _random_job(6, seed)
+    jobs.insert(3, (src, None, head, s1, s2, np.zeros_like(tg)))  # not a permutation
+    want.insert(3, None)
+    jobs.append((np.zeros(0, np.uint8), None, head, s1, s2, tg))  # empty source
+    want.append([])
+    jobs.append((src, None, (0, 700, 16, 0), np.zeros(0, np.uint32), np.zeros(0, np.uint8),
+                 np.zeros(0, np.int32)))  # count 0
+    want.append([])
+    got = eng.hash_search_batch(jobs, seed, device=False, raise_on_error=False)
+    assert [st for st, _ in got] == [0, 0, 0, rsync_amd._lib.ERR_INVALID, 0, 0, 0, 0, 0]
+    for k, (st, m) in enumerate(got):
+        if want[k] is not None:
+            assert m == want[k], k
+    with pytest.raises(rsync_amd.RsgError) as e:
+        eng.hash_search_batch(jobs, seed, device=False)
+    assert "permutation" in str(e.value)
+    good = [j for k, j in enumerate(jobs) if want[k] is not None]
+    assert eng.hash_search_batch(good, seed, device=False) == [w for w in want if w is not None]
+
+
+def test_batch_device_matches_single(eng):
+    """Device-resident batch (one aligned and one misaligned source, two 64 MiB
+    cfg3-shaped files) equals the single-file calls and the oracle."""
+    seed = cases.SEED
+    bufs, jobs, want = [], [], []
+    for k in range(3):
+        basis = cases.splitmix64_bytes(30 + k, (64 << 20) if k < 2 else 300_000)
+        head, s1, s2 = basis_sums(basis, 0, seed)
+        src = cases.mutate(basis, 40 + k, 0.5, 1, 2 * head[1], n_ins=3, n_del=3)
+        tg = orc.stable_targets(s1)
+        shift = 5 if k == 2 else 0
+        buf = eng.alloc(src.size + 16)
+        buf.upload(np.concatenate([np.zeros(shift, np.uint8), src]))
+
+        class View:
+            ptr = buf.ptr + shift
+        bufs.append(buf)
+        jobs.append((View, src.size, head, s1, s2, tg))
+        want.append(orc.hash_search(src, head, s1, s2, tg, seed)[0])
+    got = eng.hash_search_batch(jobs, seed)
+    assert got == want
+    assert got == [eng.hash_search_device(*j, seed) for j in jobs]
