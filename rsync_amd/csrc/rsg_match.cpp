@@ -70,6 +70,7 @@ struct Search {
     std::vector<rsg_match> out;
     hipStream_t side = nullptr;  // prefix pass (beside the previous file's roll)
     hipStream_t copy = nullptr;  // candidate read-back
+    hipStream_t cst = nullptr;   // confirmation batches (the compute stream)
     // Called once, right after the first confirmation batch is issued (or at
     // the end of finish() if none is): the batch issues a later job there.
     std::function<rsg_status()> hook;
@@ -142,12 +143,12 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
     if ((s = ensure_dev(ctx, ctx->d_wg, plan.wg_file.size() * sizeof(uint32_t) + 4)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, ctx->d_out[0], plan.total_blocks * kRecordBytes)) != RSG_OK) return s;
     RSG_HIP(ctx, hipMemcpyAsync(ctx->d_files.p, plan.files.data(), plan.files.size() * sizeof(DevFile),
-                                hipMemcpyHostToDevice, S.st));
+                                hipMemcpyHostToDevice, S.cst));
     RSG_HIP(ctx, hipMemcpyAsync(ctx->d_wg.p, plan.wg_file.data(), plan.wg_file.size() * sizeof(uint32_t),
-                                hipMemcpyHostToDevice, S.st));
+                                hipMemcpyHostToDevice, S.cst));
     if ((s = ensure_dev(ctx, ctx->d_fb[0], rsg::block_sums_scratch_bytes(plan.total_blocks))) != RSG_OK) return s;
     if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, S.d_src, S.seed, ctx->d_out[0].p, ctx->d_fb[0].p,
-                         S.st)) != RSG_OK)
+                         S.cst)) != RSG_OK)
         return s;
     // Each window resolves on the GPU to the first block in targets order with
     // equal Sum1, length and sum2[:s2len] (match.go:108-136); only the block
@@ -156,12 +157,12 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
     RSG_HIP(ctx, rsg::launch_resolve((const uint8_t *)ctx->d_out[0].p, (const DevFile *)ctx->d_files.p,
                                      plan.total_blocks, S.d_groups, S.d_hi16, S.d_sum2,
                                      S.head.count, S.head.block_len, S.head.rem, S.head.s2len,
-                                     (int32_t *)ctx->d_res.p, S.st));
+                                     (int32_t *)ctx->d_res.p, S.cst));
     if ((s = ensure_pin(ctx, ctx->h_out[0], plan.total_blocks * 4)) != RSG_OK) return s;
     const int32_t *found = (const int32_t *)ctx->h_out[0].p;
-    RSG_HIP(ctx, hipMemcpyAsync(ctx->h_out[0].p, ctx->d_res.p, plan.total_blocks * 4, hipMemcpyDeviceToHost, S.st));
+    RSG_HIP(ctx, hipMemcpyAsync(ctx->h_out[0].p, ctx->d_res.p, plan.total_blocks * 4, hipMemcpyDeviceToHost, S.cst));
     if (!S.sl->confirmed) RSG_HIP(ctx, hipEventCreateWithFlags(&S.sl->confirmed, hipEventDisableTiming));
-    RSG_HIP(ctx, hipEventRecord(S.sl->confirmed, S.st));
+    RSG_HIP(ctx, hipEventRecord(S.sl->confirmed, S.cst));
     if (S.hook) {  // the next job's work queues behind this batch, and the host builds its tables meanwhile
         const std::function<rsg_status()> h = std::move(S.hook);
         S.hook = nullptr;
@@ -496,6 +497,7 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
         S->ctx = ctx;
         S->sl = &ctx->search[slot];
         S->st = ctx->side[0];
+        S->cst = ctx->side[0];
         S->side = ctx->side[1];
         S->copy = ctx->stream;
         S->size = j.src_len;
