@@ -270,12 +270,18 @@ __device__ __forceinline__ void hash_block_deep(const uint8_t *arena, uintptr_t 
     }
 }
 
-template <bool ALIGNED>
-__global__ __launch_bounds__(64) void block_sums_long(
+// Workgroups of W waves.  With few windows (the sender's ~23 K confirmation
+// windows) W = 2 puts the two waves of a CU on separate SIMDs: one-wave
+// workgroups took 0.31 or 0.55-0.60 ms depending on whether two landed on one
+// SIMD, four-wave workgroups 0.46 ms (four waves share the CU's memory
+// pipeline).  With more waves than 2 per CU, W = 1 spreads them better.
+template <bool ALIGNED, int W>
+__global__ __launch_bounds__(64 * W) void block_sums_long(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed,
     uint8_t *__restrict__ out) {
-    const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    constexpr uint32_t kLongThreads = 64 * W;
+    const uint64_t g = (uint64_t)blockIdx.x * kLongThreads + threadIdx.x;
     if (g >= total_blocks) return;
     // wg_file is indexed per 256-lane workgroup of the plan
     uint32_t lo = wg_file[g / kBlockSumThreads], hi = wg_file[g / kBlockSumThreads + 1];
@@ -902,13 +908,22 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                                wg_file, nwg, total_blocks, seed, out);
             break;
         case 3: {
-            const dim3 g64((uint32_t)((total_blocks + 63) / 64)), b64(64);
-            if (aligned)
-                hipLaunchKernelGGL(block_sums_long<true>, g64, b64, 0, stream, arena, arena_bytes, files, wg_file,
+            const uint64_t waves = (total_blocks + 63) / 64;
+            const bool two = waves <= 2ull * park_grid(~0ull >> 8);  // at most two waves per CU
+            const uint32_t lt = two ? 128u : 64u;
+            const dim3 lg((uint32_t)((total_blocks + lt - 1) / lt)), lb(lt);
+            if (aligned && two)
+                hipLaunchKernelGGL((block_sums_long<true, 2>), lg, lb, 0, stream, arena, arena_bytes, files, wg_file,
                                    total_blocks, seed, out);
+            else if (aligned)
+                hipLaunchKernelGGL((block_sums_long<true, 1>), lg, lb, 0, stream, arena, arena_bytes, files, wg_file,
+                                   total_blocks, seed, out);
+            else if (two)
+                hipLaunchKernelGGL((block_sums_long<false, 2>), lg, lb, 0, stream, arena, arena_bytes, files,
+                                   wg_file, total_blocks, seed, out);
             else
-                hipLaunchKernelGGL(block_sums_long<false>, g64, b64, 0, stream, arena, arena_bytes, files, wg_file,
-                                   total_blocks, seed, out);
+                hipLaunchKernelGGL((block_sums_long<false, 1>), lg, lb, 0, stream, arena, arena_bytes, files,
+                                   wg_file, total_blocks, seed, out);
             break;
         }
         default:

@@ -79,7 +79,10 @@ hipError_t launch_resolve(const uint8_t *records, const DevFile *files, uint64_t
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
                        const uint32_t *bitmap, const uint64_t *table, uint32_t bmask, uint64_t *cand,
-                       uint32_t cap, uint32_t *count, uint32_t grid, hipStream_t stream);
+                       uint32_t cap, uint32_t *count, uint32_t grid, bool fused, hipStream_t stream);
+// Block lengths up to which roll derives its window sums itself (no tile_agg
+// / tile_scan passes): each workgroup reads B extra bytes once.
+constexpr uint32_t kFusedMaxB = 4 * kScanTile;
 
 // ---- whole-file sums (rsg_filesums.hip)
 struct FileSpan {

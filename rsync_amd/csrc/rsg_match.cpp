@@ -81,6 +81,7 @@ struct Search {
     const uint8_t *d_sum2 = nullptr;
     const uint64_t *d_table = nullptr;
     uint32_t ntiles = 0, tile_end = 0, bmask = 0, cus = 256;
+    bool fused = false;  // roll derives its window sums itself (B <= kFusedMaxB)
     bool pending = false;  // prepare() launched the roll of [0, tile_end) and its count read-back
 
     int64_t len_of(int32_t i) const {
@@ -343,10 +344,13 @@ rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
         src = (const uint8_t *)sl.src.p;
     }
     S.d_src = src;
-    const uint32_t r = (uint32_t)(S.head.block_len % kScanTile);
-    RSG_HIP(ctx, rsg::launch_tile_agg(S.d_src, S.size, r, (TileAgg *)sl.agg.p, S.ntiles, S.side));
-    RSG_HIP(ctx, rsg::launch_tile_scan((const TileAgg *)sl.agg.p, S.ntiles, (TilePrefix *)sl.prefix.p, S.side));
-    RSG_HIP(ctx, hipEventRecord(sl.scanned, S.side));
+    S.fused = (uint32_t)S.head.block_len <= rsg::kFusedMaxB;
+    if (!S.fused) {  // long blocks: global prefix sums of the source first
+        const uint32_t r = (uint32_t)(S.head.block_len % kScanTile);
+        RSG_HIP(ctx, rsg::launch_tile_agg(S.d_src, S.size, r, (TileAgg *)sl.agg.p, S.ntiles, S.side));
+        RSG_HIP(ctx, rsg::launch_tile_scan((const TileAgg *)sl.agg.p, S.ntiles, (TilePrefix *)sl.prefix.p, S.side));
+    }
+    RSG_HIP(ctx, hipEventRecord(sl.scanned, S.side));  // also orders the realigning copy
 
     RSG_HIP(ctx, hipMemcpyAsync(sl.blob.p, sl.stage.p, S.blob_bytes, hipMemcpyHostToDevice, S.st));
     const uint8_t *blob = (const uint8_t *)sl.blob.p;
@@ -376,7 +380,7 @@ rsg_status launch_range(Search &S, uint32_t lo, uint32_t hi) {
     RSG_HIP(ctx, rsg::launch_roll(S.d_src, S.size, (uint32_t)S.head.block_len, (uint32_t)S.head.rem, (uint64_t)S.end,
                                   lo, hi, (const TileAgg *)sl.agg.p, (const TilePrefix *)sl.prefix.p, S.ntiles,
                                   S.d_filter, S.d_table, S.bmask, (uint64_t *)sl.list.p, kCandCap,
-                                  (uint32_t *)sl.counts.p, S.cus, S.st));
+                                  (uint32_t *)sl.counts.p, S.cus, S.fused, S.st));
     RSG_HIP(ctx, hipMemcpyAsync(sl.count.p, sl.counts.p, 4, hipMemcpyDeviceToHost, S.st));
     RSG_HIP(ctx, hipEventRecord(sl.rolled, S.st));
     return RSG_OK;

@@ -227,17 +227,18 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
     uint32_t tile_hi, const TileAgg *__restrict__ agg, const TilePrefix *__restrict__ pre, uint32_t ntiles,
     const uint32_t *__restrict__ bitmap_g, const uint64_t *__restrict__ table, uint32_t bmask,
-    uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count) {
+    uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count, uint32_t fused) {
     constexpr uint32_t kWaves = kRollThreads / 64;
     __shared__ uint32_t bitmap[kFilterBits / 32];       // 128 KiB
     __shared__ uint2 queue[kWaves][2][kQueueCap];        // (tile-local offset, sum), per tile parity
     __shared__ uint4 wsum[2][kWaves];                     // scan partials, double-buffered per tile
+    __shared__ uint2 carry[2];                            // fused prefix: next tile's (D1, DM), per tile parity
     for (uint32_t i = threadIdx.x; i < kFilterBits / 32; i += kRollThreads) bitmap[i] = bitmap_g[i];
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t Bt = B / kScanTile;
-    const TilePrefix tot = pre[ntiles];
+    const TilePrefix tot = fused ? TilePrefix{0, 0} : pre[ntiles];
     const uint32_t rem_flag = (rem != 0 && rem != B) ? 4u : 2u;
     uint32_t parity = 0;
 
@@ -271,6 +272,46 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     const uint32_t t_end = min(tile_hi, t_begin + per);
     const uint32_t lo = threadIdx.x * kRollPerThread;  // local offset of this lane's first offset
     const uint32_t sh = B & 3u;  // (q0 + lo + B) & 3: q0, lo are multiples of 32
+    // Fused prefix (B <= kFusedMaxB, no tile_agg / tile_scan passes): the
+    // window at tile start q0 needs only D1 = sum x and DM = sum i*x (absolute
+    // i, mod 2^32) over [q0, q0 + B), bytes past the source's end reading 0.
+    // The run's first tile reduces them directly; each further tile follows
+    //   D1(q0 + T) = D1(q0) + sum(shifted bytes) - sum(own bytes)
+    // (and the same for DM) from totals the tile's scan produces anyway.
+    uint32_t D1 = 0, DM = 0;
+    if (fused && t_begin < t_end) {
+        const uint64_t qb = (uint64_t)t_begin * kScanTile;
+        uint32_t a1 = 0, a2 = 0;
+        for (uint32_t off = threadIdx.x * 16u; off < B; off += kRollThreads * 16u) {
+            uint32_t w[4];
+            load_vec(src, size, qb + off, w);
+            if (off + 16u > B) {  // keep bytes < B only
+                const uint32_t keep = B - off;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++) {
+                    const uint32_t nb = keep > 4 * q ? min(keep - 4 * q, 4u) : 0u;
+                    w[q] &= nb >= 4 ? 0xffffffffu : ((1u << (8 * nb)) - 1u);
+                }
+            }
+            int32_t v1, v2;
+            vec_sums(w, v1, v2);
+            a1 += (uint32_t)v1;
+            a2 += (uint32_t)v2 + (uint32_t)(qb + off) * (uint32_t)v1;
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            a1 += __shfl_xor(a1, m, 64);
+            a2 += __shfl_xor(a2, m, 64);
+        }
+        if (lane == 0) wsum[0][wave] = make_uint4(a1, a2, 0, 0);
+        __syncthreads();
+#pragma unroll
+        for (uint32_t w = 0; w < kWaves; w++) {
+            D1 += __builtin_amdgcn_readfirstlane(wsum[0][w].x);
+            DM += __builtin_amdgcn_readfirstlane(wsum[0][w].y);
+        }
+        __syncthreads();
+    }
     // own bytes [qt, qt+32) and the 4-byte aligned shifted bytes around
     // [qt+B, qt+B+32) of tile t; the next tile's are loaded while this one
     // is scanned (one workgroup per CU: nothing else would hide the latency)
@@ -355,16 +396,27 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
             const uint4 p = wsum[parity][w];
             if (w < wave) { add.x += p.x; add.y += p.y; add.z += p.z; add.w += p.w; }
         }
+        if (fused && t != t_begin) {  // the previous tile's last lane left this tile's start window
+            const uint2 c = carry[parity];
+            D1 = __builtin_amdgcn_readfirstlane(c.x);
+            DM = __builtin_amdgcn_readfirstlane(c.y);
+        }
         const uint32_t ex[4] = {incl[0] - v[0] + add.x, incl[1] - v[1] + add.y, incl[2] - v[2] + add.z,
                                 incl[3] - v[3] + add.w};
         parity ^= 1u;
         // Lanes past `end` stay in the loop (they never hit): the probes spread the
         // wave's parked hits over all 64 lanes.
-        // P, Q at qt
-        const uint32_t Pq = pre[t].p + ex[0];
-        const uint32_t Qq = pre[t].q + ex[1] + (uint32_t)q0 * ex[0];
         uint32_t W1, W2, k;
-        if (qt + B <= size) {
+        if (fused) {
+            // window [qt, qt + B) = [q0, q0 + B) - [q0, qt) + [q0 + B, qt + B)
+            W1 = D1 - ex[0] + ex[2];
+            const uint32_t M = DM + (ex[3] + (uint32_t)(q0 + B) * ex[2]) - (ex[1] + (uint32_t)q0 * ex[0]);
+            k = qt + B <= size ? B : (qt < size ? (uint32_t)(size - qt) : 0u);
+            W2 = (uint32_t)(qt + k) * W1 - M;
+        } else if (qt + B <= size) {
+            // P, Q at qt
+            const uint32_t Pq = pre[t].p + ex[0];
+            const uint32_t Qq = pre[t].q + ex[1] + (uint32_t)q0 * ex[0];
             const uint32_t u = min(t + Bt, ntiles);  // tile holding q0 + B
             const uint32_t ur1 = u < ntiles ? agg[u].r1 : 0u, ur2 = u < ntiles ? agg[u].r2 : 0u;
             const uint32_t Pb = pre[u].p + ur1;                                              // P[q0 + B]
@@ -375,6 +427,8 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
             W2 = (uint32_t)(qt + B) * W1 - (Qe - Qq);
             k = B;
         } else {
+            const uint32_t Pq = pre[t].p + ex[0];
+            const uint32_t Qq = pre[t].q + ex[1] + (uint32_t)q0 * ex[0];
             W1 = tot.p - Pq;
             W2 = (uint32_t)size * W1 - (tot.q - Qq);
             k = qt < size ? (uint32_t)(size - qt) : 0u;
@@ -466,6 +520,11 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
+        // Fused prefix: after its 32 updates the tile's last lane holds the
+        // window at q0 + T (length k): the next tile's D1 = W1 and
+        // DM = (q0 + T + k) W1 - W2 (only their low 16 bits matter).
+        if (fused && threadIdx.x == kRollThreads - 1)
+            carry[parity] = make_uint2(W1, (uint32_t)(q0 + kScanTile + k) * W1 - W2);
         if (pv) {
             uint32_t fl = 0;
 #pragma unroll
@@ -540,11 +599,11 @@ hipError_t launch_tile_scan(const TileAgg *agg, uint32_t ntiles, TilePrefix *pre
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
                        const uint32_t *bitmap, const uint64_t *table, uint32_t bmask, uint64_t *cand,
-                       uint32_t cap, uint32_t *count, uint32_t grid, hipStream_t stream) {
+                       uint32_t cap, uint32_t *count, uint32_t grid, bool fused, hipStream_t stream) {
     if (tile_hi <= tile_lo) return hipSuccess;
     const uint32_t g = min(grid, tile_hi - tile_lo);
     hipLaunchKernelGGL(roll_kernel, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, tile_hi,
-                       agg, pre, ntiles, bitmap, table, bmask, cand, cap, count);
+                       agg, pre, ntiles, bitmap, table, bmask, cand, cap, count, fused ? 1u : 0u);
     return hipGetLastError();
 }
 

@@ -208,3 +208,19 @@ def test_batch_device_matches_single(eng):
     got = eng.hash_search_batch(jobs, seed)
     assert got == want
     assert got == [eng.hash_search_device(*j, seed) for j in jobs]
+
+
+@pytest.mark.parametrize("blen", [131073, 200000])
+def test_long_blocks_prefix_pass(eng, blen):
+    """B > 128 KiB: the roll kernel takes its window sums from the tile_agg /
+    tile_scan prefix passes instead of deriving them itself (rsg_match.cpp
+    enqueue_scan); both paths must give the oracle's matches."""
+    rng = np.random.default_rng(blen)
+    basis = cases.splitmix64_bytes(blen, 3 << 20)
+    src = cases.mutate(basis, blen + 1, 0.3, 1, 2 * blen, n_ins=3, n_del=3)
+    seed = int(rng.integers(-2**31, 2**31))
+    head, s1, s2 = basis_sums(basis, blen, seed)
+    tg = orc.stable_targets(s1)
+    want, _, _ = orc.hash_search(src, head, s1, s2, tg, seed)
+    assert len(want) > 0
+    assert eng.hash_search(src, head, s1, s2, tg, seed) == want
