@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--ab", action="store_true", help="A/B the block-sum kernel variants (interleaved rounds)")
-    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4"],
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5"],
                     help="cfg2 = receiver block sums (the metric); cfg3 = sender match, reported separately")
     ap.add_argument("--cfg3-files", type=int, default=10)
     return ap.parse_args()
@@ -72,6 +72,8 @@ def main():
         return bench_sender(args, rank, world, local)
     if args.workload == "cfg4":
         return bench_mixed(args, rank, world, local)
+    if args.workload == "cfg5":
+        return bench_long(args, rank, world, local)
 
     eng = rsync_amd.Engine(local)
     stream = torch.cuda.Stream(device=local)
@@ -205,6 +207,37 @@ def main():
         extra["host_path"]["pinned_sources_parity"] = pin_rec == host_rec
         del views
         eng.free_pinned(pin)
+        # the generator's whole host loop (rsg_generate_files_fd): the files
+        # on a filesystem (page cache), read by the engine, sums stream (idx,
+        # SumHead, records, phase markers) handed to a writer that counts it
+        import tempfile
+        tmp = tempfile.mkdtemp(dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+        fds = []
+        try:
+            for f, d in enumerate(files):
+                p = os.path.join(tmp, f"f{f}")
+                with open(p, "wb") as fh:
+                    fh.write(d.tobytes())
+                fds.append(os.open(p, os.O_RDONLY))
+            sink = [0]
+
+            def count(b):
+                sink[0] += len(b)
+            gen = [(fd, FILE_BYTES) for fd in fds]
+            eng.generate_files_fd(gen[:8], SEED, count, block_len=BLOCK_LEN, idx=list(range(8)))
+            h0 = time.perf_counter()
+            for _ in range(reps):
+                _, nw = eng.generate_files_fd(gen, SEED, count, block_len=BLOCK_LEN, idx=list(range(256)), mux=True)
+            gdt = (time.perf_counter() - h0) / reps
+            extra["host_path"]["generate_files_fd_gib_s"] = round(256 * FILE_BYTES / gdt / GIB, 3)
+            extra["host_path"]["generate_files_fd_sample"] = (
+                f"256 x 1 MiB files in {tmp.split('/')[1]} (page cache), pread by the engine, mux-framed sums "
+                f"stream of {nw} bytes to a counting writer")
+        finally:
+            for fd in fds:
+                os.close(fd)
+            import shutil
+            shutil.rmtree(tmp, ignore_errors=True)
 
     # ---- CPU baseline: the scalar C restatement (oracle) on 1 host core
     cpu = None
@@ -502,6 +535,88 @@ def bench_mixed(args, rank, world, local):
                          "frac": round(algo / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "traffic": cfg4_traffic(world, plan.total_records),
                          "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": int(algo)},
+            "cpu_baseline": cpu}), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_long(args, rank, world, local):
+    """cfg5: 8 x 32 GiB files at B = 128 KiB, one file per GPU (weak scaling:
+    rank r hashes its own 32 GiB file, generated on the device).  One step =
+    one launch over the whole file (262 144 blocks of 2049 MD4 compressions).
+    Parity by sampled blocks (1024 random + the last) against the oracle, which
+    also times the CPU baseline on them.  Reported beside cfg2."""
+    import torch
+    import torch.distributed as dist
+    import rsync_amd
+    size, B = 32 << 30, 131072
+    eng = rsync_amd.Engine(local)
+    stream = torch.cuda.Stream(device=local)
+    sptr = stream.cuda_stream
+    arena = eng.alloc(size)
+    eng.fill_splitmix64(arena, size, 5000 + rank, stream=sptr)
+    plan = eng.plan([(0, size, B)], size)
+    nrec = plan.total_records
+    recs = eng.alloc(nrec * rsync_amd.RECORD_BYTES)
+    eng.synchronize(sptr)
+    steps = max(1, args.steps)
+    for _ in range(max(3, min(args.warmup, 40))):
+        plan.run(arena, SEED, recs, stream=sptr)
+    eng.synchronize(sptr)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        plan.run(arena, SEED, recs, stream=sptr)
+    ev1.record(stream)
+    eng.synchronize(sptr)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / steps
+    if world > 1:
+        tt = torch.tensor([wall, kernel_ms], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall, kernel_ms = float(tt[0]), float(tt[1])
+    cpu, parity = None, None
+    if rank == 0:
+        from oracle import oracle as orc
+        lib = orc.lib()
+        rng = np.random.default_rng(55)
+        sample = sorted(set(rng.integers(0, nrec, 1024).tolist()) | {nrec - 1})
+        got_all = recs.download(nrec * 20).reshape(-1, 20)
+        out = np.empty(20, np.uint8)
+        t_cpu, parity = 0.0, True
+        for b in sample:
+            blk = arena.download(B, offset=b * B)
+            c0 = time.perf_counter()
+            lib.orc_block_sums(orc._ptr(blk), blk.size, B, orc._i32(SEED), orc._ptr(out))
+            t_cpu += time.perf_counter() - c0
+            parity &= bool((got_all[b] == out).all())
+        if not args.no_cpu:
+            cpu = {"value": round(len(sample) * B / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+                   "sample": f"{len(sample)} sampled 128 KiB blocks of rank 0's file (1024 random + the last), "
+                             f"oracle/rsg_oracle.c orc_block_sums, 1 thread, {t_cpu:.1f} s"}
+        algo = size + nrec * rsync_amd.RECORD_BYTES
+        print(json.dumps({
+            "metric": "GiB/s block-checksummed (weak+MD4), device-resident, at 1/2/4/8 MI355X",
+            "value": round(world * size * steps / wall / GIB, 2), "unit": "GiB/s", "n_gpus": world,
+            "steps": steps, "warmup": args.warmup, "ms_per_step": round(wall * 1e3 / steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (splitmix64 bytes generated on device)",
+            "config": {"workload": "cfg5: one 32 GiB file per GPU (8 x 32 GiB at 8 GPUs), B=131072, weak+MD4",
+                       "file_bytes": size, "block_len": B, "records_per_gpu": nrec,
+                       "parallelism": f"one file per GPU, {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": round(algo / (kernel_ms * 1e-3) / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(algo / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": int(algo)},
+            "sampled_block_parity": {"blocks": len(sample), "equal": parity},
             "cpu_baseline": cpu}), flush=True)
     eng.close()
     if world > 1:

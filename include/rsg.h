@@ -51,6 +51,7 @@ typedef int32_t rsg_status;
 #define RSG_ERR_NODEV (-4)     /* no gfx950 device at that ordinal           */
 #define RSG_ERR_TRUNCATED (-5) /* output capacity too small; size reported   */
 #define RSG_ERR_CORRUPT (-6)   /* whole-file sum mismatch (receiver.go:171)  */
+#define RSG_ERR_IO (-7)        /* file read failed / short, or writer failed */
 
 typedef struct rsg_ctx rsg_ctx;
 typedef struct rsg_plan rsg_plan;
@@ -142,14 +143,16 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
 
 /* Tuning knob (process-wide): block-sum kernel variant.  Every variant
  * gives identical records; only speed differs.  -1 = automatic (default),
- * 0 = direct per-lane loads, 1 = staged LDS-DMA slabs, 2 = park (three loader
- * waves stream 64-block tiles through LDS, five hasher waves park the blocks
- * in registers; blocks <= 703 bytes, otherwise 1 is used), 3 = deep per-lane
- * prefetch for long blocks.  Automatic: aligned batches take 2 when 512 <= the largest block
- * <= 703 bytes, else 1; unaligned batches (a block not 4-byte aligned) take 3
- * for blocks >= 8 KiB, else 0 (1 and 2 fall back to 0 there).  The
- * environment variable RSG_BLOCKSUMS_KERNEL sets the initial value.  Returns
- * RSG_ERR_INVALID outside -1..3. */
+ * 0 = direct per-lane loads, 1 = staged LDS-DMA slabs (256 bytes of every
+ * block per segment), 2 = park (three loader waves stream 64-block tiles
+ * through LDS, five hasher waves park the blocks in registers; blocks <= 703
+ * bytes, otherwise 1 is used), 3 = deep per-lane prefetch for long blocks,
+ * 4 / 5 = staged with 128- / 512-byte segments.  Automatic: aligned batches
+ * take 2 when 512 <= the largest block <= 703 bytes, else 1; unaligned
+ * batches (a block not 4-byte aligned) take 3 for blocks >= 8 KiB, else 0
+ * (1, 2, 4 and 5 fall back to 0 there).  The environment variable
+ * RSG_BLOCKSUMS_KERNEL sets the initial value.  Returns RSG_ERR_INVALID
+ * outside -1..5. */
 rsg_status rsg_set_block_sums_kernel(int32_t variant);
 
 /* Timing diagnostics for DESIGN.md's roofline analysis, NOT for use: while
@@ -171,6 +174,39 @@ rsg_status rsg_block_sums_device(rsg_ctx *ctx, const void *d_arena, uint64_t are
  * memory, overlapping H2D, kernel and D2H.  Synchronous. */
 rsg_status rsg_block_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, int32_t seed,
                                uint8_t *records, uint64_t records_cap);
+
+/* ---------------------------------- receiver: the generator's host loop (§8f row 1)
+ * Replaces GenerateFiles' per-file work for files that reach
+ * generateAndSendSums (generator.go:143-322,325-350): for each file in list
+ * order, int32 idx (generator.go:317, with RSG_GEN_IDX), the SumHead
+ * (types.go:79-86) and count x (int32 LE sum1, sum2[16]); RSG_GEN_TERMINATE
+ * appends the two int32 -1 phase markers (generator.go:31,40).  File bytes
+ * are read with pread from `fd` at [offset, offset+len) (io.ReadFull of every
+ * block, generator.go:335): a file shorter than len is RSG_ERR_IO "unexpected
+ * EOF".  Reading (a few threads, 2 MiB pieces), H2D + kernel + D2H and the
+ * writes of consecutive <= 64 MiB batches overlap.  The stream goes to
+ * write(user, data, len) once per batch (0 = ok; anything else stops the
+ * call with RSG_ERR_IO), framed as <= 256 KiB MsgData messages with
+ * RSG_GEN_MUX (the server side's MultiplexWriter, wire.go:28-36; the demuxed
+ * bytes equal the reference's, message boundaries differ).  heads_out (may be
+ * NULL) receives nfiles heads; *bytes_written counts the bytes handed to
+ * write.  On failure, the bytes already written are a prefix of the stream.
+ * Synchronous; write is called on the calling thread. */
+typedef struct rsg_fd_file {
+    int32_t fd;          /* open for reading (Go: int(f.Fd()))          */
+    int32_t idx;         /* file-list index written before the SumHead  */
+    int64_t offset;      /* first byte of the file in fd (normally 0)   */
+    uint64_t len;        /* fileLen of generateAndSendSums              */
+    int32_t block_len;   /* 0 = SumSizesSqroot, else explicit B          */
+    int32_t reserved;
+} rsg_fd_file;
+typedef int32_t (*rsg_write_fn)(void *user, const uint8_t *data, uint64_t len);
+#define RSG_GEN_IDX 1
+#define RSG_GEN_TERMINATE 2
+#define RSG_GEN_MUX 4
+rsg_status rsg_generate_files_fd(rsg_ctx *ctx, const rsg_fd_file *files, uint64_t nfiles, int32_t seed,
+                                 int32_t flags, rsg_write_fn write, void *user, rsg_sum_head *heads_out,
+                                 uint64_t *bytes_written);
 
 /* ---------------------------------------------- sender: hash search (★ a11)
  * Replaces the per-byte search of (*sender.Transfer).hashSearch

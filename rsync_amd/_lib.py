@@ -31,6 +31,10 @@ ERR_HIP = -3
 ERR_NODEV = -4
 ERR_TRUNCATED = -5
 ERR_CORRUPT = -6
+ERR_IO = -7
+GEN_IDX = 1        # rsg_generate_files_fd flags
+GEN_TERMINATE = 2
+GEN_MUX = 4
 
 
 class SumHead(ctypes.Structure):
@@ -61,6 +65,15 @@ class SearchJob(ctypes.Structure):
                 ("matches", ctypes.POINTER(Match)), ("match_cap", ctypes.c_uint64),
                 ("n_matches", ctypes.c_uint64), ("status", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
+
+class FdFile(ctypes.Structure):
+    """rsg_fd_file: one basis file of rsg_generate_files_fd."""
+    _fields_ = [("fd", ctypes.c_int32), ("idx", ctypes.c_int32), ("offset", ctypes.c_int64),
+                ("len", ctypes.c_uint64), ("block_len", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+# rsg_write_fn: int32 (*)(void *user, const uint8_t *data, uint64_t len)
+WRITE_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
 
 _vp = ctypes.c_void_p
 _u64 = ctypes.c_uint64
@@ -93,6 +106,8 @@ _PROTOS = {
     "rsg_set_block_sums_diagnostic": (_st, [_i32]),
     "rsg_block_sums_device": (_st, [_vp, _vp, _u64, ctypes.POINTER(File), _u64, _i32, _vp, _u64]),
     "rsg_block_sums_host": (_st, [_vp, ctypes.POINTER(File), _u64, _i32, _vp, _u64]),
+    "rsg_generate_files_fd": (_st, [_vp, ctypes.POINTER(FdFile), _u64, _i32, _i32, WRITE_FN, _vp,
+                                    ctypes.POINTER(SumHead), ctypes.POINTER(_u64)]),
     "rsg_hash_search_host": (_st, [_vp, _vp, _u64, ctypes.POINTER(SumHead), _vp, _vp, _vp, _i32,
                                    ctypes.POINTER(Match), _u64, ctypes.POINTER(_u64)]),
     "rsg_hash_search_device": (_st, [_vp, _vp, _u64, ctypes.POINTER(SumHead), _vp, _vp, _vp, _i32,

@@ -417,7 +417,7 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
 }
 
 rsg_status rsg_set_block_sums_kernel(int32_t variant) {
-    if (variant < -1 || variant > 3) return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..3");
+    if (variant < -1 || variant > 5) return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..5");
     rsg::set_block_sums_variant(variant);
     return RSG_OK;
 }

@@ -312,11 +312,18 @@ __global__ __launch_bounds__(64 * W) void block_sums_long(
 // every 16-lane group).  While the wave hashes segment s out of registers,
 // segment s+1 is already in flight.  The default for aligned batches whose
 // blocks are longer than the park kernel's 703 bytes.
-constexpr uint32_t kSegBytes = 256;
-constexpr uint32_t kPiece = kSegBytes + 16;          // padded piece stride in LDS
-constexpr uint32_t kWaveSlab = 64 * kPiece;          // 17408 bytes per wave
-constexpr uint32_t kDmaPerSeg = kWaveSlab / 1024;    // 17 DMA instructions per segment
-static_assert(kWaveSlab % 1024 == 0, "slab must be a whole number of DMA instructions");
+// SEG = bytes of every block per segment (256 by default; 128 and 512 are
+// variants 4 and 5 for long blocks: more waves per CU vs longer pieces).
+template <uint32_t SEG>
+struct Seg {
+    static constexpr uint32_t kSegBytes = SEG;
+    static constexpr uint32_t kUnits = SEG / 16 + 1;           // 16-byte units per padded piece
+    static constexpr uint32_t kPiece = SEG + 16;               // padded piece stride in LDS
+    static constexpr uint32_t kWaveSlab = 64 * kPiece;         // 17408 bytes per wave at SEG = 256
+    static constexpr uint32_t kDmaPerSeg = kWaveSlab / 1024;   // 17 DMA instructions per segment
+    static constexpr uint32_t kChunks = SEG / 64;              // MD4 chunks per segment
+    static_assert(kWaveSlab % 1024 == 0, "slab must be a whole number of DMA instructions");
+};
 
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 #pragma unroll
@@ -335,13 +342,19 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     }
     return v;
 }
-// MODE 0 = the product kernel.  Timing diagnostics (outputs meaningless):
-// MODE 1 = DMA + LDS reads only (the memory cost of this access pattern),
-// MODE 2 = hashing only, no DMA (the compute cost).
-template <int MODE>
+// KIND % 10: 0 = the product kernel; timing diagnostics (outputs
+// meaningless): 1 = DMA + LDS reads only (the memory cost of this access
+// pattern), 2 = hashing only, no DMA (the compute cost).  KIND / 10 picks the
+// segment: 0 = 256 bytes, 1 = 128, 2 = 512.
+template <int KIND>
 __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
+    constexpr int MODE = KIND % 10;
+    constexpr uint32_t SEG = KIND >= 20 ? 512u : (KIND >= 10 ? 128u : 256u);
+    constexpr uint32_t kSegBytes = Seg<SEG>::kSegBytes, kUnits = Seg<SEG>::kUnits, kPiece = Seg<SEG>::kPiece;
+    constexpr uint32_t kWaveSlab = Seg<SEG>::kWaveSlab, kDmaPerSeg = Seg<SEG>::kDmaPerSeg;
+    constexpr uint32_t kChunks = Seg<SEG>::kChunks;
     __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * kWaveSlab];
     const uint32_t lane = threadIdx.x & 63u;
     // readfirstlane: provably wave-uniform values keep the LDS base (M0) and
@@ -353,7 +366,7 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     uint64_t off = 0;
     uint32_t n = 0;
     if (g < total_blocks) locate_block(files, wg_file, g, off, n);
-    const uint32_t nseg = n ? ((n >> 6) >> 2) + 1 : 0;  // segments through the tail chunk
+    const uint32_t nseg = n ? (n >> 6) / kChunks + 1 : 0;  // segments through the tail chunk
     const uint32_t S = __builtin_amdgcn_readfirstlane((uint32_t)wave_max_u64(nseg));
     const uint64_t lo_v = wave_min_u64(n ? off : ~0ull);
     const uint64_t base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo_v >> 32)) << 32) |
@@ -378,18 +391,20 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
         __builtin_amdgcn_make_buffer_rsrc((void *)(arena + base), (short)0, 0x7FFFFFFF, 0x00020000);
     const uint32_t rel = (uint32_t)(off - base);
     // DMA instruction i, lane t fills slab bytes [16*(64 i + t), +16): piece
-    // j = (64 i + t) / 17 (lane j's block), unit u = (64 i + t) % 17.  u == 16
-    // is the pad: its offset is past num_records, so the buffer range check
-    // drops it without a memory request.
-    uint32_t voff[kDmaPerSeg];
+    // j = (64 i + t) / kUnits (lane j's block), unit u = (64 i + t) % kUnits.
+    // u == kUnits - 1 is the pad: its offset is past num_records, so the
+    // buffer range check drops it without a memory request.
+    // (fixed bound: an array sized by a template-dependent local makes hipcc's
+    // host pass drop this kernel's launch stubs; entries past kDmaPerSeg are dead)
+    uint32_t voff[Seg<512>::kDmaPerSeg];
 #pragma unroll
     for (uint32_t i = 0; i < kDmaPerSeg; i++) {
         const uint32_t idx = 64u * i + lane;
-        const uint32_t j = idx / 17u, u = idx - 17u * j;
+        const uint32_t j = idx / kUnits, u = idx - kUnits * j;
         const uint32_t v = (uint32_t)__shfl((int)rel, (int)j, 64) + 16u * u;
-        voff[i] = u < 16u ? v : 0x80000000u;
+        voff[i] = u + 1 < kUnits ? v : 0x80000000u;
     }
-    uint32_t R[64];
+    uint32_t R[Seg<512>::kSegBytes / 4];  // fixed bound, as voff
     const uint8_t *mine = slab + lane * kPiece;
 #define RSG_DMA_SEGMENT(S_)                                                                                      \
     do {                                                                                                         \
@@ -401,7 +416,7 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
 #define RSG_READ_SEGMENT()                                                                                       \
     do {                                                                                                         \
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                                         \
-        _Pragma("unroll") for (int q_ = 0; q_ < 16; q_++) {                                                      \
+        _Pragma("unroll") for (int q_ = 0; q_ < (int)(SEG / 16); q_++) {                                         \
             const uint4 v_ = *reinterpret_cast<const uint4 *>(mine + 16 * q_);                                  \
             R[4 * q_ + 0] = v_.x; R[4 * q_ + 1] = v_.y; R[4 * q_ + 2] = v_.z; R[4 * q_ + 3] = v_.w;              \
         }                                                                                                        \
@@ -420,11 +435,11 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
         if (MODE != 2 && more) RSG_DMA_SEGMENT(cs + 1);  // in flight while segment cs hashes
         if (MODE == 1) {
 #pragma unroll
-            for (int q = 0; q < 64; q++) h[q & 3] ^= R[q];
+            for (int q = 0; q < (int)(SEG / 4); q++) h[q & 3] ^= R[q];
         } else {
 #pragma unroll
-            for (uint32_t i = 0; i < 4; i++) {
-                const uint32_t c = 4u * cs + i;
+            for (uint32_t i = 0; i < kChunks; i++) {
+                const uint32_t c = kChunks * cs + i;
                 if (c < nfull) hash_chunk<true>(R + 16 * i, 0u, 0u, c, h, s1, t);
                 else if (c == nfull) hash_tail<true>(R + 16 * i, 0u, 0u, n, seed, h, s1, t);
             }
@@ -853,7 +868,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     if (g_variant == -2) {
         const char *e = getenv("RSG_BLOCKSUMS_KERNEL");
         g_variant = e ? atoi(e) : -1;
-        if (g_variant < -1 || g_variant > 3) g_variant = -1;
+        if (g_variant < -1 || g_variant > 5) g_variant = -1;
     }
     if (g_diag == -2) {
         const char *e = getenv("RSG_BLOCKSUMS_DIAG");
@@ -864,11 +879,11 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     if (g_diag > 0 && aligned) {
         switch (g_diag) {
             case 1:
-                hipLaunchKernelGGL(block_sums_staged<1>, grid, block, 0, stream, arena, arena_bytes, files, wg_file,
+                hipLaunchKernelGGL((block_sums_staged<1>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
                                    total_blocks, seed, out);
                 break;
             case 2:
-                hipLaunchKernelGGL(block_sums_staged<2>, grid, block, 0, stream, arena, arena_bytes, files, wg_file,
+                hipLaunchKernelGGL((block_sums_staged<2>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
                                    total_blocks, seed, out);
                 break;
             case 3:
@@ -896,16 +911,24 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     if (v == -1)
         v = aligned ? ((max_blen <= kRegMaxBytes && max_blen >= kParkMinBytes) ? 2 : 1)
                     : (max_blen >= kLongBlockBytes ? 3 : 0);
-    if (!aligned && (v == 1 || v == 2)) v = 0;  // the LDS-DMA kernels need 4-byte aligned blocks
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;  // the LDS-DMA kernels need 4-byte aligned blocks
     if (v == 2 && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
-            hipLaunchKernelGGL(block_sums_staged<0>, grid, block, 0, stream, arena, arena_bytes, files, wg_file,
+            hipLaunchKernelGGL((block_sums_staged<0>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
                                total_blocks, seed, out);
             break;
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders>), pgrid, pblock, 0, stream, arena, arena_bytes, files,
                                wg_file, nwg, total_blocks, seed, out);
+            break;
+        case 4:
+            hipLaunchKernelGGL((block_sums_staged<10>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
+                               total_blocks, seed, out);
+            break;
+        case 5:
+            hipLaunchKernelGGL((block_sums_staged<20>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
+                               total_blocks, seed, out);
             break;
         case 3: {
             const uint64_t waves = (total_blocks + 63) / 64;

@@ -272,6 +272,43 @@ class Engine:
         conn.write(mux_frame(stream) if mux else stream)
         return heads
 
+    def generate_files_fd(self, files: Sequence, seed: int, write, block_len=0, idx=None,
+                          terminate: bool = True, mux: bool = False) -> Tuple[List[SumHead], int]:
+        """GenerateFiles' host loop from open files (generator.go:143-350):
+        files = [(fd, len)] or [(fd, len, offset)]; file bytes are read by the
+        engine (pread, overlapped with the GPU), the sums stream goes to
+        write(bytes) once per batch.  idx = file-list indices written before
+        each SumHead (None: no idx words).  -> (heads, bytes written)."""
+        n = len(files)
+        bl = list(block_len) if isinstance(block_len, (list, tuple)) else [block_len] * n
+        desc = (_lib.FdFile * max(n, 1))()
+        for i, f in enumerate(files):
+            desc[i].fd = f[0]
+            desc[i].len = f[1]
+            desc[i].offset = f[2] if len(f) > 2 else 0
+            desc[i].block_len = bl[i]
+            desc[i].idx = idx[i] if idx is not None else 0
+        flags = (_lib.GEN_IDX if idx is not None else 0) | (_lib.GEN_TERMINATE if terminate else 0) | \
+                (_lib.GEN_MUX if mux else 0)
+        err = []
+
+        def _cb(_user, data, nbytes):
+            try:
+                write(ctypes.string_at(data, nbytes))
+                return 0
+            except Exception as e:  # surfaces as RSG_ERR_IO; re-raised below
+                err.append(e)
+                return -1
+
+        cb = _lib.WRITE_FN(_cb)
+        heads = (SumHead * max(n, 1))()
+        written = ctypes.c_uint64()
+        st = lib.rsg_generate_files_fd(self.ctx, desc, n, _i32(seed), flags, cb, None, heads, ctypes.byref(written))
+        if err:
+            raise err[0]
+        check(st, self.ctx)
+        return [heads[i] for i in range(n)], written.value
+
     # ------------------------------------------------------------ whole-file sums
     def file_sums(self, files: Sequence, mode: int = _lib.FILESUM_PLAIN, seed: int = 0) -> List[bytes]:
         """Whole-file MD4 of each host buffer, one GPU lane per file:

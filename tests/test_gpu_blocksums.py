@@ -176,10 +176,11 @@ def test_generate_and_send_sums_wire(eng):
     assert bytes(conn.buf) == want
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("blen", [700, 64, 1773, 4096, 131072])
 def test_kernel_variants_match(eng, variant, blen):
-    """Every kernel variant (direct / staged / park / long) gives the oracle's
+    """Every kernel variant (direct / staged / park / long / staged with 128-
+    and 512-byte segments) gives the oracle's
     records, including waves and park tiles that straddle files; unaligned
     arenas make the LDS-DMA variants fall back to direct."""
     from rsync_amd import _lib
@@ -200,7 +201,7 @@ def test_kernel_variants_match(eng, variant, blen):
     assert rec_dev == want
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_variants_device_aligned_arena(eng, variant):
     """Aligned device arena (the staged / park fast paths), files straddling
     waves and tiles, a file ending exactly at the arena end (park's direct
@@ -221,7 +222,7 @@ def test_variants_device_aligned_arena(eng, variant):
         datas.append(d)
     arena = eng.alloc(arena_bytes)
     arena.upload(host)
-    for blen in (700, 64, 703):
+    for blen in (700, 64, 703, 4096):
         want = b"".join(orc.block_sums(d, blen, cases.SEED) for d in datas)
         try:
             _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))

@@ -17,11 +17,13 @@ sys.path.insert(0, ROOT)
 
 SEED = 0x1BADB002
 SHAPES = [  # (files, file bytes, block length, arenas)
-    (1, 1 << 30, 131072, 2),      # one 1 GiB file, cfg5's block length
     (1, 32 << 30, 131072, 1),     # cfg5's per-GPU share: one 32 GiB file
-    (1024, 1 << 20, 700, 2),      # cfg2 (park applies to blocks <= 703 bytes only)
+    (1, 1 << 30, 131072, 2),      # one 1 GiB file, cfg5's block length
+    (1024, 1 << 20, 1024, 2),     # 1 MiB files at the reference's own sizing (B = 1024)
+    (256, 4 << 20, 4096, 2),      # 4 KiB blocks
 ]
-VARIANTS = {1: "staged", 2: "park", 3: "long_deep_prefetch"}
+VARIANTS = {1: "staged", 4: "staged_seg128", 5: "staged_seg512", 2: "park", 3: "long_deep_prefetch"}
+DIAGS = {1: "diag_staged_memory_only", 2: "diag_staged_hash_only", 6: "diag_linear_read_ldsdma"}
 
 
 def main():
@@ -41,8 +43,10 @@ def main():
         recs = eng.alloc(plan.total_records * rsync_amd.RECORD_BYTES)
         eng.synchronize(sp)
         res = {}
-        for v, name in VARIANTS.items():
+        runs = [(v, 0, name) for v, name in VARIANTS.items()] + [(1, d, name) for d, name in DIAGS.items()]
+        for v, d, name in runs:
             _lib.check(_lib.lib.rsg_set_block_sums_kernel(v))
+            _lib.check(_lib.lib.rsg_set_block_sums_diagnostic(d))
             steps = 5 if total > (4 << 30) else 30
             for i in range(10):
                 plan.run(arenas[i % narena], SEED, recs, stream=sp)
@@ -56,6 +60,7 @@ def main():
             res[name] = {"kernel_ms": round(ms, 4), "gib_s": round(total / 2**30 / (ms / 1e3), 1),
                          "hbm_frac_8tbs": round((total + plan.total_records * 20) / (ms / 1e3) / 8e12, 4)}
         _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+        _lib.check(_lib.lib.rsg_set_block_sums_diagnostic(0))
         print(json.dumps({"files": nf, "file_bytes": fb, "block_len": blen, "records": plan.total_records,
                           "variants": res}), flush=True)
         plan.close()
