@@ -160,7 +160,7 @@ rsg_status rsg_set_block_sums_kernel(int32_t variant);
  * product kernel and the "records" it writes are meaningless.  1 = staged
  * memory only, 2 = staged hashing only, 3 = park memory only, 4 = park
  * hashing only, 5 = linear read of the arena (plain loads), 6 = linear read
- * (LDS DMA).  0 = off (default;
+ * (LDS DMA); 5 and 6 run on arenas below 4 GiB only.  0 = off (default;
  * environment RSG_BLOCKSUMS_DIAG).  Kept apart from rsg_set_block_sums_kernel
  * so the product knob can never select a diagnostic. */
 rsg_status rsg_set_block_sums_diagnostic(int32_t diag);
@@ -184,7 +184,7 @@ rsg_status rsg_block_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfi
  * are read with pread from `fd` at [offset, offset+len) (io.ReadFull of every
  * block, generator.go:335): a file shorter than len is RSG_ERR_IO "unexpected
  * EOF".  Reading (a few threads, 2 MiB pieces), H2D + kernel + D2H and the
- * writes of consecutive <= 64 MiB batches overlap.  The stream goes to
+ * writes of consecutive batches (RSG_GEN_BATCH_MB, default 32 MiB) overlap.  The stream goes to
  * write(user, data, len) once per batch (0 = ok; anything else stops the
  * call with RSG_ERR_IO), framed as <= 256 KiB MsgData messages with
  * RSG_GEN_MUX (the server side's MultiplexWriter, wire.go:28-36; the demuxed

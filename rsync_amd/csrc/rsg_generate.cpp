@@ -32,8 +32,16 @@ using rsg::kRecordBytes;
 
 namespace {
 
-constexpr uint64_t kBatchBytes = 64ull << 20;  // staging per slot, as rsg_block_sums_host
 constexpr uint64_t kBatchRecords = 1ull << 22;
+
+// Staging per slot: RSG_GEN_BATCH_MB (default 32 MiB; smaller batches start
+// the GPU sooner and overlap more of the reads, larger ones cost fewer
+// launches).
+uint64_t batch_bytes() {
+    const char *e = getenv("RSG_GEN_BATCH_MB");
+    const long v = e ? atol(e) : 32;
+    return (uint64_t)std::max(1L, std::min(v, 1024L)) << 20;
+}
 constexpr uint64_t kReadPiece = 2ull << 20;
 constexpr uint32_t kMaxMessage = 256 * 1024;  // wire.go:46-47
 
@@ -71,13 +79,11 @@ int read_full(int fd, uint8_t *dst, uint64_t n, int64_t off) {
     return 0;
 }
 
+// Reader threads: RSG_COPY_THREADS (default 8), as the host path's copies.
 int read_threads() {
-    static const int t = [] {
-        const char *e = getenv("RSG_COPY_THREADS");
-        const int v = e ? atoi(e) : 8;
-        return std::max(1, std::min(v, 64));
-    }();
-    return t;
+    const char *e = getenv("RSG_COPY_THREADS");
+    const int v = e ? atoi(e) : 8;
+    return std::max(1, std::min(v, 64));
 }
 
 // All jobs on a few threads; returns the first failing job's index (or -1)
@@ -167,6 +173,7 @@ rsg_status rsg_generate_files_fd(rsg_ctx *ctx, const rsg_fd_file *files, uint64_
     }
     // Batches of whole blocks, <= kBatchBytes of staging (a single block
     // larger than that travels alone), files cut on block boundaries.
+    const uint64_t kBatchBytes = batch_bytes();
     std::vector<Batch> batches(1);
     for (uint64_t i = 0; i < nfiles; i++) {
         const uint64_t B = (uint64_t)heads[i].block_len, cnt = (uint64_t)heads[i].count;

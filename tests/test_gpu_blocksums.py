@@ -201,6 +201,27 @@ def test_kernel_variants_match(eng, variant, blen):
     assert rec_dev == want
 
 
+@pytest.mark.parametrize("variant", [1, 3, 4, 5])
+def test_variants_long_blocks_full_waves(eng, variant):
+    """cfg5's block length with full 64-block waves (the staged LDS-DMA path
+    of variants 1/4/5, not only their direct fallback): a 24 MiB file at
+    B = 128 KiB plus a ragged second file."""
+    from rsync_amd import _lib
+    lens = [24 << 20, (3 << 20) + 777]
+    datas = [cases.splitmix64_bytes(6000 + i, n) for i, n in enumerate(lens)]
+    offs = [0, lens[0]]
+    arena = eng.alloc(sum(lens))
+    arena.upload(np.concatenate(datas))
+    want = b"".join(orc.block_sums(d, 131072, cases.SEED) for d in datas)
+    try:
+        _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))
+        recs, total = eng.block_sums_device(arena, [(o, n, 131072) for o, n in zip(offs, lens)], cases.SEED)
+        got = recs.download(total * 20).tobytes()
+    finally:
+        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+    assert got == want
+
+
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_variants_device_aligned_arena(eng, variant):
     """Aligned device arena (the staged / park fast paths), files straddling
