@@ -66,6 +66,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")  # control plane only; data moves over RCCL
+    # one rank per GPU; on a box with fewer GPUs than ranks (a 1-GPU rehearsal
+    # of the multi-rank path) ranks share devices round-robin
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     import rsync_amd
     if args.workload == "cfg3":
@@ -156,8 +159,44 @@ def main():
     value = world * in_bytes * args.steps / wall / GIB
     achieved = (in_bytes + out_bytes) / (kernel_ms * 1e-3) / 1e9
 
+    cpu = None  # filled in below on rank 0 at N = 1
+
+    def bench_line(more):
+        traffic = None
+        tp = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(tp):
+            try:
+                traffic = json.load(open(tp)).get("block_sums_kernel_cfg2_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": "GiB/s block-checksummed (weak+MD4), device-resident, at 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "warmup_effective": warm,
+            "ms_per_step": round(wall * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (splitmix64 bytes generated on device)",
+            "config": {"workload": "cfg2: receiver block sums, 1024 x 1 MiB files per GPU, B=700, weak+MD4",
+                       "files_per_gpu": n, "file_bytes": FILE_BYTES, "block_len": BLOCK_LEN,
+                       "records_per_gpu": plan.total_records, "parallelism": f"files sharded, {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel_ms": round(kernel_ms, 4),
+                         "algorithmic_bytes_per_launch": int(in_bytes + out_bytes)},
+            "cpu_baseline": cpu,
+        }
+        line.update(more)
+        return line
+
     # ---- RCCL gather of every rank's records to rank 0 (the one exchange step)
-    if world > 1:
+    def run_gather():
         uid = [rsync_amd.Engine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init(world, rank, uid[0])
@@ -177,8 +216,28 @@ def main():
         dist.all_reduce(gt, op=dist.ReduceOp.MAX)
         gather_ms = float(gt[0])
         step_ms = wall * 1e3 / args.steps
-        extra["gather"] = {"bytes_to_root": int(out_bytes) * (world - 1), "ms": round(gather_ms, 4),
-                           "kernel_plus_gather_gib_s": round(world * in_bytes / ((step_ms + gather_ms) * 1e-3) / GIB, 2)}
+        return {"bytes_to_root": int(out_bytes) * (world - 1), "ms": round(gather_ms, 4),
+                "kernel_plus_gather_gib_s": round(world * in_bytes / ((step_ms + gather_ms) * 1e-3) / GIB, 2)}
+
+    if world > 1:
+        # The timed steps are over; the gather is reported beside them.  A
+        # watchdog on every rank keeps a stuck collective from swallowing the
+        # bench line: after 120 s rank 0 prints it without the gather and
+        # every rank exits.
+        import threading
+        gather_done = threading.Event()
+
+        def watchdog():
+            if not gather_done.wait(120.0):
+                if rank == 0:
+                    print(json.dumps(bench_line(dict(extra, gather={"error": "timed out after 120 s"}))), flush=True)
+                os._exit(0)
+        threading.Thread(target=watchdog, daemon=True).start()
+        try:
+            extra["gather"] = run_gather()
+        except Exception as e:  # reported, never fatal to the bench line
+            extra["gather"] = {"error": str(e)[:300]}
+        gather_done.set()
 
     # ---- PCIe-inclusive host path (rank 0, N = 1): host buffers in, records out
     if rank == 0 and world == 1 and not args.no_host_path:
@@ -294,38 +353,7 @@ def main():
                       f"same orc_block_sums, {wdt:.1f} s wall"}
 
     if rank == 0:
-        traffic = None
-        tp = os.path.join(ROOT, "profiles", "traffic.json")
-        if os.path.exists(tp):
-            try:
-                traffic = json.load(open(tp)).get("block_sums_kernel_cfg2_bytes_per_launch")
-            except Exception:
-                traffic = None
-        line = {
-            "metric": "GiB/s block-checksummed (weak+MD4), device-resident, at 1/2/4/8 MI355X",
-            "value": round(value, 2),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "warmup_effective": warm,
-            "ms_per_step": round(wall * 1e3 / args.steps, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic (splitmix64 bytes generated on device)",
-            "config": {"workload": "cfg2: receiver block sums, 1024 x 1 MiB files per GPU, B=700, weak+MD4",
-                       "files_per_gpu": n, "file_bytes": FILE_BYTES, "block_len": BLOCK_LEN,
-                       "records_per_gpu": plan.total_records, "parallelism": f"files sharded, {world} GPU(s)"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel_ms": round(kernel_ms, 4),
-                         "algorithmic_bytes_per_launch": int(in_bytes + out_bytes)},
-            "cpu_baseline": cpu,
-        }
-        line.update(extra)
-        print(json.dumps(line), flush=True)
+        print(json.dumps(bench_line(extra)), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
