@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--ab", action="store_true", help="A/B the block-sum kernel variants (interleaved rounds)")
-    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5"],
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5", "filesums"],
                     help="cfg2 = receiver block sums (the metric); cfg3 = sender match, reported separately")
     ap.add_argument("--cfg3-files", type=int, default=10)
     return ap.parse_args()
@@ -77,6 +77,8 @@ def main():
         return bench_mixed(args, rank, world, local)
     if args.workload == "cfg5":
         return bench_long(args, rank, world, local)
+    if args.workload == "filesums":
+        return bench_filesums(args, rank, world, local)
 
     eng = rsync_amd.Engine(local)
     stream = torch.cuda.Stream(device=local)
@@ -649,6 +651,79 @@ def bench_long(args, rank, world, local):
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_filesums(args, rank, world, local):
+    """Whole-file MD4 over cfg4's file set: 100 000
+    files of uniform length in [4096, 65536] (PRNG seed 4), one lane per file,
+    both modes -- seeded MD4(int32_LE(seed) || file), the transfer's file sum
+    (match.go:52-53, receiver.go:117-120), and plain MD4(file), the
+    --checksum file list (rsyncchecksum.go:60-66).  One step = one
+    rsg_file_sums_device call (descriptor upload + launch + wait) over the
+    whole set, resident in HBM.  Spot parity and the CPU baseline use the
+    oracle's orc_file_sum."""
+    import ctypes
+    import rsync_amd
+    from rsync_amd import _lib
+    NF = 100_000
+    lengths = np.random.default_rng(4).integers(4096, 65537, NF).tolist()
+    eng = rsync_amd.Engine(local)
+    offs, at = [], 0
+    for n in lengths:
+        offs.append(at)
+        at += (n + 15) & ~15
+    arenas = [eng.alloc(at) for _ in range(2)]
+    for k, a in enumerate(arenas):
+        for f in range(0, NF, 1):
+            eng.fill_splitmix64(a, lengths[f], f + 1, offset=offs[f])
+    eng.synchronize()
+    desc = (_lib.File * NF)()
+    for i, (o, n) in enumerate(zip(offs, lengths)):
+        desc[i].offset, desc[i].len = o, n
+    out = eng.alloc(NF * 16)
+    total = sum(lengths)
+    res = {}
+    for mode, name in ((_lib.FILESUM_SEEDED, "seeded"), (_lib.FILESUM_PLAIN, "plain")):
+        def call(i):
+            _lib.check(_lib.lib.rsg_file_sums_device(eng.ctx, ctypes.c_void_p(arenas[i & 1].ptr), at, desc, NF,
+                                                     mode, ctypes.c_int32(SEED),
+                                                     ctypes.c_void_p(out.ptr)), eng.ctx)
+        for i in range(5):
+            call(i)
+        steps = max(4, min(args.steps, 40))
+        t0 = time.perf_counter()
+        for i in range(steps):
+            call(i)
+        dt = (time.perf_counter() - t0) / steps
+        res[name] = {"ms_per_call": round(dt * 1e3, 4), "gib_s": round(total / dt / GIB, 2),
+                     "hbm_frac_8tbs": round(total / dt / 1e9 / HBM_PEAK_GBS, 4)}
+    # parity (plain mode is the last one run, on arena (steps - 1) & 1) and the CPU baseline
+    from oracle import oracle as orc
+    last = arenas[(steps - 1) & 1]
+    dig = out.download(NF * 16).reshape(NF, 16)
+    parity, t_cpu, done, k = True, 0.0, 0, 0
+    rng = np.random.default_rng(9)
+    while t_cpu < args.cpu_seconds / 2 and k < 4096:
+        f = int(rng.integers(0, NF))
+        data = last.download(lengths[f], offset=offs[f])
+        c0 = time.perf_counter()
+        want = orc.file_sum(_lib.FILESUM_PLAIN, 0, data)
+        t_cpu += time.perf_counter() - c0
+        done += lengths[f]
+        if k < 256:
+            parity &= bytes(dig[f]) == want
+        k += 1
+    print(json.dumps({
+        "metric": "GiB/s whole-file MD4 (lane per file), device-resident", "value": res["seeded"]["gib_s"],
+        "unit": "GiB/s", "n_gpus": 1, "steps": steps, "higher_is_better": True, "dtype": "u32",
+        "data": "synthetic (splitmix64 bytes generated on device)",
+        "config": {"workload": "whole-file MD4 over cfg4's 100k files (4-64 KiB)", "files": NF, "total_bytes": total,
+                   "call": "rsg_file_sums_device, descriptors uploaded and waited on per call"},
+        "modes": res, "spot_parity": {"files": min(k, 256), "equal": parity},
+        "cpu_baseline": {"value": round(done / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+                         "sample": f"{k} random files of the set, oracle/rsg_oracle.c orc_file_sum (plain), "
+                                   f"1 thread, {t_cpu:.1f} s"}}), flush=True)
+    eng.close()
 
 
 if __name__ == "__main__":

@@ -11,7 +11,6 @@
 
 #include <algorithm>
 #include <mutex>
-#include <numeric>
 #include <vector>
 
 #include "rsg_host.h"
@@ -26,12 +25,22 @@ rsg_status check_mode(rsg_ctx *ctx, int32_t mode) {
     return RSG_OK;
 }
 
-// Longest first, so the 64 lanes of a wave hash similar numbers of chunks.
+// Longest first, so the 64 lanes of a wave hash similar numbers of chunks
+// (and the one-wave workgroups form an LPT schedule).  Only approximate order
+// matters: a counting sort on the length in KiB (capped), stable, O(n).
 std::vector<uint32_t> lane_order(const std::vector<rsg::FileSpan> &spans) {
+    constexpr uint64_t kKeys = 1u << 16;
+    auto key = [](uint64_t len) { return (uint32_t)std::min<uint64_t>(len >> 10, kKeys - 1); };
+    std::vector<uint32_t> count(kKeys + 1, 0);
+    for (const rsg::FileSpan &f : spans) count[kKeys - 1 - key(f.len)]++;  // descending length
+    uint32_t at = 0;
+    for (uint64_t k = 0; k <= kKeys; k++) {
+        const uint32_t c = count[k];
+        count[k] = at;
+        at += c;
+    }
     std::vector<uint32_t> order(spans.size());
-    std::iota(order.begin(), order.end(), 0u);
-    std::stable_sort(order.begin(), order.end(),
-                     [&](uint32_t a, uint32_t b) { return spans[a].len > spans[b].len; });
+    for (uint32_t i = 0; i < (uint32_t)spans.size(); i++) order[count[kKeys - 1 - key(spans[i].len)]++] = i;
     return order;
 }
 
