@@ -579,6 +579,13 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
     const uint32_t fmax = wg_file[nwg256];  // the batch's last block's file: no tile needs a later one
     uint64_t off = 0;
     uint32_t n = 0;
+    // The tile's lowest block offset, its highest block offset + 704 and its
+    // largest block length, from the descriptors (wave-uniform, scalar
+    // arithmetic: no cross-lane reductions, whose serialized bpermutes cost
+    // the loader ~1 us per tile).  Within a file, offsets grow with the block
+    // index; the largest B bounds every n.
+    uint64_t lo_off = ~0ull, top = 0;
+    uint32_t bmax = 0;
     // Small files (cfg4: 4-64 KiB) put up to ~11 files in a tile: four
     // descriptors per step, their scalar loads issued together.
     bool done = false;
@@ -590,21 +597,30 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
 #pragma unroll
         for (uint32_t i = 0; i < 4; i++) {
             if (done) break;
-            if (g >= F[i].first_block && g < F[i].first_block + F[i].nblocks) {
-                const uint64_t boff = (g - F[i].first_block) * F[i].blen;
+            const uint64_t fb = F[i].first_block, fe = fb + F[i].nblocks;
+            if (g >= fb && g < fe) {
+                const uint64_t boff = (g - fb) * F[i].blen;
                 const uint64_t left = F[i].len - boff;
                 n = left < F[i].blen ? (uint32_t)left : F[i].blen;  // generator.go:334
                 off = F[i].offset + boff;
             }
-            done = F[i].first_block + F[i].nblocks >= gend || f + i >= fmax;
+            if (fe > fb && fe > g0 && fb < gend) {  // the file has blocks in this tile
+                const uint64_t b_first = (g0 > fb ? g0 : fb) - fb, b_last = (gend < fe ? gend : fe) - 1 - fb;
+                const uint64_t o_first = F[i].offset + b_first * F[i].blen;
+                const uint64_t o_top = F[i].offset + b_last * F[i].blen + 704u;
+                lo_off = o_first < lo_off ? o_first : lo_off;
+                top = o_top > top ? o_top : top;
+                bmax = F[i].blen > bmax ? F[i].blen : bmax;
+            }
+            done = fe >= gend || f + i >= fmax;
         }
     }
-    const uint64_t lo_v = wave_min_u64(n ? off : ~0ull);
-    d.base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo_v >> 32)) << 32) |
-             __builtin_amdgcn_readfirstlane((uint32_t)lo_v);
-    const uint64_t top = wave_max_u64(n ? off + 704u : 0);
-    const uint32_t nmax = (uint32_t)wave_max_u64(n);
-    d.staged = (g0 + 64 <= total_blocks) && nmax <= kRegMaxBytes && top <= arena_bytes &&
+    d.base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo_off >> 32)) << 32) |
+             __builtin_amdgcn_readfirstlane((uint32_t)lo_off);
+    top = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(top >> 32)) << 32) |
+          __builtin_amdgcn_readfirstlane((uint32_t)top);
+    bmax = __builtin_amdgcn_readfirstlane(bmax);
+    d.staged = (g0 + 64 <= total_blocks) && bmax <= kRegMaxBytes && top <= arena_bytes &&
                top - d.base <= 0x7FFFFFFFull;
     d.off = off;
     d.n = n;
@@ -660,8 +676,31 @@ __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, con
         }
     } else {
         if constexpr (UNROLL) {
+            // Irregular tile: each instruction's offsets come from two
+            // ds_bpermutes.  Issued one instruction at a time, every DMA waits
+            // for its own bpermutes (an lgkmcnt wait per instruction, the LDS
+            // busy with DMA writes and the hashers' copy-out); in batches of 9
+            // the 18 bpermutes go out back to back and the 9 DMAs follow.
+            constexpr uint32_t kBatch = 9;
+            static_assert(kPkDma % kBatch == 0, "whole batches");
 #pragma unroll
-            for (uint32_t i = 0; i < kPkDma; i++) RSG_PK_ONE(i, false);
+            for (uint32_t i0 = 0; i0 < kPkDma; i0 += kBatch) {
+                uint32_t rj[kBatch], nj[kBatch];
+#pragma unroll
+                for (uint32_t k = 0; k < kBatch; k++) {
+                    rj[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * jj[i0 + k]), rel);
+                    nj[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * jj[i0 + k]), (int)d.n);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (uint32_t k = 0; k < kBatch; k++) {
+                    const uint32_t u16 = uu[i0 + k];
+                    const uint32_t vo = u16 < nj[k] ? rj[k] + u16 : 0x80000000u;
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * (i0 + k)), 16, vo, 0, 0, AUX);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
         } else {
 #pragma unroll 1
             for (uint32_t i = 0; i < kPkDma; i++) RSG_PK_ONE(i, false);
