@@ -147,12 +147,14 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
  * block per segment), 2 = park (three loader waves stream 64-block tiles
  * through LDS, five hasher waves park the blocks in registers; blocks <= 703
  * bytes, otherwise 1 is used), 3 = deep per-lane prefetch for long blocks,
- * 4 / 5 = staged with 128- / 512-byte segments.  Automatic: aligned batches
- * take 2 when 512 <= the largest block <= 703 bytes, else 1; unaligned
- * batches (a block not 4-byte aligned) take 3 for blocks >= 8 KiB, else 0
- * (1, 2, 4 and 5 fall back to 0 there).  The environment variable
- * RSG_BLOCKSUMS_KERNEL sets the initial value.  Returns RSG_ERR_INVALID
- * outside -1..5. */
+ * 4 / 5 = staged with 128- / 512-byte segments, 6 = staged for blocks at
+ * any byte offset (pieces fetched from the 4-byte aligned address below the
+ * block, funnel-shifted in registers; needs a 4-byte aligned arena, else 3).
+ * Automatic: aligned batches take 2 when 512 <= the largest block <= 703
+ * bytes, else 1; unaligned batches (a block not 4-byte aligned) take 6 for
+ * blocks >= 8 KiB, else 0 (1, 2, 4 and 5 fall back to 0 there).  The
+ * environment variable RSG_BLOCKSUMS_KERNEL sets the initial value.  Returns
+ * RSG_ERR_INVALID outside -1..6. */
 rsg_status rsg_set_block_sums_kernel(int32_t variant);
 
 /* Timing diagnostics for DESIGN.md's roofline analysis, NOT for use: while

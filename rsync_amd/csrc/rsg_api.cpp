@@ -145,7 +145,7 @@ rsg_status launch_plan(rsg_ctx *ctx, const HostPlan &plan, const void *d_files, 
     RSG_HIP(ctx, rsg::launch_block_sums((const uint8_t *)d_arena, plan.arena_bytes, (const DevFile *)d_files,
                                         (const uint32_t *)d_wg, plan.total_blocks, plan.nwg, aligned,
                                         plan.max_blen, (uint32_t)seed, (uint8_t *)d_records,
-                                        (uint32_t *)d_scratch, stream));
+                                        (uint32_t *)d_scratch, plan.lds_reserve, stream));
     return RSG_OK;
 }
 
@@ -242,6 +242,7 @@ rsg_status rsg_ctx_create(int32_t device, rsg_ctx **out) {
     if ((e = hipSetDevice(device)) != hipSuccess || (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&c->side[0], hipStreamNonBlocking)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&c->side[1], hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->confirm, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->side_done[0], hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->side_done[1], hipEventDisableTiming)) != hipSuccess) {
         rsg_status s = hip_fail(nullptr, e, "context streams");
@@ -258,6 +259,7 @@ void rsg_ctx_destroy(rsg_ctx *c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     for (int i = 0; i < 2; i++)
         if (c->side[i]) hipStreamSynchronize(c->side[i]);
+    if (c->confirm) hipStreamSynchronize(c->confirm);
     DevBuf *dbs[] = {&c->d_files, &c->d_wg, &c->d_in[0], &c->d_in[1], &c->d_out[0], &c->d_out[1],
                      &c->d_desc[0], &c->d_desc[1], &c->d_fb[0], &c->d_fb[1], &c->d_res};
     for (DevBuf *b : dbs)
@@ -280,6 +282,7 @@ void rsg_ctx_destroy(rsg_ctx *c) {
         if (c->side_done[i]) hipEventDestroy(c->side_done[i]);
         if (c->side[i]) hipStreamDestroy(c->side[i]);
     }
+    if (c->confirm) hipStreamDestroy(c->confirm);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -417,7 +420,7 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
 }
 
 rsg_status rsg_set_block_sums_kernel(int32_t variant) {
-    if (variant < -1 || variant > 5) return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..5");
+    if (variant < -1 || variant > 6) return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..6");
     rsg::set_block_sums_variant(variant);
     return RSG_OK;
 }

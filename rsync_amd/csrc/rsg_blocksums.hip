@@ -344,14 +344,19 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 }
 // KIND % 10: 0 = the product kernel; timing diagnostics (outputs
 // meaningless): 1 = DMA + LDS reads only (the memory cost of this access
-// pattern), 2 = hashing only, no DMA (the compute cost).  KIND / 10 picks the
-// segment: 0 = 256 bytes, 1 = 128, 2 = 512.
+// pattern), 2 = hashing only, no DMA (the compute cost).  (KIND / 10) % 10
+// picks the segment: 0 = 256 bytes, 1 = 128, 2 = 512.  KIND >= 100: blocks
+// start at any byte (the sender's confirmation windows; the arena itself
+// 4-byte aligned): each piece is fetched from the block's start rounded down
+// to 4 bytes, one 16-byte unit longer (the pad unit carries data), and the
+// lane funnel-shifts its words (alignbyte) as the direct kernel does.
 template <int KIND>
 __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
+    constexpr bool UNAL = KIND >= 100;
     constexpr int MODE = KIND % 10;
-    constexpr uint32_t SEG = KIND >= 20 ? 512u : (KIND >= 10 ? 128u : 256u);
+    constexpr uint32_t SEG = (KIND % 100) >= 20 ? 512u : ((KIND % 100) >= 10 ? 128u : 256u);
     constexpr uint32_t kSegBytes = Seg<SEG>::kSegBytes, kUnits = Seg<SEG>::kUnits, kPiece = Seg<SEG>::kPiece;
     constexpr uint32_t kWaveSlab = Seg<SEG>::kWaveSlab, kDmaPerSeg = Seg<SEG>::kDmaPerSeg;
     constexpr uint32_t kChunks = Seg<SEG>::kChunks;
@@ -366,12 +371,14 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     uint64_t off = 0;
     uint32_t n = 0;
     if (g < total_blocks) locate_block(files, wg_file, g, off, n);
+    const uint32_t sh = UNAL ? (uint32_t)(off & 3u) : 0u;
+    const uint64_t loff = off - sh;  // 4-byte aligned fetch start
     const uint32_t nseg = n ? (n >> 6) / kChunks + 1 : 0;  // segments through the tail chunk
     const uint32_t S = __builtin_amdgcn_readfirstlane((uint32_t)wave_max_u64(nseg));
-    const uint64_t lo_v = wave_min_u64(n ? off : ~0ull);
+    const uint64_t lo_v = wave_min_u64(n ? loff : ~0ull);
     const uint64_t base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo_v >> 32)) << 32) |
                           __builtin_amdgcn_readfirstlane((uint32_t)lo_v);
-    const uint64_t top = wave_max_u64(n ? off + (uint64_t)kSegBytes * S : 0);
+    const uint64_t top = wave_max_u64(n ? loff + (uint64_t)kSegBytes * S + (UNAL ? 16u : 0u) : 0);
     // Wave-uniform choice of path: the staged path needs all 64 blocks, every
     // DMA read inside the arena and the span addressable by a 31-bit buffer
     // offset.  Otherwise (last partial wave, a file ending at the arena's end,
@@ -383,13 +390,13 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
         md4_init(h);
         int32_t s1 = 0;
         uint32_t t = 0;
-        hash_block_direct<true>(arena, (uintptr_t)(arena + arena_bytes), off, n, seed, h, s1, t);
+        hash_block_direct<!UNAL>(arena, (uintptr_t)(arena + arena_bytes), off, n, seed, h, s1, t);
         store_record(out, g, n, s1, t, h);
         return;
     }
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)(arena + base), (short)0, 0x7FFFFFFF, 0x00020000);
-    const uint32_t rel = (uint32_t)(off - base);
+    const uint32_t rel = (uint32_t)(loff - base);
     // DMA instruction i, lane t fills slab bytes [16*(64 i + t), +16): piece
     // j = (64 i + t) / kUnits (lane j's block), unit u = (64 i + t) % kUnits.
     // u == kUnits - 1 is the pad: its offset is past num_records, so the
@@ -402,9 +409,9 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
         const uint32_t idx = 64u * i + lane;
         const uint32_t j = idx / kUnits, u = idx - kUnits * j;
         const uint32_t v = (uint32_t)__shfl((int)rel, (int)j, 64) + 16u * u;
-        voff[i] = u + 1 < kUnits ? v : 0x80000000u;
+        voff[i] = (UNAL || u + 1 < kUnits) ? v : 0x80000000u;
     }
-    uint32_t R[Seg<512>::kSegBytes / 4];  // fixed bound, as voff
+    uint32_t R[Seg<512>::kSegBytes / 4 + 4];  // fixed bound, as voff
     const uint8_t *mine = slab + lane * kPiece;
 #define RSG_DMA_SEGMENT(S_)                                                                                      \
     do {                                                                                                         \
@@ -416,7 +423,7 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
 #define RSG_READ_SEGMENT()                                                                                       \
     do {                                                                                                         \
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                                         \
-        _Pragma("unroll") for (int q_ = 0; q_ < (int)(SEG / 16); q_++) {                                         \
+        _Pragma("unroll") for (int q_ = 0; q_ < (int)(SEG / 16) + (UNAL ? 1 : 0); q_++) {                        \
             const uint4 v_ = *reinterpret_cast<const uint4 *>(mine + 16 * q_);                                  \
             R[4 * q_ + 0] = v_.x; R[4 * q_ + 1] = v_.y; R[4 * q_ + 2] = v_.z; R[4 * q_ + 3] = v_.w;              \
         }                                                                                                        \
@@ -440,8 +447,8 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
 #pragma unroll
             for (uint32_t i = 0; i < kChunks; i++) {
                 const uint32_t c = kChunks * cs + i;
-                if (c < nfull) hash_chunk<true>(R + 16 * i, 0u, 0u, c, h, s1, t);
-                else if (c == nfull) hash_tail<true>(R + 16 * i, 0u, 0u, n, seed, h, s1, t);
+                if (c < nfull) hash_chunk<!UNAL>(R + 16 * i, R[16 * i + 16], sh, c, h, s1, t);
+                else if (c == nfull) hash_tail<!UNAL>(R + 16 * i, R[16 * i + 16], sh, n, seed, h, s1, t);
             }
         }
         if (more) RSG_READ_SEGMENT();
@@ -901,13 +908,14 @@ static uint32_t park_grid(uint64_t total_blocks) {
 
 hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const DevFile *files,
                              const uint32_t *wg_file, uint64_t total_blocks, uint32_t nwg, bool aligned,
-                             uint32_t max_blen, uint32_t seed, uint8_t *out, uint32_t *scratch, hipStream_t stream) {
+                             uint32_t max_blen, uint32_t seed, uint8_t *out, uint32_t *scratch,
+                             uint32_t lds_reserve, hipStream_t stream) {
     (void)scratch;
     if (total_blocks == 0) return hipSuccess;
     if (g_variant == -2) {
         const char *e = getenv("RSG_BLOCKSUMS_KERNEL");
         g_variant = e ? atoi(e) : -1;
-        if (g_variant < -1 || g_variant > 5) g_variant = -1;
+        if (g_variant < -1 || g_variant > 6) g_variant = -1;
     }
     if (g_diag == -2) {
         const char *e = getenv("RSG_BLOCKSUMS_DIAG");
@@ -951,8 +959,11 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     int v = g_variant;
     if (v == -1)
         v = aligned ? ((max_blen <= kRegMaxBytes && max_blen >= kParkMinBytes) ? 2 : 1)
-                    : (max_blen >= kLongBlockBytes ? 3 : 0);
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;  // the LDS-DMA kernels need 4-byte aligned blocks
+                    : (max_blen >= kLongBlockBytes ? 6 : 0);
+    // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
+    // staged kernel (6) needs a 4-byte aligned arena
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
+    if (v == 6 && ((uintptr_t)arena & 3u)) v = 3;
     if (v == 2 && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
@@ -962,6 +973,14 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders>), pgrid, pblock, 0, stream, arena, arena_bytes, files,
                                wg_file, nwg, total_blocks, seed, out);
+            break;
+        case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel
+            if (aligned)
+                hipLaunchKernelGGL((block_sums_staged<0>), grid, block, lds_reserve, stream, arena, arena_bytes, files,
+                                   wg_file, total_blocks, seed, out);
+            else
+                hipLaunchKernelGGL((block_sums_staged<100>), grid, block, lds_reserve, stream, arena, arena_bytes,
+                                   files, wg_file, total_blocks, seed, out);
             break;
         case 4:
             hipLaunchKernelGGL((block_sums_staged<10>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
@@ -977,16 +996,16 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             const uint32_t lt = two ? 128u : 64u;
             const dim3 lg((uint32_t)((total_blocks + lt - 1) / lt)), lb(lt);
             if (aligned && two)
-                hipLaunchKernelGGL((block_sums_long<true, 2>), lg, lb, 0, stream, arena, arena_bytes, files, wg_file,
+                hipLaunchKernelGGL((block_sums_long<true, 2>), lg, lb, lds_reserve, stream, arena, arena_bytes, files, wg_file,
                                    total_blocks, seed, out);
             else if (aligned)
-                hipLaunchKernelGGL((block_sums_long<true, 1>), lg, lb, 0, stream, arena, arena_bytes, files, wg_file,
+                hipLaunchKernelGGL((block_sums_long<true, 1>), lg, lb, lds_reserve, stream, arena, arena_bytes, files, wg_file,
                                    total_blocks, seed, out);
             else if (two)
-                hipLaunchKernelGGL((block_sums_long<false, 2>), lg, lb, 0, stream, arena, arena_bytes, files,
+                hipLaunchKernelGGL((block_sums_long<false, 2>), lg, lb, lds_reserve, stream, arena, arena_bytes, files,
                                    wg_file, total_blocks, seed, out);
             else
-                hipLaunchKernelGGL((block_sums_long<false, 1>), lg, lb, 0, stream, arena, arena_bytes, files,
+                hipLaunchKernelGGL((block_sums_long<false, 1>), lg, lb, lds_reserve, stream, arena, arena_bytes, files,
                                    wg_file, total_blocks, seed, out);
             break;
         }

@@ -42,6 +42,7 @@ struct rsg_ctx {
     hipStream_t stream = nullptr;
     hipStream_t side[2] = {nullptr, nullptr};  // host-path pipeline streams; sender search slots
     hipEvent_t side_done[2] = {nullptr, nullptr};
+    hipStream_t confirm = nullptr;  // sender confirmation batches, beside the next file's roll
     std::recursive_mutex mu;
     std::string err;
     // scratch reused by one-shot calls
@@ -65,6 +66,8 @@ struct HostPlan {
     bool aligned = true;      // every block start is 4-byte aligned (arena base aside)
     uint32_t max_blen = 0;    // largest block length (picks blocks per lane)
     uint64_t arena_bytes = 0;
+    uint32_t lds_reserve = 0;  // dynamic LDS per workgroup of the long-block kernel (keeps it off CUs
+                               // that hold a roll workgroup, rsg_match.cpp)
 };
 
 struct rsg_plan {

@@ -53,6 +53,8 @@ struct PhaseTimer {
     }
 };
 
+constexpr int kConfirmCus = 32;  // default RSG_CONFIRM_CUS (0 / 16 / 24 / 32 / 40 / 48 / 64 measured)
+
 struct Search {
     PhaseTimer pt;
     rsg_ctx *ctx;
@@ -81,6 +83,8 @@ struct Search {
     const uint8_t *d_sum2 = nullptr;
     const uint64_t *d_table = nullptr;
     uint32_t ntiles = 0, tile_end = 0, bmask = 0, cus = 256;
+    uint32_t roll_grid = 0;    // roll workgroups (0 = one per CU)
+    uint32_t confirm_lds = 0;  // dynamic LDS of the confirmation kernel's workgroups
     bool fused = false;  // roll derives its window sums itself (B <= kFusedMaxB)
     bool pending = false;  // prepare() launched the roll of [0, tile_end) and its count read-back
 
@@ -126,6 +130,7 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
     plan.aligned = false;
     plan.arena_bytes = S.size;
     plan.max_blen = 0;
+    plan.lds_reserve = S.confirm_lds;
     std::vector<uint32_t> wlen(idx.size());
     for (size_t i = 0; i < idx.size(); i++) {
         const uint64_t q = C[idx[i]];
@@ -363,7 +368,7 @@ rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
 
     int dev_cus = 256;
     hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    S.cus = (uint32_t)dev_cus;
+    S.cus = S.roll_grid ? std::min<uint32_t>(S.roll_grid, (uint32_t)dev_cus) : (uint32_t)dev_cus;
     const uint64_t scan_end = std::min<uint64_t>((uint64_t)S.end, S.size);
     S.tile_end = (uint32_t)((scan_end + kScanTile - 1) / kScanTile);
     if ((s = launch_range(S, 0, S.tile_end)) != RSG_OK) return s;
@@ -486,6 +491,14 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
     RSG_HIP(ctx, hipEventRecord(ctx->side_done[0], ctx->stream));
     for (int k = 0; k < 2; k++) RSG_HIP(ctx, hipStreamWaitEvent(ctx->side[k], ctx->side_done[0], 0));
 
+    // RSG_CONFIRM_CUS: CUs the roll leaves to the confirmation of the
+    // previous job (0 = the confirmation queues behind the next roll on one
+    // stream, as before)
+    int dev_cus = 256;
+    RSG_HIP(ctx, hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    const char *cc = getenv("RSG_CONFIRM_CUS");
+    const int spare = std::max(0, std::min(cc ? atoi(cc) : kConfirmCus, dev_cus - 1));
+    const bool split = spare > 0 && njobs > 1;  // one job: nothing to overlap its confirmation with
     std::unique_ptr<Search> live[kSearchSlots];
     // Validate job i and issue its stage 1.  Returns only fatal statuses; a
     // job-local failure is recorded on the job, which then holds no search.
@@ -502,6 +515,17 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
         S->sl = &ctx->search[slot];
         S->st = ctx->side[0];
         S->cst = ctx->side[0];
+        if (split) {
+            // Confirmation of job i on its own stream, beside the roll of job
+            // i+1: the roll leaves `spare` CUs free (one persistent workgroup
+            // per CU on the others), and the confirmation workgroups reserve
+            // 8 KiB of LDS they do not use, which cannot fit beside a roll
+            // workgroup's 156 KiB, so they land on the free CUs (or on CUs the
+            // roll has finished with) instead of slowing the roll's SIMDs.
+            S->cst = ctx->confirm;
+            S->roll_grid = (uint32_t)std::max(1, dev_cus - spare);
+            S->confirm_lds = 8192;
+        }
         S->side = ctx->side[1];
         S->copy = ctx->stream;
         S->size = j.src_len;
@@ -518,6 +542,7 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
     };
     // RSG_SEARCH_OVERLAP=0: issue job i+1 only after job i is finished (A/B measurement)
     const char *ov = getenv("RSG_SEARCH_OVERLAP");
+
     const bool overlap = !(ov && ov[0] == '0');
     rsg_status fatal = RSG_OK;
     uint64_t i = 0;

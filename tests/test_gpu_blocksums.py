@@ -176,7 +176,7 @@ def test_generate_and_send_sums_wire(eng):
     assert bytes(conn.buf) == want
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("blen", [700, 64, 1773, 4096, 131072])
 def test_kernel_variants_match(eng, variant, blen):
     """Every kernel variant (direct / staged / park / long / staged with 128-
@@ -201,7 +201,33 @@ def test_kernel_variants_match(eng, variant, blen):
     assert rec_dev == want
 
 
-@pytest.mark.parametrize("variant", [1, 3, 4, 5])
+@pytest.mark.parametrize("variant", [-1, 3, 6])
+@pytest.mark.parametrize("blen", [32768, 8192, 131072])
+def test_unaligned_windows(eng, variant, blen):
+    """The sender's confirmation shape: windows of one block each at random
+    byte offsets of a source (plus windows cut short by the source's end and
+    one ending exactly there), enough for full 64-window waves of the
+    unaligned staged kernel (variant 6, the automatic choice for unaligned
+    blocks >= 8 KiB) and of the deep-prefetch kernel (3)."""
+    from rsync_amd import _lib
+    size = 24 << 20
+    src = cases.splitmix64_bytes(777, size)
+    arena = eng.alloc(size)
+    arena.upload(src)
+    rng = np.random.default_rng(blen)
+    offs = sorted(int(x) for x in rng.integers(0, size - blen, 300))
+    wins = [(o, blen) for o in offs] + [(size - blen // 3, blen // 3), (size - blen, blen), (size - 1, 1)]
+    want = b"".join(orc.block_sums(src[o:o + n], blen, cases.SEED) for o, n in wins)
+    try:
+        _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))
+        recs, total = eng.block_sums_device(arena, [(o, n, blen) for o, n in wins], cases.SEED)
+        got = recs.download(total * 20).tobytes()
+    finally:
+        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+    assert got == want
+
+
+@pytest.mark.parametrize("variant", [1, 3, 4, 5, 6])
 def test_variants_long_blocks_full_waves(eng, variant):
     """cfg5's block length with full 64-block waves (the staged LDS-DMA path
     of variants 1/4/5, not only their direct fallback): a 24 MiB file at
@@ -222,7 +248,7 @@ def test_variants_long_blocks_full_waves(eng, variant):
     assert got == want
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 def test_variants_device_aligned_arena(eng, variant):
     """Aligned device arena (the staged / park fast paths), files straddling
     waves and tiles, a file ending exactly at the arena end (park's direct
