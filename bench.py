@@ -428,17 +428,29 @@ def bench_sender(args, rank, world, local):
     # pass (SendFiles' loop over the files, pipelined across files)
     eng.hash_search_batch(jobs, SEED, as_arrays=True)
     steps = max(1, min(args.steps, 5))
+    import torch.distributed as dist
+    if world > 1:  # files shard across ranks with no exchange: max-over-ranks wall time
+        dist.barrier()
     t0 = time.perf_counter()
     nm = 0
     for _ in range(steps):
         nm += sum(len(m) for m in eng.hash_search_batch(jobs, SEED, as_arrays=True))
     dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt[0])
     # the same files through one single-file call each (no cross-file overlap)
     t1 = time.perf_counter()
     for j in jobs:
         eng.hash_search_device(*j, SEED)
     dt1 = time.perf_counter() - t1
     scanned = sum(m[0] for m in metas) * steps
+    single_gib_s = round(scanned / steps / dt1 / GIB, 2)  # this rank's files, one call each
+    if world > 1:  # every rank's files (all ranks scan the same number of bytes)
+        st = torch.tensor([float(scanned)], dtype=torch.float64)
+        dist.all_reduce(st)
+        scanned = float(st[0])
     if rank == 0:
         print(json.dumps({"metric": "GiB/s source scanned (sender rolling match), device-resident",
                           "value": round(scanned / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
@@ -448,7 +460,7 @@ def bench_sender(args, rank, world, local):
                                      "files": args.cfg3_files, "matches_per_pass": nm // steps,
                                      "call": "rsg_hash_search_batch_device, one call per pass"},
                           "ms_per_file": round(dt * 1e3 / (steps * len(metas)), 3),
-                          "single_file_calls_gib_s": round(scanned / steps / dt1 / GIB, 2)}), flush=True)
+                          "single_file_calls_gib_s": single_gib_s}), flush=True)
     eng.close()
 
 
