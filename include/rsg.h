@@ -193,7 +193,8 @@ rsg_status rsg_block_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfi
  * bytes equal the reference's, message boundaries differ).  heads_out (may be
  * NULL) receives nfiles heads; *bytes_written counts the bytes handed to
  * write.  On failure, the bytes already written are a prefix of the stream.
- * Synchronous; write is called on the calling thread. */
+ * Synchronous; write is called on the calling thread and must not call into
+ * the same context (it holds the context's staging buffers). */
 typedef struct rsg_fd_file {
     int32_t fd;          /* open for reading (Go: int(f.Fd()))          */
     int32_t idx;         /* file-list index written before the SumHead  */

@@ -460,6 +460,12 @@ rsg_status rsg_block_sums_device(rsg_ctx *ctx, const void *d_arena, uint64_t are
 rsg_status rsg_block_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, int32_t seed,
                                uint8_t *records, uint64_t records_cap) {
     RSG_ENTER(ctx);
+    struct Drain {  // no batch stays queued past an early return
+        rsg_ctx *c;
+        ~Drain() {
+            for (int k = 0; k < 2; k++) (void)hipStreamSynchronize(c->side[k]);
+        }
+    } drain_guard{ctx};
     const uint64_t kBatchBytes = 64ull << 20;
     const uint64_t kBatchRecords = 1ull << 22;
     std::vector<rsg_sum_head> heads(nfiles);

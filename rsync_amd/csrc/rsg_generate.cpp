@@ -157,6 +157,15 @@ rsg_status rsg_generate_files_fd(rsg_ctx *ctx, const rsg_fd_file *files, uint64_
     if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
     std::lock_guard<std::recursive_mutex> lock(ctx->mu);
     RSG_HIP(ctx, hipSetDevice(ctx->device));
+    // Whatever path leaves (a read or writer failure mid-batch included),
+    // nothing stays queued on the slot streams that a later call's buffer
+    // growth could free under it.
+    struct Drain {
+        rsg_ctx *c;
+        ~Drain() {
+            for (int k = 0; k < 2; k++) (void)hipStreamSynchronize(c->side[k]);
+        }
+    } drain_guard{ctx};
     if (bytes_written) *bytes_written = 0;
     if (!write || (nfiles && !files)) return fail(ctx, RSG_ERR_INVALID, "NULL argument");
     if (flags & ~(RSG_GEN_IDX | RSG_GEN_TERMINATE | RSG_GEN_MUX))
@@ -268,8 +277,6 @@ rsg_status rsg_generate_files_fd(rsg_ctx *ctx, const rsg_fd_file *files, uint64_
         const int64_t badj = parallel_read(jobs, &code);
         if (badj >= 0) {
             const unsigned long long f = (unsigned long long)jobs[(size_t)badj].file;
-            // drain the other slot so nothing is left queued on the context
-            (void)hipStreamSynchronize(ctx->side[slot ^ 1]);
             if (code == -1) return fail(ctx, RSG_ERR_IO, "file %llu: unexpected EOF", f);  // io.ReadFull
             return fail(ctx, RSG_ERR_IO, "file %llu: read: %s", f, strerror(code));
         }

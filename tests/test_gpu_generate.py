@@ -118,3 +118,31 @@ def test_generate_files_fd_errors(eng, tmp_path):
         assert b"".join(chunks) == expected_stream([data], [700], terminate=False)
     finally:
         os.close(fds[0])
+
+
+def test_generate_files_fd_writer_fails_mid_stream(eng, tmp_path):
+    """A writer that fails on the second batch leaves nothing queued: the next
+    call (with larger batches, so the staging buffers grow) is exact."""
+    import rsync_amd
+    rng = np.random.default_rng(21)
+    datas = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in ((40 << 20) + 7, 3 << 20)]
+    fds = write_files(tmp_path, datas)
+    try:
+        calls = []
+
+        def flaky(b):
+            calls.append(len(b))
+            if len(calls) == 2:
+                raise IOError("peer went away")
+        with pytest.raises(IOError):
+            eng.generate_files_fd([(fd, len(d)) for fd, d in zip(fds, datas)], SEED, flaky, block_len=700)
+        os.environ["RSG_GEN_BATCH_MB"] = "128"
+        try:
+            chunks = []
+            eng.generate_files_fd([(fd, len(d)) for fd, d in zip(fds, datas)], SEED, chunks.append, block_len=700)
+        finally:
+            del os.environ["RSG_GEN_BATCH_MB"]
+        assert b"".join(chunks) == expected_stream(datas, [700, 700])
+    finally:
+        for fd in fds:
+            os.close(fd)
