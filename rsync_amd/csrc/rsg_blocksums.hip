@@ -751,8 +751,10 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
 // MODE 0 = product; diagnostics: 1 = memory only (DMA + copy, no hashing),
 // 2 = hashing only (no DMA: the hashers hash whatever the slots hold).
 // The tile DMA uses the nt cache policy (aux = 2): every byte is read once.
+// (A/B, profiles/r02f_ab_park_cache_policy*.json: the default policy, sc0 or
+// sc1 alone cost 6-9 %; nt combined with sc0 / sc1 equals nt.)
 // NL = loader waves (1 or 2); the other 8 - NL waves hash.
-template <int MODE, int NL>
+template <int MODE, int NL, int AUX>
 __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
@@ -804,7 +806,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             sh.n[slot][lane] = cur.n;
             if (lane == 0) sh.kind[slot] = cur.staged ? 1u : 0u;
             const bool staged = cur.staged;
-            if (staged && MODE != 2) pk_issue<2, true>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
+            if (staged && MODE != 2) pk_issue<AUX, true>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
             uint32_t kn = k + 1;
             while (!owned(kn)) kn++;
             const uint64_t tn = blockIdx.x + (uint64_t)kn * G;
@@ -935,12 +937,12 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                 break;
             case 3:
                 if (max_blen <= kRegMaxBytes)
-                    hipLaunchKernelGGL((block_sums_park<1, kParkLoaders>), pgrid, pblock, 0, stream, arena, arena_bytes,
+                    hipLaunchKernelGGL((block_sums_park<1, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                        files, wg_file, nwg, total_blocks, seed, out);
                 break;
             case 4:
                 if (max_blen <= kRegMaxBytes)
-                    hipLaunchKernelGGL((block_sums_park<2, kParkLoaders>), pgrid, pblock, 0, stream, arena, arena_bytes,
+                    hipLaunchKernelGGL((block_sums_park<2, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                        files, wg_file, nwg, total_blocks, seed, out);
                 break;
             case 5:
@@ -971,7 +973,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                                total_blocks, seed, out);
             break;
         case 2:
-            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders>), pgrid, pblock, 0, stream, arena, arena_bytes, files,
+            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes, files,
                                wg_file, nwg, total_blocks, seed, out);
             break;
         case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel
