@@ -420,7 +420,7 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
 }
 
 rsg_status rsg_set_block_sums_kernel(int32_t variant) {
-    if (variant < -1 || variant > 7) return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..7");
+    if (variant < -1 || variant > 6) return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..6");
     rsg::set_block_sums_variant(variant);
     return RSG_OK;
 }

@@ -354,8 +354,11 @@ template <int KIND>
 __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
-    constexpr bool UNAL = (KIND % 1000) >= 100;
-    constexpr int DMA_AUX = KIND >= 1000 ? 2 : 0;  // 1000 + k: kind k with the nt policy on its DMA
+    constexpr bool UNAL = KIND >= 100;
+    // nt policy on the DMA: every byte is read once (A/B against the default
+    // policy, profiles/r02f_blocklen_sweep_nt.jsonl: B = 4096 0.239 -> 0.219 ms,
+    // cfg5 6.48 -> 6.25 ms, B = 1024 and the sender's confirmation unchanged)
+    constexpr int DMA_AUX = 2;
     constexpr int MODE = KIND % 10;
     constexpr uint32_t SEG = (KIND % 100) >= 20 ? 512u : ((KIND % 100) >= 10 ? 128u : 256u);
     constexpr uint32_t kSegBytes = Seg<SEG>::kSegBytes, kUnits = Seg<SEG>::kUnits, kPiece = Seg<SEG>::kPiece;
@@ -918,7 +921,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     if (g_variant == -2) {
         const char *e = getenv("RSG_BLOCKSUMS_KERNEL");
         g_variant = e ? atoi(e) : -1;
-        if (g_variant < -1 || g_variant > 7) g_variant = -1;
+        if (g_variant < -1 || g_variant > 6) g_variant = -1;
     }
     if (g_diag == -2) {
         const char *e = getenv("RSG_BLOCKSUMS_DIAG");
@@ -966,7 +969,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
     if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
-    if ((v == 6 || v == 7) && ((uintptr_t)arena & 3u)) v = 3;
+    if (v == 6 && ((uintptr_t)arena & 3u)) v = 3;
     if (v == 2 && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
@@ -976,14 +979,6 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes, files,
                                wg_file, nwg, total_blocks, seed, out);
-            break;
-        case 7:  // A/B: staged (aligned: 1, unaligned: 6) with the nt policy on its DMA
-            if (aligned)
-                hipLaunchKernelGGL((block_sums_staged<1000>), grid, block, lds_reserve, stream, arena, arena_bytes,
-                                   files, wg_file, total_blocks, seed, out);
-            else
-                hipLaunchKernelGGL((block_sums_staged<1100>), grid, block, lds_reserve, stream, arena, arena_bytes,
-                                   files, wg_file, total_blocks, seed, out);
             break;
         case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel
             if (aligned)

@@ -201,7 +201,7 @@ def test_kernel_variants_match(eng, variant, blen):
     assert rec_dev == want
 
 
-@pytest.mark.parametrize("variant", [-1, 3, 6, 7])
+@pytest.mark.parametrize("variant", [-1, 3, 6])
 @pytest.mark.parametrize("blen", [32768, 8192, 131072])
 def test_unaligned_windows(eng, variant, blen):
     """The sender's confirmation shape: windows of one block each at random
@@ -248,7 +248,7 @@ def test_variants_long_blocks_full_waves(eng, variant):
     assert got == want
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 def test_variants_device_aligned_arena(eng, variant):
     """Aligned device arena (the staged / park fast paths), files straddling
     waves and tiles, a file ending exactly at the arena end (park's direct
