@@ -963,13 +963,12 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         return hipGetLastError();
     }
     int v = g_variant;
-    if (v == -1)
-        v = aligned ? ((max_blen <= kRegMaxBytes && max_blen >= kParkMinBytes) ? 2 : 1)
-                    : (max_blen >= kLongBlockBytes ? 6 : 0);
+    if (v == -1)  // unaligned: the staged kernel wins at every block length measured
+        v = aligned ? ((max_blen <= kRegMaxBytes && max_blen >= kParkMinBytes) ? 2 : 1) : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
     if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
-    if (v == 6 && ((uintptr_t)arena & 3u)) v = 3;
+    if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
     if (v == 2 && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:

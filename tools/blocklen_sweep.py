@@ -16,6 +16,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 SEED = 0x1BADB002
+SHAPES_UNALIGNED = [  # files at odd offsets (every block unaligned): direct / long / unaligned staged
+    (1024, 1 << 20, 700, 2),
+    (1024, 1 << 20, 1024, 2),
+    (256, 4 << 20, 4096, 2),
+]
+VARIANTS_UNALIGNED = {0: "direct", 3: "long_deep_prefetch", 6: "staged_unaligned"}
 SHAPES = [  # (files, file bytes, block length, arenas)
     (1, 1 << 30, 131072, 2),      # one 1 GiB file, cfg5's block length
     (1024, 1 << 20, 1024, 2),     # 1 MiB files at the reference's own sizing (B = 1024)
@@ -27,6 +33,8 @@ DIAGS = {1: "diag_staged_memory_only", 2: "diag_staged_hash_only", 6: "diag_line
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--unaligned":
+        return unaligned()
     import torch
     import rsync_amd
     from rsync_amd import _lib
@@ -75,6 +83,51 @@ def main():
         _lib.check(_lib.lib.rsg_set_block_sums_diagnostic(0))
         print(json.dumps({"files": nf, "file_bytes": fb, "block_len": blen, "records": plan.total_records,
                           "variants": res}), flush=True)
+        plan.close()
+        for a in arenas:
+            a.free()
+        recs.free()
+
+
+def unaligned():
+    """Files placed at offsets f * (file bytes + 1): no block is 4-byte aligned
+    after the first file, so the batch takes the unaligned kernels."""
+    import time
+    import torch
+    import rsync_amd
+    from rsync_amd import _lib
+    eng = rsync_amd.Engine(0)
+    stream = torch.cuda.Stream()
+    sp = stream.cuda_stream
+    for nf, fb, blen, narena in SHAPES_UNALIGNED:
+        stride = fb + 1
+        total = nf * stride
+        arenas = [eng.alloc(total) for _ in range(narena)]
+        for k, a in enumerate(arenas):
+            for f in range(nf):
+                eng.fill_splitmix64(a, fb, 1 + f + 7919 * k, offset=f * stride, stream=sp)
+        plan = eng.plan([(f * stride, fb, blen) for f in range(nf)], total)
+        recs = eng.alloc(plan.total_records * rsync_amd.RECORD_BYTES)
+        eng.synchronize(sp)
+        w0 = time.perf_counter()
+        while time.perf_counter() - w0 < 0.3:
+            plan.run(arenas[0], SEED, recs, stream=sp)
+            eng.synchronize(sp)
+        res = {}
+        for v, name in VARIANTS_UNALIGNED.items():
+            _lib.check(_lib.lib.rsg_set_block_sums_kernel(v))
+            for i in range(10):
+                plan.run(arenas[i % narena], SEED, recs, stream=sp)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for i in range(30):
+                plan.run(arenas[i % narena], SEED, recs, stream=sp)
+            e1.record(stream)
+            eng.synchronize(sp)
+            ms = e0.elapsed_time(e1) / 30
+            res[name] = {"kernel_ms": round(ms, 4), "hbm_frac_8tbs": round((nf * fb + plan.total_records * 20) / (ms / 1e3) / 8e12, 4)}
+        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+        print(json.dumps({"files": nf, "file_bytes": fb, "block_len": blen, "unaligned": True, "variants": res}), flush=True)
         plan.close()
         for a in arenas:
             a.free()
