@@ -151,7 +151,7 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
  * any byte offset (pieces fetched from the 4-byte aligned address below the
  * block, funnel-shifted in registers; needs a 4-byte aligned arena, else 3).
  * Automatic: aligned batches take 2 when 512 <= the largest block <= 703
- * bytes, else 1; unaligned batches (a block not 4-byte aligned) take 6 (3
+ * bytes, 4 when it is 704..1536 bytes, else 1; unaligned batches (a block not 4-byte aligned) take 6 (3
  * for blocks >= 8 KiB, else 0, when the arena itself is not 4-byte aligned;
  * 1, 2, 4 and 5 fall back to 0 there).  The
  * environment variable RSG_BLOCKSUMS_KERNEL sets the initial value.  Returns

@@ -963,8 +963,15 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         return hipGetLastError();
     }
     int v = g_variant;
-    if (v == -1)  // unaligned: the staged kernel wins at every block length measured
-        v = aligned ? ((max_blen <= kRegMaxBytes && max_blen >= kParkMinBytes) ? 2 : 1) : 6;
+    // Aligned: park for 512..703-byte blocks, 128-byte segments up to 1536
+    // (B = 1024: 0.197-0.204 ms against 0.207-0.224 for 256-byte segments in
+    // three sweeps), 256-byte segments beyond (equal at 4 KiB, 12 % better at
+    // 128 KiB).  Unaligned: the staged kernel wins at every block length
+    // measured.
+    if (v == -1)
+        v = aligned ? ((max_blen <= kRegMaxBytes && max_blen >= kParkMinBytes) ? 2
+                                                                               : (max_blen > kRegMaxBytes && max_blen <= 1536 ? 4 : 1))
+                    : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
     if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
