@@ -225,7 +225,8 @@ def main():
         # The timed steps are over; the gather is reported beside them.  A
         # watchdog on every rank keeps a stuck collective from swallowing the
         # bench line: after 120 s rank 0 prints it without the gather and
-        # every rank exits.
+        # every rank exits with status 3, so a harness that checks the exit
+        # status still sees the failed collective.
         import threading
         gather_done = threading.Event()
 
@@ -233,7 +234,7 @@ def main():
             if not gather_done.wait(120.0):
                 if rank == 0:
                     print(json.dumps(bench_line(dict(extra, gather={"error": "timed out after 120 s"}))), flush=True)
-                os._exit(0)
+                os._exit(3)
         threading.Thread(target=watchdog, daemon=True).start()
         try:
             extra["gather"] = run_gather()

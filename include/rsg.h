@@ -163,10 +163,20 @@ rsg_status rsg_set_block_sums_kernel(int32_t variant);
  * product kernel and the "records" it writes are meaningless.  1 = staged
  * memory only, 2 = staged hashing only, 3 = park memory only, 4 = park
  * hashing only, 5 = linear read of the arena (plain loads), 6 = linear read
- * (LDS DMA); 5 and 6 run on arenas below 4 GiB only.  0 = off (default;
- * environment RSG_BLOCKSUMS_DIAG).  Kept apart from rsg_set_block_sums_kernel
- * so the product knob can never select a diagnostic. */
+ * (LDS DMA).  0 = off (default; environment RSG_BLOCKSUMS_DIAG).  Kept apart
+ * from rsg_set_block_sums_kernel so the product knob can never select a
+ * diagnostic. */
 rsg_status rsg_set_block_sums_diagnostic(int32_t diag);
+
+/* Fallback census of ctx's device since the last reset: counts[0] = full
+ * 64-block waves of the staged kernels (1, 4, 5, 6), counts[1] = full
+ * 64-block tiles of the park kernel (2), that could not be staged through
+ * LDS and were hashed with per-lane loads instead (a span past a 31-bit
+ * offset, reads that would run past the arena's end).  Records are identical
+ * either way; this tells a test or a bench that the fast path was taken.
+ * Waits for all work on the device.  reset != 0 zeroes the counters after
+ * reading them. */
+rsg_status rsg_block_sums_fallbacks(rsg_ctx *ctx, uint64_t counts[2], int32_t reset);
 
 /* One-shot device call: plan + launch + wait. */
 rsg_status rsg_block_sums_device(rsg_ctx *ctx, const void *d_arena, uint64_t arena_bytes,

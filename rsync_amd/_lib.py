@@ -104,6 +104,7 @@ _PROTOS = {
     "rsg_block_sums_planned": (_st, [_vp, _vp, _vp, _i32, _vp, _vp]),
     "rsg_set_block_sums_kernel": (_st, [_i32]),
     "rsg_set_block_sums_diagnostic": (_st, [_i32]),
+    "rsg_block_sums_fallbacks": (_st, [_vp, ctypes.POINTER(_u64), _i32]),
     "rsg_block_sums_device": (_st, [_vp, _vp, _u64, ctypes.POINTER(File), _u64, _i32, _vp, _u64]),
     "rsg_block_sums_host": (_st, [_vp, ctypes.POINTER(File), _u64, _i32, _vp, _u64]),
     "rsg_generate_files_fd": (_st, [_vp, ctypes.POINTER(FdFile), _u64, _i32, _i32, WRITE_FN, _vp,

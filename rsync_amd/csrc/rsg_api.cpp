@@ -431,6 +431,13 @@ rsg_status rsg_set_block_sums_diagnostic(int32_t diag) {
     return RSG_OK;
 }
 
+rsg_status rsg_block_sums_fallbacks(rsg_ctx *ctx, uint64_t counts[2], int32_t reset) {
+    RSG_ENTER(ctx);
+    if (!counts) return fail(ctx, RSG_ERR_INVALID, "counts is NULL");
+    RSG_HIP(ctx, rsg::read_block_sums_fallbacks(counts, reset != 0));
+    return RSG_OK;
+}
+
 rsg_status rsg_block_sums_device(rsg_ctx *ctx, const void *d_arena, uint64_t arena_bytes, const rsg_file *files,
                                  uint64_t nfiles, int32_t seed, void *d_records, uint64_t records_cap) {
     RSG_ENTER(ctx);

@@ -30,6 +30,15 @@ namespace rsg {
 
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
+// Fallback census (rsg_block_sums_fallbacks): [0] full 64-block waves of the
+// staged kernels, [1] full 64-block tiles of the park kernel that could not
+// take the LDS-DMA path and were hashed with per-lane loads.  The records are
+// the same either way, only speed differs, so this is how a test tells that
+// the fast path was really taken.  One atomic per fallback wave (vector
+// atomic from lane 0), nothing on the fast path.
+__device__ unsigned long long g_fallbacks[2];
+__device__ __forceinline__ void count_fallback(int k) { atomicAdd(&g_fallbacks[k], 1ull); }
+
 // 16 message words from a 4-byte-aligned address known to lie inside the arena.
 __device__ __forceinline__ void load16(const uint8_t *p, uint32_t w[16]) {
     const u32x4a4 *q = reinterpret_cast<const u32x4a4 *>(p);
@@ -378,17 +387,17 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     const uint32_t sh = UNAL ? (uint32_t)(off & 3u) : 0u;
     const uint64_t loff = off - sh;  // 4-byte aligned fetch start
     const uint32_t nseg = n ? (n >> 6) / kChunks + 1 : 0;  // segments through the tail chunk
-    const uint32_t S = __builtin_amdgcn_readfirstlane((uint32_t)wave_max_u64(nseg));
-    const uint64_t lo_v = wave_min_u64(n ? loff : ~0ull);
-    const uint64_t base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo_v >> 32)) << 32) |
-                          __builtin_amdgcn_readfirstlane((uint32_t)lo_v);
-    const uint64_t top = wave_max_u64(n ? loff + (uint64_t)kSegBytes * S + (UNAL ? 16u : 0u) : 0);
+    const uint32_t S = rfl32((uint32_t)wave_max_u64(nseg));
+    const uint64_t base = rfl64(wave_min_u64(n ? loff : ~0ull));
+    const uint64_t top = rfl64(wave_max_u64(n ? loff + (uint64_t)kSegBytes * S + (UNAL ? 16u : 0u) : 0));
     // Wave-uniform choice of path: the staged path needs all 64 blocks, every
     // DMA read inside the arena and the span addressable by a 31-bit buffer
     // offset.  Otherwise (last partial wave, a file ending at the arena's end,
     // giant spans) the lanes hash with per-lane loads.
-    const bool staged = (wave_first + 63 < total_blocks) && top <= arena_bytes && (top - base) <= 0x7FFFFFFFull;
+    const bool full = wave_first + 63 < total_blocks;
+    const bool staged = full && top <= arena_bytes && (top - base) <= 0x7FFFFFFFull;
     if (!staged) {
+        if (MODE == 0 && full && lane == 0) count_fallback(0);
         if (n == 0) return;
         uint32_t h[4];
         md4_init(h);
@@ -477,10 +486,8 @@ __global__ __launch_bounds__(256) void diag_linear_read(const uint8_t *__restric
     for (uint64_t base = (uint64_t)blockIdx.x * 256 * 64; base + 256 * 64 <= bytes; base += per_iter) {
         if (LDS) {
             const uint64_t wb = base + wave * 4096;
-            const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)(arena + ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(wb >> 32)) << 32 |
-                                  __builtin_amdgcn_readfirstlane((uint32_t)wb))),
-                (short)0, 0x7FFFFFFF, 0x00020000);
+            const __amdgpu_buffer_rsrc_t r =
+                __builtin_amdgcn_make_buffer_rsrc((void *)(arena + rfl64(wb)), (short)0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
             for (int i = 0; i < 4; i++)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -626,11 +633,9 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
             done = fe >= gend || f + i >= fmax;
         }
     }
-    d.base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo_off >> 32)) << 32) |
-             __builtin_amdgcn_readfirstlane((uint32_t)lo_off);
-    top = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(top >> 32)) << 32) |
-          __builtin_amdgcn_readfirstlane((uint32_t)top);
-    bmax = __builtin_amdgcn_readfirstlane(bmax);
+    d.base = rfl64(lo_off);
+    top = rfl64(top);
+    bmax = rfl32(bmax);
     d.staged = (g0 + 64 <= total_blocks) && bmax <= kRegMaxBytes && top <= arena_bytes &&
                top - d.base <= 0x7FFFFFFFull;
     d.off = off;
@@ -882,7 +887,10 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             }
             store_record(out, g, n, s1, tw, h);
         } else {
-            if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);
+            if (lane == 0) {
+                pk_store(&sh.freeq[slot], k + kPkSlots);
+                if (MODE == 0 && t * 64 + 64 <= total_blocks) count_fallback(1);
+            }
             if (g < total_blocks) pk_direct(arena, arena_bytes, files, wg_file, nwg256, g, seed, out);
         }
     }
@@ -891,10 +899,14 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
 
 // Kernel variants (rsg_set_block_sums_kernel; identical results, only speed
 // differs): -1 = automatic, 0 = direct per-lane loads, 1 = staged LDS-DMA
-// slabs, 2 = park (three loader waves + five hashers with register-parked
-// blocks, blocks <= 703 bytes), 3 = long blocks with deep per-lane prefetch.
-// Automatic: aligned batches take park when 512 <= max block <= 703, else
-// staged; unaligned batches take long when blocks are >= 8 KiB, else direct.
+// slabs (256-byte segments), 2 = park (three loader waves + five hashers with
+// register-parked blocks, blocks <= 703 bytes), 3 = long blocks with deep
+// per-lane prefetch, 4 / 5 = staged with 128- / 512-byte segments, 6 = staged
+// for blocks at any byte offset (funnel-shifted pieces).
+// Automatic (launch_block_sums below): aligned batches take park when
+// 512 <= max block <= 703, 4 when the max block is 704..1536, else 1;
+// unaligned batches take 6 (3 for blocks >= 8 KiB, else 0, when the arena
+// itself is not 4-byte aligned).
 //
 // Timing diagnostics (rsg_set_block_sums_diagnostic, a separate knob so the
 // product knob can never select one; their "records" are meaningless):
@@ -950,12 +962,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                                        files, wg_file, nwg, total_blocks, seed, out);
                 break;
             case 5:
-                if (arena_bytes >= (4ull << 30)) break;  // the read ceilings are measured on <= 4 GiB arenas
                 hipLaunchKernelGGL(diag_linear_read<false>, dim3(2048), dim3(256), 0, stream, arena, arena_bytes,
                                    (uint32_t *)out);
                 break;
             case 6:
-                if (arena_bytes >= (4ull << 30)) break;  // faulted on a 32 GiB arena (r02e sweep); diagnostic only
                 hipLaunchKernelGGL(diag_linear_read<true>, dim3(2048), dim3(256), 0, stream, arena, arena_bytes,
                                    (uint32_t *)out);
                 break;
@@ -1035,6 +1045,19 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
 
 void set_block_sums_variant(int v) { g_variant = v; }
 void set_block_sums_diagnostic(int d) { g_diag = d; }
+
+hipError_t read_block_sums_fallbacks(uint64_t out[2], bool reset) {
+    unsigned long long v[2] = {0, 0};
+    hipError_t e = hipDeviceSynchronize();  // the counters are bumped on any of the context's streams
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_fallbacks), sizeof v, 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && reset) {
+        const unsigned long long z[2] = {0, 0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_fallbacks), z, sizeof z, 0, hipMemcpyHostToDevice);
+    }
+    out[0] = v[0];
+    out[1] = v[1];
+    return e;
+}
 
 // ------------------------------------------------------------------ synthetic data
 __global__ void fill_splitmix64_kernel(uint8_t *dst, uint64_t n, uint64_t seed) {

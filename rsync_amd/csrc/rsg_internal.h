@@ -31,10 +31,14 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
 // Device scratch a block-sum launch needs: 4 + 4 * ceil(total_blocks / 64) bytes.
 inline uint64_t block_sums_scratch_bytes(uint64_t total_blocks) { return 8 + 4 * ((total_blocks + 63) / 64); }
 
-// Product variants (-1 auto, 0 direct, 1 staged, 2 park, 3 long) and timing
-// diagnostics (0 off, 1..5; outputs meaningless), rsg_blocksums.hip.
+// Product variants (-1 auto, 0 direct, 1 staged, 2 park, 3 long, 4/5 staged
+// with 128/512-byte segments, 6 staged at any byte offset) and timing
+// diagnostics (0 off, 1..6; outputs meaningless), rsg_blocksums.hip.
 void set_block_sums_variant(int v);
 void set_block_sums_diagnostic(int d);
+// Fallback census of the current device: [0] staged waves, [1] park tiles
+// (full ones that took per-lane loads); synchronises the device.
+hipError_t read_block_sums_fallbacks(uint64_t out[2], bool reset);
 
 // ---- sender search (rsg_match_kernels.hip)
 constexpr uint32_t kScanTile = 32768;                          // source bytes per tile

@@ -586,7 +586,11 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
             first_err = msg;
         }
     }
-    for (int k = 0; k < 2; k++) (void)hipStreamSynchronize(ctx->side[k]);  // nothing outlives the call
+    // nothing outlives the call: a fatal error inside a hook can return
+    // before a job's confirmation (ctx->confirm, then its D2H into
+    // ctx->h_out[0]) has been waited for
+    for (int k = 0; k < 2; k++) (void)hipStreamSynchronize(ctx->side[k]);
+    (void)hipStreamSynchronize(ctx->confirm);
     (void)hipStreamSynchronize(ctx->stream);
     if (first != RSG_OK) ctx->err = first_err;
     return first;

@@ -14,6 +14,17 @@
 
 namespace rsg {
 
+// Wave-uniform copies in SGPRs.  __builtin_amdgcn_readfirstlane returns int:
+// widening that to 64 bits directly sign-extends the low word, so every
+// 64-bit value is rebuilt from two uint32_t halves (an offset with bit 31 set
+// otherwise came back with its upper word all ones).
+__device__ __forceinline__ uint32_t rfl32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+    return ((uint64_t)rfl32((uint32_t)(v >> 32)) << 32) | (uint64_t)rfl32((uint32_t)v);
+}
+
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) {
     return __builtin_amdgcn_alignbit(x, x, 32 - s);
 }

@@ -210,6 +210,14 @@ class Engine:
     def plan(self, files: Sequence[Tuple[int, int, int]], arena_bytes: int) -> Plan:
         return Plan(self, files, arena_bytes)
 
+    def block_sums_fallbacks(self, reset: bool = True) -> Tuple[int, int]:
+        """Fallback census (rsg_block_sums_fallbacks): (staged waves, park
+        tiles) of full 64-block groups hashed with per-lane loads instead of
+        the LDS-DMA path since the last reset.  Waits for the device."""
+        c = (ctypes.c_uint64 * 2)()
+        check(lib.rsg_block_sums_fallbacks(self.ctx, c, int(reset)), self.ctx)
+        return int(c[0]), int(c[1])
+
     # ------------------------------------------------------------ receiver
     def block_sums(self, files: Sequence, seed: int, block_len=0):
         """Block sums of host buffers (the PCIe-inclusive path).

@@ -1,0 +1,202 @@
+/*
+ * abi_conformance.c -- C-language conformance program for include/rsg.h.
+ *
+ * A cgo binding (go/rsyncgpu) sees the structs of rsg.h with
+ * the C compiler's layout, so this program pins that layout for every struct
+ * a caller fills or reads -- rsg_sum_head, rsg_file, rsg_match,
+ * rsg_search_job, rsg_fd_file -- at compile time (_Static_assert) and prints
+ * it as JSON for tests/test_c_abi.py to compare with the ctypes mirror.
+ *
+ * Modes:
+ *   abi_conformance layout        sizes/offsets as JSON (no GPU needed)
+ *   abi_conformance nodev         the no-GPU contract: rsg_ctx_create fails
+ *                                 with RSG_ERR_NODEV and a message (CPU box)
+ *   abi_conformance gpu <out>     one block-sum -> rsg_encode_sums ->
+ *                                 rsg_decode_sums round trip through the
+ *                                 library (receiver generateAndSendSums,
+ *                                 generator.go:325-350, then the sender's
+ *                                 receiveSums, sender.go:118-151); the records
+ *                                 go to <out> for the test to check against
+ *                                 the oracle.
+ * Built by __graft_entry__.build() with gcc against include/rsg.h and
+ * rsync_amd/librsg.so (test infrastructure, not part of the product).
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "rsg.h"
+
+#define PIN(T, F, OFF) _Static_assert(offsetof(T, F) == (OFF), #T "." #F " offset")
+#define SIZE(T, N) _Static_assert(sizeof(T) == (N), #T " size")
+
+/* SumHead wire order (types.go:79-86) */
+SIZE(rsg_sum_head, 16);
+PIN(rsg_sum_head, count, 0);
+PIN(rsg_sum_head, block_len, 4);
+PIN(rsg_sum_head, s2len, 8);
+PIN(rsg_sum_head, rem, 12);
+SIZE(rsg_file, 32);
+PIN(rsg_file, data, 0);
+PIN(rsg_file, offset, 8);
+PIN(rsg_file, len, 16);
+PIN(rsg_file, block_len, 24);
+PIN(rsg_file, reserved, 28);
+SIZE(rsg_match, 16);
+PIN(rsg_match, offset, 0);
+PIN(rsg_match, index, 8);
+PIN(rsg_match, reserved, 12);
+SIZE(rsg_search_job, 88);
+PIN(rsg_search_job, src, 0);
+PIN(rsg_search_job, src_len, 8);
+PIN(rsg_search_job, head, 16);
+PIN(rsg_search_job, sum1, 32);
+PIN(rsg_search_job, sum2, 40);
+PIN(rsg_search_job, targets, 48);
+PIN(rsg_search_job, matches, 56);
+PIN(rsg_search_job, match_cap, 64);
+PIN(rsg_search_job, n_matches, 72);
+PIN(rsg_search_job, status, 80);
+PIN(rsg_search_job, reserved, 84);
+SIZE(rsg_fd_file, 32);
+PIN(rsg_fd_file, fd, 0);
+PIN(rsg_fd_file, idx, 4);
+PIN(rsg_fd_file, offset, 8);
+PIN(rsg_fd_file, len, 16);
+PIN(rsg_fd_file, block_len, 24);
+PIN(rsg_fd_file, reserved, 28);
+
+#define F(T, M) printf("\"%s\": [%zu, %zu]", #M, offsetof(T, M), sizeof(((T *)0)->M))
+
+static void layout(void) {
+    printf("{\"abi_version\": %d, \"record_bytes\": %d, \"chunk_size\": %d, \"max_block_len\": %d,\n",
+           RSG_ABI_VERSION, RSG_RECORD_BYTES, RSG_CHUNK_SIZE, RSG_MAX_BLOCK_LEN);
+    printf(" \"rsg_sum_head\": {\"size\": %zu, ", sizeof(rsg_sum_head));
+    F(rsg_sum_head, count); printf(", "); F(rsg_sum_head, block_len); printf(", ");
+    F(rsg_sum_head, s2len); printf(", "); F(rsg_sum_head, rem); printf("},\n");
+    printf(" \"rsg_file\": {\"size\": %zu, ", sizeof(rsg_file));
+    F(rsg_file, data); printf(", "); F(rsg_file, offset); printf(", "); F(rsg_file, len); printf(", ");
+    F(rsg_file, block_len); printf(", "); F(rsg_file, reserved); printf("},\n");
+    printf(" \"rsg_match\": {\"size\": %zu, ", sizeof(rsg_match));
+    F(rsg_match, offset); printf(", "); F(rsg_match, index); printf(", "); F(rsg_match, reserved); printf("},\n");
+    printf(" \"rsg_search_job\": {\"size\": %zu, ", sizeof(rsg_search_job));
+    F(rsg_search_job, src); printf(", "); F(rsg_search_job, src_len); printf(", "); F(rsg_search_job, head);
+    printf(", "); F(rsg_search_job, sum1); printf(", "); F(rsg_search_job, sum2); printf(", ");
+    F(rsg_search_job, targets); printf(", "); F(rsg_search_job, matches); printf(", ");
+    F(rsg_search_job, match_cap); printf(", "); F(rsg_search_job, n_matches); printf(", ");
+    F(rsg_search_job, status); printf(", "); F(rsg_search_job, reserved); printf("},\n");
+    printf(" \"rsg_fd_file\": {\"size\": %zu, ", sizeof(rsg_fd_file));
+    F(rsg_fd_file, fd); printf(", "); F(rsg_fd_file, idx); printf(", "); F(rsg_fd_file, offset); printf(", ");
+    F(rsg_fd_file, len); printf(", "); F(rsg_fd_file, block_len); printf(", "); F(rsg_fd_file, reserved);
+    printf("}}\n");
+}
+
+static int nodev(void) {
+    rsg_ctx *ctx = (rsg_ctx *)1;
+    rsg_status st = rsg_ctx_create(0, &ctx);
+    const char *msg = rsg_last_error(NULL);
+    printf("{\"status\": %d, \"ctx_null\": %d, \"message\": \"%s\", \"device_count\": %d}\n", (int)st,
+           ctx == NULL, msg ? msg : "", (int)rsg_device_count());
+    if (st != RSG_ERR_NODEV || ctx != NULL || !msg || !msg[0]) return 1;
+    /* pure host arithmetic works without a device: SumSizesSqroot of 1 MiB */
+    rsg_sum_head h;
+    if (rsg_sum_head_for(1 << 20, 0, &h) != RSG_OK || h.count != 1024 || h.block_len != 1024 || h.s2len != 16 ||
+        h.rem != 0)
+        return 2;
+    /* and bad input is an error status, never an abort */
+    if (rsg_sum_head_for(-1, 0, &h) != RSG_ERR_INVALID) return 3;
+    return 0;
+}
+
+/* splitmix64 byte stream */
+static void splitmix64_bytes(uint64_t seed, uint8_t *dst, size_t n) {
+    uint64_t st = seed;
+    for (size_t i = 0; i < n; i += 8) {
+        st += 0x9E3779B97F4A7C15ULL;
+        uint64_t z = st;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        z ^= z >> 31;
+        for (size_t b = 0; b < 8 && i + b < n; b++) dst[i + b] = (uint8_t)(z >> (8 * b));
+    }
+}
+
+#define CHECK(x)                                                                       \
+    do {                                                                               \
+        rsg_status s_ = (x);                                                           \
+        if (s_ != RSG_OK) {                                                            \
+            fprintf(stderr, "%s:%d %s -> %d: %s\n", __FILE__, __LINE__, #x, (int)s_,  \
+                    rsg_last_error(ctx));                                              \
+            return 10;                                                                 \
+        }                                                                              \
+    } while (0)
+
+static int gpu(const char *out_path) {
+    rsg_ctx *ctx = NULL;
+    CHECK(rsg_ctx_create(0, &ctx));
+    const uint64_t lens[3] = {1u << 20, 1000, 0};
+    const int32_t blens[3] = {700, 0, 700};
+    uint8_t *data[3];
+    rsg_file files[3];
+    memset(files, 0, sizeof files);
+    for (int i = 0; i < 3; i++) {
+        data[i] = (uint8_t *)malloc(lens[i] + 1);
+        splitmix64_bytes((uint64_t)i + 1, data[i], lens[i]);
+        files[i].data = data[i];
+        files[i].len = lens[i];
+        files[i].block_len = blens[i];
+    }
+    rsg_sum_head heads[3];
+    uint64_t first[3], total = 0;
+    CHECK(rsg_plan_block_sums(files, 3, heads, first, &total));
+    uint8_t *rec = (uint8_t *)malloc(total * RSG_RECORD_BYTES + 1);
+    const int32_t seed = 0x1BADB002;
+    CHECK(rsg_block_sums_host(ctx, files, 3, seed, rec, total));
+    /* the generator's stream, then the sender's parse of file 0 */
+    const int32_t idx[3] = {0, 1, 2};
+    uint64_t slen = 0;
+    CHECK(rsg_encode_sums(idx, heads, 3, rec, 1, NULL, 0, &slen));
+    uint8_t *stream = (uint8_t *)malloc(slen);
+    CHECK(rsg_encode_sums(idx, heads, 3, rec, 1, stream, slen, &slen));
+    rsg_sum_head h;
+    uint32_t *sum1 = (uint32_t *)malloc(4u * (size_t)heads[0].count);
+    uint8_t *sum2 = (uint8_t *)malloc(16u * (size_t)heads[0].count);
+    uint64_t used = 0;
+    CHECK(rsg_decode_sums(stream + 4, slen - 4, &h, sum1, sum2, (uint64_t)heads[0].count, &used));
+    int bad = memcmp(&h, &heads[0], sizeof h) != 0 || used != 16 + (uint64_t)h.count * 20;
+    for (int32_t b = 0; b < h.count && !bad; b++) {
+        uint32_t r1;
+        memcpy(&r1, rec + (size_t)b * 20, 4);
+        bad = r1 != sum1[b] || memcmp(rec + (size_t)b * 20 + 4, sum2 + 16 * (size_t)b, 16) != 0;
+    }
+    /* phase markers at the stream's end (generator.go:31,40) */
+    int32_t m1, m2;
+    memcpy(&m1, stream + slen - 8, 4);
+    memcpy(&m2, stream + slen - 4, 4);
+    bad |= m1 != -1 || m2 != -1;
+    FILE *f = fopen(out_path, "wb");
+    if (!f || fwrite(rec, 20, total, f) != total) return 11;
+    fclose(f);
+    printf("{\"records\": %llu, \"stream_bytes\": %llu, \"round_trip_ok\": %d}\n", (unsigned long long)total,
+           (unsigned long long)slen, !bad);
+    rsg_ctx_destroy(ctx);
+    for (int i = 0; i < 3; i++) free(data[i]);
+    free(rec);
+    free(stream);
+    free(sum1);
+    free(sum2);
+    return bad ? 12 : 0;
+}
+
+int main(int argc, char **argv) {
+    if (argc >= 2 && strcmp(argv[1], "layout") == 0) {
+        layout();
+        return 0;
+    }
+    if (argc >= 2 && strcmp(argv[1], "nodev") == 0) return nodev();
+    if (argc >= 3 && strcmp(argv[1], "gpu") == 0) return gpu(argv[2]);
+    fprintf(stderr, "usage: %s layout | nodev | gpu <records-out>\n", argv[0]);
+    return 2;
+}

@@ -202,13 +202,14 @@ def test_kernel_variants_match(eng, variant, blen):
 
 
 @pytest.mark.parametrize("variant", [-1, 3, 6])
-@pytest.mark.parametrize("blen", [32768, 8192, 131072])
+@pytest.mark.parametrize("blen", [700, 32768, 8192, 131072])
 def test_unaligned_windows(eng, variant, blen):
     """The sender's confirmation shape: windows of one block each at random
     byte offsets of a source (plus windows cut short by the source's end and
     one ending exactly there), enough for full 64-window waves of the
-    unaligned staged kernel (variant 6, the automatic choice for unaligned
-    blocks >= 8 KiB) and of the deep-prefetch kernel (3)."""
+    unaligned staged kernel (variant 6, the automatic choice for every
+    unaligned batch in a 4-byte aligned arena) and of the deep-prefetch
+    kernel (3)."""
     from rsync_amd import _lib
     size = 24 << 20
     src = cases.splitmix64_bytes(777, size)
@@ -248,12 +249,14 @@ def test_variants_long_blocks_full_waves(eng, variant):
     assert got == want
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 5, 6])
 def test_variants_device_aligned_arena(eng, variant):
     """Aligned device arena (the staged / park fast paths), files straddling
     waves and tiles, a file ending exactly at the arena end (park's direct
     tiles), blocks of 700/64/703 bytes (64: park with tiny blocks, ragged
-    tails hashed by the predicated path)."""
+    tails hashed by the predicated path) and the automatic choice's
+    boundaries (-1: 703 park, 704..1536 128-byte segments, 1537 and up
+    256-byte segments)."""
     from rsync_amd import _lib
     lens = [1 << 20, 700 * 64 * 3 + 5, 12344, 64, 4, 0, 300_000, 70_000 * 3]
     offs, o = [], 0
@@ -269,7 +272,7 @@ def test_variants_device_aligned_arena(eng, variant):
         datas.append(d)
     arena = eng.alloc(arena_bytes)
     arena.upload(host)
-    for blen in (700, 64, 703, 4096):
+    for blen in (700, 64, 703, 704, 1024, 1536, 1537, 4096):
         want = b"".join(orc.block_sums(d, blen, cases.SEED) for d in datas)
         try:
             _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))

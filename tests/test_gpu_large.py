@@ -1,0 +1,245 @@
+"""GPU parity on multi-GiB arenas: file offsets and block offsets past 2 GiB
+and 4 GiB, cfg4's full 100 000-file set and cfg5's 32 GiB file.
+
+The reference takes int64 lengths and offsets everywhere
+(internal/receiver/generator.go:325 `fileLen int64`, rsynccommon.go:14,
+rsyncwire/wire.go:144 WriteInt64 past 2 GiB), so the kernels must give the
+same records wherever a block sits in the arena -- and, since the records are
+identical either way, the fallback census (rsg_block_sums_fallbacks) shows
+that the LDS-DMA fast path was taken for every full wave / tile instead of
+the per-lane fallback (the round-2 readfirstlane sign-extension bug sent
+every wave with bit 31 of its offset set to the fallback).
+
+Arenas are filled on the device with ONE splitmix64 stream, so any window of
+them is regenerated on the host with cases.splitmix64_range; the oracle
+checks every record of the small files near the 2/4 GiB boundaries and
+sampled block ranges of the big files.
+"""
+import numpy as np
+import pytest
+
+import cases
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+GIB = 1 << 30
+STREAM_SEED = 0xC0FFEE
+PAD = 1 << 20  # bytes after the last file: no wave reads past the arena, so no fallback is legitimate
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import rsync_amd
+    e = rsync_amd.Engine(0)
+    yield e
+    e.close()
+
+
+def _layout(unaligned: bool):
+    """Files tiling [0, ~5 GiB): a big file up to 2 GiB - 8 MiB, ~16 MiB of
+    4-64 KiB files across 2 GiB (irregular park tiles, waves straddling many
+    files), a big file up to 4 GiB - 8 MiB, small files across 4 GiB, a big
+    file of 1 GiB past it.  -> ([(offset, len)], kinds, arena_bytes)."""
+    rng = np.random.default_rng(31)
+    files, kinds, at = [], [], 0
+
+    def add(n, kind):
+        nonlocal at
+        off = at
+        if unaligned:  # odd offsets; the length shrinks so files never overlap
+            sh = 1 + len(files) % 3
+            files.append((off + sh, n - sh))
+        else:
+            files.append((off, n))
+        kinds.append(kind)
+        at = (off + n + 15) & ~15
+
+    add(2 * GIB - (8 << 20) - 777, "big")
+    while at < 2 * GIB + (8 << 20):
+        add(int(rng.integers(4096, 65537)), "small")
+    add(4 * GIB - (8 << 20) - at - 333, "big")
+    while at < 4 * GIB + (8 << 20):
+        add(int(rng.integers(4096, 65537)), "small")
+    add(GIB + 12345, "big")
+    return files, kinds, at + PAD
+
+
+_ARENAS = {}
+
+
+def _arena(eng, unaligned):
+    """One device arena per layout for the whole module (5 GiB each)."""
+    if unaligned not in _ARENAS:
+        files, kinds, nbytes = _layout(unaligned)
+        a = eng.alloc(nbytes)
+        eng.fill_splitmix64(a, nbytes, STREAM_SEED)
+        eng.synchronize()
+        _ARENAS[unaligned] = (a, files, kinds)
+    return _ARENAS[unaligned]
+
+
+def _ranges(files, kinds, B, rng):
+    """(file, b0, b1) block ranges to check: every block of the small files,
+    and of each big file its first and last 64 blocks, 64 blocks around each
+    of 2 GiB and 4 GiB when inside it, and 16 random blocks."""
+    out = []
+    for i, ((off, n), kind) in enumerate(zip(files, kinds)):
+        nb = (n + B - 1) // B
+        if kind == "small":
+            out.append((i, 0, nb))
+            continue
+        out += [(i, 0, min(64, nb)), (i, max(0, nb - 64), nb)]
+        for x in (2 * GIB, 4 * GIB):
+            if off <= x < off + n:
+                b = (x - off) // B
+                out.append((i, max(0, b - 32), min(nb, b + 32)))
+        out += [(i, int(b), int(b) + 1) for b in rng.integers(0, nb, 16)]
+    return out
+
+
+def _check(files, kinds, B, seed, rec, first):
+    rng = np.random.default_rng(B)
+    bad = []
+    for i, b0, b1 in _ranges(files, kinds, B, rng):
+        off, n = files[i]
+        lo, hi = b0 * B, min(b1 * B, n)
+        win = cases.splitmix64_range(STREAM_SEED, off + lo, hi - lo)
+        want = orc.block_sums(win, B, seed)
+        got = rec[(first[i] + b0) * 20:(first[i] + b1) * 20].tobytes()
+        if got != want:
+            bad.append((i, off, b0, b1))
+    return bad
+
+
+def _run(eng, unaligned, variant, B, seed=cases.SEED):
+    from rsync_amd import _lib
+    arena, files, kinds = _arena(eng, unaligned)
+    desc = [(o, n, B) for o, n in files]
+    plan = eng.plan(desc, arena.nbytes)
+    recs = eng.alloc(plan.total_records * 20)
+    eng.block_sums_fallbacks(reset=True)
+    try:
+        _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))
+        plan.run(arena, seed, recs)
+        eng.synchronize()
+    finally:
+        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+    fb = eng.block_sums_fallbacks(reset=True)
+    rec = recs.download(plan.total_records * 20)
+    recs.free()
+    first = plan.first_record
+    plan.close()
+    return files, kinds, rec, first, fb
+
+
+@pytest.mark.parametrize("variant,B", [(-1, 700), (2, 700), (1, 700), (4, 700), (4, 1024), (1, 131072),
+                                       (-1, 131072), (5, 4096)])
+def test_aligned_arena_past_4gib(eng, variant, B):
+    """Aligned batch on a 5 GiB arena: park (regular and irregular tiles) and
+    the staged kernels, every checked record equal to the oracle's and not one
+    full wave or tile on the per-lane fallback."""
+    files, kinds, rec, first, fb = _run(eng, False, variant, B)
+    assert _check(files, kinds, B, cases.SEED, rec, first) == []
+    assert fb == (0, 0), fb
+
+
+@pytest.mark.parametrize("variant,B", [(-1, 700), (6, 700), (6, 32768), (6, 131072)])
+def test_unaligned_arena_past_4gib(eng, variant, B):
+    """The same arena with every file at an odd offset (the unaligned staged
+    kernel: pieces from the 4-byte aligned address below each block)."""
+    files, kinds, rec, first, fb = _run(eng, True, variant, B, seed=-1)
+    assert _check(files, kinds, B, -1, rec, first) == []
+    assert fb == (0, 0), fb
+
+
+def test_cfg4_full_set(eng):
+    """BASELINE cfg4 at its real size: 100 000 files of uniform length in
+    [4096, 65536] (PRNG seed 4, the bench's set), 3.48 GB arena at B = 700,
+    automatic kernel (park; nearly every tile spans files).  256 random files
+    plus the first and last against the oracle; no full tile on the fallback."""
+    NF = 100_000
+    lengths = np.random.default_rng(4).integers(4096, 65537, NF).tolist()
+    offs, at = [], 0
+    for n in lengths:
+        offs.append(at)
+        at += (n + 15) & ~15
+    arena = eng.alloc(at + PAD)
+    for f in range(NF):
+        eng.fill_splitmix64(arena, lengths[f], f + 1, offset=offs[f])
+    plan = eng.plan([(o, n, 700) for o, n in zip(offs, lengths)], arena.nbytes)
+    recs = eng.alloc(plan.total_records * 20)
+    eng.synchronize()
+    eng.block_sums_fallbacks(reset=True)
+    plan.run(arena, cases.SEED, recs)
+    eng.synchronize()
+    fb = eng.block_sums_fallbacks(reset=True)
+    assert plan.total_records == sum((n + 699) // 700 for n in lengths)
+    rng = np.random.default_rng(44)
+    picks = sorted(set(rng.integers(0, NF, 256).tolist()) | {0, NF - 1})
+    for f in picks:
+        cnt = (lengths[f] + 699) // 700
+        got = recs.download(cnt * 20, offset=plan.first_record[f] * 20).tobytes()
+        assert got == orc.block_sums(cases.splitmix64_bytes(f + 1, lengths[f]), 700, cases.SEED), f
+    assert fb == (0, 0), fb
+    arena.free()
+    recs.free()
+    plan.close()
+
+
+def test_cfg5_32gib_file(eng):
+    """BASELINE cfg5's per-GPU share at its real size: one 32 GiB file at
+    B = 128 KiB (262 144 blocks of 2049 compressions).  Sampled blocks (48
+    random, the blocks at every 2^31-byte boundary, the last) against the
+    oracle; no full wave on the fallback."""
+    size, B = 32 << 30, 131072
+    arena = eng.alloc(size + PAD)
+    eng.fill_splitmix64(arena, size, 5000)
+    plan = eng.plan([(0, size, B)], arena.nbytes)
+    nrec = plan.total_records
+    assert nrec == size // B
+    recs = eng.alloc(nrec * 20)
+    eng.synchronize()
+    eng.block_sums_fallbacks(reset=True)
+    plan.run(arena, cases.SEED, recs)
+    eng.synchronize()
+    fb = eng.block_sums_fallbacks(reset=True)
+    got = recs.download(nrec * 20).reshape(-1, 20)
+    rng = np.random.default_rng(5)
+    picks = set(rng.integers(0, nrec, 48).tolist()) | {nrec - 1}
+    picks |= {(k << 31) // B for k in range(1, 16)} | {((k << 31) // B) - 1 for k in range(1, 17)}
+    for b in sorted(picks):
+        blk = cases.splitmix64_range(5000, b * B, B)
+        assert got[b].tobytes() == orc.block_sums(blk, B, cases.SEED), b
+    assert fb == (0, 0), fb
+    arena.free()
+    recs.free()
+    plan.close()
+
+
+@pytest.mark.parametrize("variant,kind", [(1, 0), (2, 1)])
+def test_fallback_census_counts(eng, variant, kind):
+    """The census is live: a file that ends exactly at the arena's end makes
+    the last full wave (staged) / tile (park) read past the arena, so it must
+    take the per-lane path -- and be counted -- with the records unchanged."""
+    from rsync_amd import _lib
+    n = 700 * 64 * 8
+    d = cases.splitmix64_bytes(71, n)
+    arena = eng.alloc(n)
+    arena.upload(d)
+    eng.block_sums_fallbacks(reset=True)
+    try:
+        _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))
+        recs, total = eng.block_sums_device(arena, [(0, n, 700)], cases.SEED)
+    finally:
+        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+    fb = eng.block_sums_fallbacks(reset=True)
+    assert recs.download(total * 20).tobytes() == orc.block_sums(d, 700, cases.SEED)
+    assert fb[kind] >= 1 and fb[1 - kind] == 0, fb
+
+
+def test_release_arenas(eng):
+    """Frees the module's 5 GiB arenas (runs last in this file)."""
+    for a, _, _ in _ARENAS.values():
+        a.free()
+    _ARENAS.clear()
