@@ -49,10 +49,15 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--no-delivery", action="store_true", help="skip the pipelined gather / D2H delivery modes")
     ap.add_argument("--ab", action="store_true", help="A/B the block-sum kernel variants (interleaved rounds)")
     ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5", "filesums"],
                     help="cfg2 = receiver block sums (the metric); cfg3 = sender match, reported separately")
     ap.add_argument("--cfg3-files", type=int, default=10)
+    ap.add_argument("--batches", type=int, default=4,
+                    help="batches per rank for the pipelined delivery modes (records of batch b move while "
+                         "batch b+1 is hashed)")
+    ap.add_argument("--delivery-steps", type=int, default=20, help="timed steps of each delivery mode")
     return ap.parse_args()
 
 
@@ -66,9 +71,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")  # control plane only; data moves over RCCL
-    # one rank per GPU; on a box with fewer GPUs than ranks (a 1-GPU rehearsal
-    # of the multi-rank path) ranks share devices round-robin
-    local = local % max(1, torch.cuda.device_count())
+    # one rank per GPU: RCCL refuses two ranks on one device, so a launch with
+    # more ranks than visible GPUs stops here with a clear message
+    ndev = torch.cuda.device_count()
+    if world > ndev or local >= ndev:
+        if rank == 0:
+            print(json.dumps({"metric": "GiB/s block-checksummed (weak+MD4), device-resident, at 1/2/4/8 MI355X",
+                              "value": None, "n_gpus": world,
+                              "error": f"{world} ranks but {ndev} visible GPU(s): one rank per GPU is required "
+                                       f"(RCCL cannot put two ranks on one device)"}), flush=True)
+        sys.exit(2)
     torch.cuda.set_device(local)
     import rsync_amd
     if args.workload == "cfg3":
@@ -197,50 +209,26 @@ def main():
         line.update(more)
         return line
 
-    # ---- RCCL gather of every rank's records to rank 0 (the one exchange step)
-    def run_gather():
-        uid = [rsync_amd.Engine.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        eng.comm_init(world, rank, uid[0])
-        sizes = [int(out_bytes)] * world
-        recv = eng.alloc(sum(sizes)) if rank == 0 else None
-        eng.gather_bytes(recs, sizes, recv, 0, stream=sptr)
-        eng.synchronize(sptr)
-        dist.barrier()
-        g0 = time.perf_counter()
-        reps = 10
-        for _ in range(reps):
-            eng.gather_bytes(recs, sizes, recv, 0, stream=sptr)
-        eng.synchronize(sptr)
-        dist.barrier()
-        gather_ms = (time.perf_counter() - g0) * 1e3 / reps
-        gt = torch.tensor([gather_ms], dtype=torch.float64)
-        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
-        gather_ms = float(gt[0])
-        step_ms = wall * 1e3 / args.steps
-        return {"bytes_to_root": int(out_bytes) * (world - 1), "ms": round(gather_ms, 4),
-                "kernel_plus_gather_gib_s": round(world * in_bytes / ((step_ms + gather_ms) * 1e-3) / GIB, 2)}
-
-    if world > 1:
-        # The timed steps are over; the gather is reported beside them.  A
-        # watchdog on every rank keeps a stuck collective from swallowing the
-        # bench line: after 120 s rank 0 prints it without the gather and
-        # every rank exits with status 3, so a harness that checks the exit
-        # status still sees the failed collective.
-        import threading
-        gather_done = threading.Event()
-
-        def watchdog():
-            if not gather_done.wait(120.0):
-                if rank == 0:
-                    print(json.dumps(bench_line(dict(extra, gather={"error": "timed out after 120 s"}))), flush=True)
-                os._exit(3)
-        threading.Thread(target=watchdog, daemon=True).start()
-        try:
-            extra["gather"] = run_gather()
-        except Exception as e:  # reported, never fatal to the bench line
-            extra["gather"] = {"error": str(e)[:300]}
-        gather_done.set()
+    # ---- delivery of the records (the one exchange step), pipelined with the
+    # hashing: RCCL gather to rank 0, and every rank's own D2H
+    if not args.no_delivery:
+        from rsync_amd.dist import ShardedBlockSums
+        nb = max(1, args.batches)
+        per = -(-n // nb)
+        groups = [list(range(g * per, min(n, (g + 1) * per))) for g in range(nb)]
+        groups = [g for g in groups if g]
+        recs_per_file = plan.total_records // n
+        descs = [[(f * FILE_BYTES, FILE_BYTES, BLOCK_LEN) for f in g] for g in groups]
+        rec_off = [g[0] * recs_per_file for g in groups]
+        send = [[len(g) * recs_per_file * rsync_amd.RECORD_BYTES] * world for g in groups]
+        recv_off = [[(q * plan.total_records + g[0] * recs_per_file) * rsync_amd.RECORD_BYTES for q in range(world)]
+                    for g in groups]
+        sb = ShardedBlockSums(eng, descs, arena_bytes, rec_off, send, recv_off)
+        extra["delivery"] = guarded_delivery(args, eng, sb, arenas, recs, world, rank, world * in_bytes,
+                                             world * plan.total_records,
+                                             lambda d: print(json.dumps(bench_line(dict(extra, delivery=d))),
+                                                             flush=True))
+        sb.close()
 
     # ---- PCIe-inclusive host path (rank 0, N = 1): host buffers in, records out
     if rank == 0 and world == 1 and not args.no_host_path:
@@ -364,6 +352,84 @@ def main():
         dist.destroy_process_group()
 
 
+def max_over_ranks(world, *vals):
+    if world == 1:
+        return vals
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(list(vals), dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return tuple(float(x) for x in t)
+
+
+def measure_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, records_all):
+    """The generator step with its records delivered, pipelined per batch
+    (rsg_block_sums_gather / rsg_block_sums_d2h): kernel of batch b+1 while
+    batch b's records move.  Each timed step hashes the rank's whole share
+    and delivers it; rates are all ranks' input bytes / the max-over-ranks
+    wall time.  -> dict for the bench line."""
+    import rsync_amd
+    out = {"batches": sb.nbatch}
+    steps = max(2, args.delivery_steps)
+
+    def timed(fn):
+        for i in range(2):
+            fn(i)
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            fn(i)
+        (dt,) = max_over_ranks(world, time.perf_counter() - t0)
+        return {"ms_per_step": round(dt * 1e3 / steps, 4), "gib_s": round(bytes_all * steps / dt / GIB, 2)}
+
+    # every rank copies its own records to pinned host memory over its own PCIe link
+    host = eng.alloc_pinned(max(sb.my_records, 1) * rsync_amd.RECORD_BYTES)
+    out["d2h_parallel_pipelined"] = timed(lambda i: sb.run_d2h(arenas[i & 1], SEED, recs, host))
+    out["d2h_parallel_pipelined"]["bytes_to_host_per_rank"] = sb.my_records * rsync_amd.RECORD_BYTES
+    eng.free_pinned(host)
+    # RCCL gather of every rank's records to rank 0 (one rank: the root's self copy)
+    if world > 1:
+        import torch.distributed as dist
+        uid = [rsync_amd.Engine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        uid = uid[0]
+    else:
+        uid = rsync_amd.Engine.comm_unique_id()
+    eng.comm_init(world, rank, uid)
+    recv = eng.alloc(max(records_all, 1) * rsync_amd.RECORD_BYTES) if rank == 0 else None
+    out["kernel_plus_gather_pipelined"] = timed(lambda i: sb.run_gather(arenas[i & 1], SEED, recs, recv, 0))
+    out["kernel_plus_gather_pipelined"]["bytes_to_root"] = (records_all - sb.my_records) * rsync_amd.RECORD_BYTES
+    out["recv"] = recv
+    return out
+
+
+def guarded_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, records_all, print_line):
+    """measure_delivery under a watchdog: a collective that stalls for 120 s
+    makes rank 0 print the bench line with the error and every rank exit 3
+    (a failed collective must not look like success); an exception is
+    reported in the line."""
+    import threading
+    done = threading.Event()
+
+    def watchdog():
+        if not done.wait(120.0):
+            if rank == 0:
+                print_line({"error": "delivery timed out after 120 s (stalled collective)"})
+            os._exit(3)
+    if world > 1:
+        threading.Thread(target=watchdog, daemon=True).start()
+    try:
+        d = measure_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, records_all)
+        d.pop("recv", None)
+    except Exception as e:  # reported, never fatal to the bench line
+        d = {"error": str(e)[:300]}
+    done.set()
+    return d
+
+
+
 def make_cfg3_file(eng, basis, src, size, seed, B, rng):
     """Source = the basis with random runs (1 B .. 2B long) overwritten until
     ~50% of the bytes differ, plus a few insertions/deletions so matches fall at
@@ -434,11 +500,16 @@ def bench_sender(args, rank, world, local):
     import torch.distributed as dist
     if world > 1:  # files shard across ranks with no exchange: max-over-ranks wall time
         dist.barrier()
+    eng.set_kernel_timing(True)
+    eng.kernel_times(reset=True)
     t0 = time.perf_counter()
     nm = 0
     for _ in range(steps):
-        nm += sum(len(m) for m in eng.hash_search_batch(jobs, SEED, as_arrays=True))
+        res = eng.hash_search_batch(jobs, SEED, as_arrays=True)
+        nm += sum(len(m) for m in res)
     dt = time.perf_counter() - t0
+    kt = eng.kernel_times(reset=True)  # HIP events around every roll / confirmation on their own streams
+    eng.set_kernel_timing(False)
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -454,6 +525,31 @@ def bench_sender(args, rank, world, local):
         st = torch.tensor([float(scanned)], dtype=torch.float64)
         dist.all_reduce(st)
         scanned = float(st[0])
+    roll_ms = kt["roll_ms"] / max(kt["roll_launches"], 1)
+    confirm_ms = kt["confirm_ms"] / max(kt["confirm_batches"], 1)
+    src_bytes = sum(m[0] for m in metas) / len(metas)  # algorithmic bytes of one roll launch: its source, read once
+    cpu, parity = None, None
+    if rank == 0 and not args.no_cpu:
+        # cpu_baseline leg: the C restatement of hashSearch (match.go:21-230)
+        # on the first 256 MiB of file 0 against file 0's basis sums, 1 core;
+        # its matches also check the benchmarked match list of file 0 (the
+        # greedy walk is left to right, so every match whose window ends
+        # before the sample's last block is the same in both)
+        from oracle import oracle as orc
+        n0, head0, s1_0, s2_0, tg0 = metas[0]
+        P = min(256 << 20, n0)
+        sample = srcs[0].download(P)
+        c0 = time.perf_counter()
+        om, _, _ = orc.hash_search(sample, head0.astuple(), s1_0, s2_0, tg0, SEED)
+        t_cpu = time.perf_counter() - c0
+        B0 = head0.block_len
+        cut = P - B0
+        gm = [(int(o), int(i)) for o, i in zip(res[0]["offset"], res[0]["index"])]
+        want = [m for m in om if m[0] + B0 <= cut]
+        parity = {"matches_compared": len(want), "equal": want == [m for m in gm if m[0] + B0 <= cut]}
+        cpu = {"value": round(P / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+               "sample": f"first {P >> 20} MiB of file 0 vs its basis sums, oracle/rsg_oracle.c orc_hash_search "
+                         f"(scalar C restatement of match.go:21-282), 1 thread, {t_cpu:.1f} s"}
     if rank == 0:
         print(json.dumps({"metric": "GiB/s source scanned (sender rolling match), device-resident",
                           "value": round(scanned / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
@@ -463,7 +559,18 @@ def bench_sender(args, rank, world, local):
                                      "files": args.cfg3_files, "matches_per_pass": nm // steps,
                                      "call": "rsg_hash_search_batch_device, one call per pass"},
                           "ms_per_file": round(dt * 1e3 / (steps * len(metas)), 3),
-                          "single_file_calls_gib_s": single_gib_s}), flush=True)
+                          "single_file_calls_gib_s": single_gib_s,
+                          "roofline": {"bound": "hbm", "kernel": "roll_kernel",
+                                       "achieved": round(src_bytes / (roll_ms * 1e-3) / 1e9, 1),
+                                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                       "frac": round(src_bytes / (roll_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                       "traffic": None, "kernel_ms": round(roll_ms, 4),
+                                       "launches": kt["roll_launches"],
+                                       "algorithmic_bytes_per_launch": int(src_bytes),
+                                       "confirm_ms_per_batch": round(confirm_ms, 4),
+                                       "confirm_batches": kt["confirm_batches"]},
+                          "oracle_parity_file0": parity,
+                          "cpu_baseline": cpu}), flush=True)
     eng.close()
 
 
@@ -483,41 +590,46 @@ def cfg4_traffic(world, records):
 def bench_mixed(args, rank, world, local):
     """cfg4: 100 000 files of uniform length in [4096, 65536] (PRNG seed 4),
     B = 700, block sums with the file list sharded by bytes over the ranks
-    (rsync_amd.shard.plan_shards: contiguous block ranges, so rank order of the
-    records is the global order; strong scaling, total work fixed).  Each
-    rank's pieces sit back to back at 16-byte aligned offsets of one arena; a
-    piece that starts inside a file starts on a block boundary, so it is
-    planned as a file of its own with the same blocks.  Reported beside cfg2,
-    never as the headline value."""
+    (rsync_amd.dist.shard_layout: contiguous block ranges, so rank order of
+    the records is the global order; strong scaling, total work fixed), each
+    rank's range cut into --batches batches.  Each rank's files sit back to
+    back at 16-byte aligned offsets of one arena; a piece that starts inside a
+    file starts on a block boundary, so it is planned as a file of its own
+    with the same blocks.  Reported beside cfg2, never as the headline.
+    Three numbers: kernel-only (the value), and the records delivered while
+    the next batch hashes -- gathered to rank 0 over RCCL, or copied to host
+    by every rank in parallel."""
     import torch
     import torch.distributed as dist
     import rsync_amd
-    from rsync_amd.shard import plan_shards
+    from rsync_amd.dist import ShardedBlockSums, rank_arena, shard_layout
     NF = 100_000
     lengths = np.random.default_rng(4).integers(4096, 65537, NF).tolist()
-    mine = plan_shards(lengths, world, BLOCK_LEN)[rank]
+    lay = shard_layout(lengths, world, max(1, args.batches), BLOCK_LEN)
     eng = rsync_amd.Engine(local)
     stream = torch.cuda.Stream(device=local)
     sptr = stream.cuda_stream
-    # whole files of this rank's pieces, then each piece's block range inside
-    files = sorted({p.file for p in mine})
-    at, fpos = 0, {}
-    for f in files:
-        fpos[f] = at
-        at += (lengths[f] + 15) & ~15
-    arena_bytes = max(at, 16)
+    pos, arena_bytes = rank_arena(lengths, lay, rank)
     arenas = [eng.alloc(arena_bytes) for _ in range(2)]
     for a in arenas:
-        for f in files:
-            eng.fill_splitmix64(a, lengths[f], f + 1, offset=fpos[f], stream=sptr)
-    desc = [(fpos[p.file] + p.offset, p.length, BLOCK_LEN) for p in mine]
-    plan = eng.plan(desc, arena_bytes)
-    recs = eng.alloc(max(plan.total_records, 1) * rsync_amd.RECORD_BYTES)
-    eng.synchronize(sptr)
+        for f, o in pos.items():
+            eng.fill_splitmix64(a, lengths[f], f + 1, offset=o, stream=sptr)
+    sb = ShardedBlockSums.from_layout(eng, lay, rank, pos, arena_bytes)
+    recs = eng.alloc(max(sb.my_records, 1) * rsync_amd.RECORD_BYTES)
+    mine = [p for g in lay.batches[rank] for p in g]
     my_bytes = sum(p.length for p in mine)
-    for i in range(max(args.warmup, 20)):
-        plan.run(arenas[i & 1], SEED, recs, stream=sptr)
+    # kernel-only step: the rank's whole share as ONE launch (the batches
+    # exist for the delivery modes below)
+    whole = eng.plan([(pos[p.file] + p.offset, p.length, p.block_len) for p in mine], arena_bytes) if mine else None
     eng.synchronize(sptr)
+
+    def kernel_step(i):
+        if whole is not None:
+            whole.run(arenas[i & 1], SEED, recs, stream=sptr)
+    for i in range(max(args.warmup, 20)):
+        kernel_step(i)
+    eng.synchronize(sptr)
+    eng.block_sums_fallbacks(reset=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -525,7 +637,7 @@ def bench_mixed(args, rank, world, local):
     t0 = time.perf_counter()
     ev0.record(stream)
     for i in range(args.steps):
-        plan.run(arenas[i & 1], SEED, recs, stream=sptr)
+        kernel_step(i)
     ev1.record(stream)
     eng.synchronize(sptr)
     torch.cuda.synchronize()
@@ -533,10 +645,8 @@ def bench_mixed(args, rank, world, local):
         dist.barrier()
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
-    if world > 1:
-        tt = torch.tensor([wall, kernel_ms], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        wall, kernel_ms = float(tt[0]), float(tt[1])
+    fallbacks = eng.block_sums_fallbacks(reset=True)
+    wall, kernel_ms = max_over_ranks(world, wall, kernel_ms)
     total = sum(lengths)
     cpu = None
     if rank == 0 and not args.no_cpu:
@@ -545,13 +655,13 @@ def bench_mixed(args, rank, world, local):
         from oracle import oracle as orc
         lib = orc.lib()
         t_cpu, done, k, parity = 0.0, 0, 0, True
-        first = plan.first_record
+        first = np.cumsum([0] + [p.b1 - p.b0 for p in mine]).tolist()
         while t_cpu < args.cpu_seconds / 2 and k < 4 * len(mine):
             j = k % len(mine)
             p = mine[j]
             data = orc.splitmix64_bytes(p.file + 1, lengths[p.file])[p.offset:p.offset + p.length]
             data = np.ascontiguousarray(data)
-            cnt = (p.length + BLOCK_LEN - 1) // BLOCK_LEN
+            cnt = p.b1 - p.b0
             out = np.empty(cnt * 20, np.uint8)
             c0 = time.perf_counter()
             lib.orc_block_sums(orc._ptr(data), data.size, BLOCK_LEN, orc._i32(SEED), orc._ptr(out))
@@ -563,9 +673,10 @@ def bench_mixed(args, rank, world, local):
         cpu = {"value": round(done / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
                "sample": f"{k} pieces of rank 0's cfg4 shard at B=700, oracle/rsg_oracle.c orc_block_sums, "
                          f"1 thread, {t_cpu:.1f} s", "gpu_parity_on_sample": parity}
-    if rank == 0:
-        algo = my_bytes + plan.total_records * rsync_amd.RECORD_BYTES
-        print(json.dumps({
+    algo = my_bytes + sb.my_records * rsync_amd.RECORD_BYTES
+
+    def line(more):
+        d = {
             "metric": "GiB/s block-checksummed (weak+MD4), device-resident, at 1/2/4/8 MI355X",
             "value": round(total * args.steps / wall / GIB, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall * 1e3 / args.steps, 4),
@@ -573,14 +684,28 @@ def bench_mixed(args, rank, world, local):
             "data": "synthetic (splitmix64 bytes generated on device)",
             "config": {"workload": "cfg4: 100k files, lengths uniform in [4096, 65536], B=700, block sums, "
                                    "file list sharded by bytes", "files": NF, "total_bytes": total,
-                       "rank0_pieces": len(mine), "rank0_records": plan.total_records,
+                       "rank0_pieces": len(mine), "rank0_records": sb.my_records, "batches_per_rank": lay.nbatch,
                        "parallelism": f"file list sharded, {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": round(algo / (kernel_ms * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "traffic": cfg4_traffic(world, plan.total_records),
+                         "traffic": cfg4_traffic(world, sb.my_records),
                          "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": int(algo)},
-            "cpu_baseline": cpu}), flush=True)
+            "fallback_census_rank0": {"staged_waves": fallbacks[0], "park_tiles": fallbacks[1]},
+            "cpu_baseline": cpu}
+        d.update(more)
+        return d
+
+    more = {}
+    if not args.no_delivery:
+        more["delivery"] = guarded_delivery(args, eng, sb, arenas, recs, world, rank, float(total),
+                                            lay.total_records, lambda d: print(json.dumps(line({"delivery": d})),
+                                                                               flush=True))
+    if rank == 0:
+        print(json.dumps(line(more)), flush=True)
+    sb.close()
+    if whole is not None:
+        whole.close()
     eng.close()
     if world > 1:
         dist.destroy_process_group()

@@ -272,6 +272,15 @@ typedef struct rsg_search_job {
 rsg_status rsg_hash_search_batch_device(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed);
 rsg_status rsg_hash_search_batch_host(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed);
 
+/* Kernel timing of the sender path for roofline measurements (bench.py):
+ * while on, every roll launch and every confirmation batch (block sums of the
+ * windows + resolve) of ctx is bracketed by HIP events on the stream it runs
+ * on.  rsg_kernel_times waits for them and returns out[0] = total roll ms,
+ * out[1] = roll launches, out[2] = total confirmation ms, out[3] =
+ * confirmation batches; reset != 0 drops the recorded events. */
+rsg_status rsg_set_kernel_timing(rsg_ctx *ctx, int32_t on);
+rsg_status rsg_kernel_times(rsg_ctx *ctx, double out[4], int32_t reset);
+
 /* Token stream of simpleSendToken (token.go:4-31) as matched() emits it
  * (match.go:233-282): literal runs in <= 256 KiB pieces (int32 LE n + n bytes),
  * a match as int32 -(i+1), terminated by int32 0 (match.go:212).  Host byte
@@ -301,6 +310,32 @@ rsg_status rsg_apply_tokens(const uint8_t *tokens, uint64_t tokens_len, const rs
 rsg_status rsg_receive_data(rsg_ctx *ctx, const uint8_t *tokens, uint64_t tokens_len, const rsg_sum_head *head,
                             const uint8_t *basis, uint64_t basis_len, int32_t seed, uint8_t *out, uint64_t out_cap,
                             uint64_t *out_len, uint64_t *consumed);
+
+/* Batched receiveData for the files of a transfer (RecvFiles' per-file
+ * receiveData calls, receiver.go:18-188): every job as rsg_receive_data,
+ * with the seeded whole-file sums of many files hashed together (one GPU
+ * lane per file; MD4 is serial within a file, so a single large file gains
+ * nothing over rsg_receive_data).  Jobs go in batches of <= 256 MiB of
+ * rebuilt bytes; batch k is hashed on the GPU while the host applies the
+ * tokens of batch k+1.  Per job: out_len, consumed and status (RSG_OK;
+ * RSG_ERR_INVALID / RSG_ERR_TRUNCATED for its own stream or capacity, as
+ * rsg_receive_data; RSG_ERR_CORRUPT on a whole-file sum mismatch).  A HIP or
+ * allocation failure stops the call and is every unfinished job's status.
+ * Returns RSG_OK or the first failing job's status. */
+typedef struct rsg_recv_job {
+    const uint8_t *tokens;   /* bytes after the SumHead: tokens, 0, 16-byte sum */
+    uint64_t tokens_len;
+    rsg_sum_head head;
+    const uint8_t *basis;    /* NULL: no local file                          */
+    uint64_t basis_len;
+    uint8_t *out;            /* rebuilt file                                 */
+    uint64_t out_cap;
+    uint64_t out_len;        /* out */
+    uint64_t consumed;       /* out: stream bytes used, including the sum     */
+    int32_t status;          /* out */
+    int32_t reserved;
+} rsg_recv_job;
+rsg_status rsg_receive_data_batch(rsg_ctx *ctx, rsg_recv_job *jobs, uint64_t njobs, int32_t seed);
 
 /* ------------------------------------------ whole-file sums
  * MD4 of whole files, one GPU lane per file (MD4 is serial within a message,
@@ -335,6 +370,37 @@ rsg_status rsg_comm_init(rsg_ctx *ctx, int32_t nranks, int32_t rank, const uint8
  * send_bytes has nranks entries on every rank.  Asynchronous on `stream`. */
 rsg_status rsg_gather_bytes(rsg_ctx *ctx, const void *d_send, const uint64_t *send_bytes,
                             void *d_recv, int32_t root, void *stream);
+/* Same with explicit landing offsets: rank q's bytes go to d_recv +
+ * recv_offsets[q] on the root (NULL = the exclusive prefix of send_bytes). */
+rsg_status rsg_gatherv_bytes(rsg_ctx *ctx, const void *d_send, const uint64_t *send_bytes, void *d_recv,
+                             const uint64_t *recv_offsets, int32_t root, void *stream);
+
+/* Pipelined sharded generator step.  A rank's share of the file list
+ * (contiguous block ranges, rsync_amd/dist.py) is cut into batches, each
+ * with its own plan over the rank's arena.  Batch b's records are written at
+ * d_records + 20 * record_offset and, while batch b+1 is hashed (kernel on
+ * the context's stream, the transfer on a second one behind an event):
+ *   rsg_block_sums_gather: sent to the root over RCCL (xGMI); every rank's
+ *     bytes of batch b (send_bytes[q], nranks entries, equal on all ranks)
+ *     land at d_recv + recv_offsets[q] on the root, so the root's buffer ends
+ *     up in global record order (GenerateFiles' file-list order,
+ *     generator.go:20-52).  Collective: every rank calls it with the same
+ *     nbatch; a rank with no blocks in batch b passes plan = NULL.
+ *   rsg_block_sums_d2h: copied to h_records + 20 * record_offset on the
+ *     host (ranks do this concurrently over their own PCIe links: the
+ *     alternative to gather-then-one-D2H).  Pinned h_records runs at DMA speed.
+ * Synchronous: returns after the last transfer. */
+typedef struct rsg_shard_batch {
+    const rsg_plan *plan;          /* this rank's pieces of batch b (NULL: none) */
+    uint64_t record_offset;        /* first record of batch b in d_records       */
+    const uint64_t *send_bytes;    /* gather: nranks entries                     */
+    const uint64_t *recv_offsets;  /* gather: nranks entries (root byte offsets)  */
+} rsg_shard_batch;
+rsg_status rsg_block_sums_gather(rsg_ctx *ctx, const rsg_shard_batch *batches, uint64_t nbatch,
+                                 const void *d_arena, int32_t seed, void *d_records, void *d_recv,
+                                 int32_t root);
+rsg_status rsg_block_sums_d2h(rsg_ctx *ctx, const rsg_shard_batch *batches, uint64_t nbatch,
+                              const void *d_arena, int32_t seed, void *d_records, uint8_t *h_records);
 
 /* ------------------------------------------ wire formats
  * Host byte formatting around the checksum path, so the engine's records

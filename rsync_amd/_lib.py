@@ -72,6 +72,20 @@ class FdFile(ctypes.Structure):
                 ("len", ctypes.c_uint64), ("block_len", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+class RecvJob(ctypes.Structure):
+    """rsg_recv_job: one file of rsg_receive_data_batch (out_len, consumed, status out)."""
+    _fields_ = [("tokens", ctypes.c_void_p), ("tokens_len", ctypes.c_uint64), ("head", SumHead),
+                ("basis", ctypes.c_void_p), ("basis_len", ctypes.c_uint64), ("out", ctypes.c_void_p),
+                ("out_cap", ctypes.c_uint64), ("out_len", ctypes.c_uint64), ("consumed", ctypes.c_uint64),
+                ("status", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class ShardBatch(ctypes.Structure):
+    """rsg_shard_batch: one batch of a rank's pipelined sharded generator step."""
+    _fields_ = [("plan", ctypes.c_void_p), ("record_offset", ctypes.c_uint64),
+                ("send_bytes", ctypes.POINTER(ctypes.c_uint64)), ("recv_offsets", ctypes.POINTER(ctypes.c_uint64))]
+
+
 # rsg_write_fn: int32 (*)(void *user, const uint8_t *data, uint64_t len)
 WRITE_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
 
@@ -115,17 +129,23 @@ _PROTOS = {
                                      ctypes.POINTER(Match), _u64, ctypes.POINTER(_u64)]),
     "rsg_hash_search_batch_device": (_st, [_vp, ctypes.POINTER(SearchJob), _u64, _i32]),
     "rsg_hash_search_batch_host": (_st, [_vp, ctypes.POINTER(SearchJob), _u64, _i32]),
+    "rsg_set_kernel_timing": (_st, [_vp, _i32]),
+    "rsg_kernel_times": (_st, [_vp, ctypes.POINTER(ctypes.c_double), _i32]),
     "rsg_encode_tokens": (_st, [_vp, _u64, ctypes.POINTER(SumHead), ctypes.POINTER(Match), _u64,
                                 _vp, _u64, ctypes.POINTER(_u64)]),
     "rsg_apply_tokens": (_st, [_vp, _u64, ctypes.POINTER(SumHead), _vp, _u64, _vp, _u64,
                                ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "rsg_receive_data": (_st, [_vp, _vp, _u64, ctypes.POINTER(SumHead), _vp, _u64, _i32, _vp, _u64,
                                ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
+    "rsg_receive_data_batch": (_st, [_vp, ctypes.POINTER(RecvJob), _u64, _i32]),
     "rsg_file_sums_host": (_st, [_vp, ctypes.POINTER(File), _u64, _i32, _i32, _vp]),
     "rsg_file_sums_device": (_st, [_vp, _vp, _u64, ctypes.POINTER(File), _u64, _i32, _i32, _vp]),
     "rsg_comm_unique_id": (_st, [_vp]),
     "rsg_comm_init": (_st, [_vp, _i32, _i32, _vp]),
     "rsg_gather_bytes": (_st, [_vp, _vp, ctypes.POINTER(_u64), _vp, _i32, _vp]),
+    "rsg_gatherv_bytes": (_st, [_vp, _vp, ctypes.POINTER(_u64), _vp, ctypes.POINTER(_u64), _i32, _vp]),
+    "rsg_block_sums_gather": (_st, [_vp, ctypes.POINTER(ShardBatch), _u64, _vp, _i32, _vp, _vp, _i32]),
+    "rsg_block_sums_d2h": (_st, [_vp, ctypes.POINTER(ShardBatch), _u64, _vp, _i32, _vp, _vp]),
     "rsg_check_sum_head": (_st, [ctypes.POINTER(SumHead)]),
     "rsg_encode_sums": (_st, [_vp, ctypes.POINTER(SumHead), _u64, _vp, _i32, _vp, _u64, ctypes.POINTER(_u64)]),
     "rsg_decode_sums": (_st, [_vp, _u64, ctypes.POINTER(SumHead), _vp, _vp, _u64, ctypes.POINTER(_u64)]),

@@ -1,5 +1,6 @@
 // rsg_api.cpp -- C-ABI of librsg.so: contexts, block-sum plans, the host
-// (PCIe-inclusive) pipeline, token encoding and the RCCL sums gather.
+// (PCIe-inclusive) pipeline and token encoding (the RCCL gather and the
+// sharded pipelines are in rsg_dist.cpp).
 // Declarations and contracts: include/rsg.h.
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -278,6 +279,10 @@ void rsg_ctx_destroy(rsg_ctx *c) {
     for (PinBuf *b : pbs)
         if (b->p) hipHostFree(b->p);
     if (c->comm) ncclCommDestroy(c->comm);
+    for (const rsg_ctx::TimedSpan &t : c->spans) {
+        hipEventDestroy(t.a);
+        hipEventDestroy(t.b);
+    }
     for (int i = 0; i < 2; i++) {
         if (c->side_done[i]) hipEventDestroy(c->side_done[i]);
         if (c->side[i]) hipStreamDestroy(c->side[i]);
@@ -653,62 +658,6 @@ rsg_status rsg_encode_tokens(const uint8_t *src, uint64_t src_len, const rsg_sum
     put_i32(0);
     *out_len = pos;
     if (!fits) return fail(nullptr, RSG_ERR_TRUNCATED, "token stream needs %llu bytes", (unsigned long long)pos);
-    return RSG_OK;
-}
-
-// ---------------------------------------------------------------- RCCL gather
-rsg_status rsg_comm_unique_id(uint8_t id[128]) {
-    if (!id) return fail(nullptr, RSG_ERR_INVALID, "id is NULL");
-    ncclUniqueId u;
-    ncclResult_t r = ncclGetUniqueId(&u);
-    if (r != ncclSuccess) return fail(nullptr, RSG_ERR_HIP, "ncclGetUniqueId: %s", ncclGetErrorString(r));
-    memcpy(id, u.internal, 128);
-    return RSG_OK;
-}
-
-rsg_status rsg_comm_init(rsg_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t id[128]) {
-    RSG_ENTER(ctx);
-    if (!id || nranks < 1 || rank < 0 || rank >= nranks) return fail(ctx, RSG_ERR_INVALID, "bad rank/nranks");
-    if (ctx->comm) {
-        ncclCommDestroy(ctx->comm);
-        ctx->comm = nullptr;
-    }
-    ncclUniqueId u;
-    memcpy(u.internal, id, 128);
-    ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, u, rank);
-    if (r != ncclSuccess) return fail(ctx, RSG_ERR_HIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
-    ctx->nranks = nranks;
-    ctx->rank = rank;
-    return RSG_OK;
-}
-
-rsg_status rsg_gather_bytes(rsg_ctx *ctx, const void *d_send, const uint64_t *send_bytes, void *d_recv,
-                            int32_t root, void *stream) {
-    RSG_ENTER(ctx);
-    if (!ctx->comm) return fail(ctx, RSG_ERR_INVALID, "rsg_comm_init not called");
-    if (!send_bytes || root < 0 || root >= ctx->nranks) return fail(ctx, RSG_ERR_INVALID, "bad gather arguments");
-    hipStream_t st = pick_stream(ctx, stream);
-    ncclResult_t r = ncclGroupStart();
-    if (ctx->rank == root) {
-        uint64_t off = 0;
-        for (int q = 0; q < ctx->nranks; q++) {
-            uint8_t *dst = (uint8_t *)d_recv + off;
-            if (send_bytes[q]) {
-                if (q == root) {
-                    hipError_t e = hipMemcpyAsync(dst, d_send, send_bytes[q], hipMemcpyDeviceToDevice, st);
-                    if (e != hipSuccess) { ncclGroupEnd(); return hip_fail(ctx, e, "gather self copy"); }
-                } else if (r == ncclSuccess) {
-                    r = ncclRecv(dst, send_bytes[q], ncclUint8, q, ctx->comm, st);
-                }
-            }
-            off += send_bytes[q];
-        }
-    } else if (send_bytes[ctx->rank] && r == ncclSuccess) {
-        r = ncclSend(d_send, send_bytes[ctx->rank], ncclUint8, root, ctx->comm, st);
-    }
-    ncclResult_t r2 = ncclGroupEnd();
-    if (r != ncclSuccess || r2 != ncclSuccess)
-        return fail(ctx, RSG_ERR_HIP, "rccl gather: %s", ncclGetErrorString(r != ncclSuccess ? r : r2));
     return RSG_OK;
 }
 

@@ -1,0 +1,187 @@
+// rsg_dist.cpp -- multi-GPU exchange of the sharded generator step
+// (SURVEY.md §8(e)): RCCL over xGMI for the records gather, and the two
+// pipelined delivery modes of a rank's batches (include/rsg.h).
+//
+// The reference has no distribution of its own: GenerateFiles writes every
+// file's sums in file-list order (internal/receiver/generator.go:20-52).
+// Here the file list is sharded over the ranks of one node (rsync_amd/dist.py
+// plans it); the only exchange is moving each rank's records to where the
+// writer is, in global order.  Both modes overlap that movement with the
+// hashing of the next batch:
+//   kernel(b)  on ctx->stream            kernel(b+1) ...
+//   move(b)    on ctx->side[0], after an event recorded behind kernel(b)
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <vector>
+
+#include "rsg_host.h"
+
+using namespace rsgh;
+
+namespace {
+
+// Root receives send_bytes[q] bytes from every rank q at recv_off[q] (or the
+// exclusive prefix of send_bytes when recv_off is NULL); grouped
+// ncclSend/ncclRecv, since the sizes are ragged (ncclGather is not).
+rsg_status gatherv(rsg_ctx *ctx, const void *d_send, const uint64_t *send_bytes, void *d_recv,
+                   const uint64_t *recv_off, int32_t root, hipStream_t st) {
+    ncclResult_t r = ncclGroupStart();
+    if (ctx->rank == root) {
+        uint64_t off = 0;
+        for (int q = 0; q < ctx->nranks; q++) {
+            uint8_t *dst = (uint8_t *)d_recv + (recv_off ? recv_off[q] : off);
+            if (send_bytes[q]) {
+                if (q == root) {
+                    const hipError_t e = hipMemcpyAsync(dst, d_send, send_bytes[q], hipMemcpyDeviceToDevice, st);
+                    if (e != hipSuccess) {
+                        ncclGroupEnd();
+                        return hip_fail(ctx, e, "gather self copy");
+                    }
+                } else if (r == ncclSuccess) {
+                    r = ncclRecv(dst, send_bytes[q], ncclUint8, q, ctx->comm, st);
+                }
+            }
+            off += send_bytes[q];
+        }
+    } else if (send_bytes[ctx->rank] && r == ncclSuccess) {
+        r = ncclSend(d_send, send_bytes[ctx->rank], ncclUint8, root, ctx->comm, st);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+        return fail(ctx, RSG_ERR_HIP, "rccl gather: %s", ncclGetErrorString(r != ncclSuccess ? r : r2));
+    return RSG_OK;
+}
+
+struct Events {  // one per batch, destroyed on every exit
+    std::vector<hipEvent_t> ev;
+    ~Events() {
+        for (hipEvent_t e : ev)
+            if (e) hipEventDestroy(e);
+    }
+};
+
+// Shared driver of the two modes: kernel(b) on ctx->stream, then `move(b)`
+// queued on ctx->side[0] behind an event of kernel(b).  Waits for both
+// streams on every exit (nothing outlives the call).
+template <class Move>
+rsg_status pipeline(rsg_ctx *ctx, const rsg_shard_batch *batches, uint64_t nbatch, const void *d_arena, int32_t seed,
+                    void *d_records, Move move) {
+    struct Drain {
+        rsg_ctx *c;
+        ~Drain() {
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipStreamSynchronize(c->side[0]);
+        }
+    } drain{ctx};
+    Events evs;
+    evs.ev.assign(nbatch, nullptr);
+    for (uint64_t b = 0; b < nbatch; b++) {
+        const rsg_shard_batch &sb = batches[b];
+        if (sb.plan) {
+            if (sb.plan->ctx != ctx) return fail(ctx, RSG_ERR_INVALID, "batch %llu: plan of another context",
+                                                 (unsigned long long)b);
+            const rsg_status s = launch_plan(ctx, sb.plan->host, sb.plan->d_files, sb.plan->d_wg, d_arena, seed,
+                                             (uint8_t *)d_records + sb.record_offset * rsg::kRecordBytes,
+                                             sb.plan->d_scratch, ctx->stream);
+            if (s != RSG_OK) return s;
+        }
+        RSG_HIP(ctx, hipEventCreateWithFlags(&evs.ev[b], hipEventDisableTiming));
+        RSG_HIP(ctx, hipEventRecord(evs.ev[b], ctx->stream));
+        RSG_HIP(ctx, hipStreamWaitEvent(ctx->side[0], evs.ev[b], 0));
+        const rsg_status s = move(b, sb);
+        if (s != RSG_OK) return s;
+    }
+    RSG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    RSG_HIP(ctx, hipStreamSynchronize(ctx->side[0]));
+    return RSG_OK;
+}
+
+uint64_t plan_records(const rsg_shard_batch &sb) { return sb.plan ? sb.plan->host.total_blocks : 0; }
+
+}  // namespace
+
+extern "C" {
+
+rsg_status rsg_comm_unique_id(uint8_t id[128]) {
+    if (!id) return fail(nullptr, RSG_ERR_INVALID, "id is NULL");
+    ncclUniqueId u;
+    const ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess) return fail(nullptr, RSG_ERR_HIP, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+    memcpy(id, u.internal, 128);
+    return RSG_OK;
+}
+
+rsg_status rsg_comm_init(rsg_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t id[128]) {
+    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    RSG_HIP(ctx, hipSetDevice(ctx->device));
+    if (!id || nranks < 1 || rank < 0 || rank >= nranks) return fail(ctx, RSG_ERR_INVALID, "bad rank/nranks");
+    if (ctx->comm) {
+        ncclCommDestroy(ctx->comm);
+        ctx->comm = nullptr;
+    }
+    ncclUniqueId u;
+    memcpy(u.internal, id, 128);
+    const ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, u, rank);
+    if (r != ncclSuccess) return fail(ctx, RSG_ERR_HIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    return RSG_OK;
+}
+
+rsg_status rsg_gather_bytes(rsg_ctx *ctx, const void *d_send, const uint64_t *send_bytes, void *d_recv, int32_t root,
+                            void *stream) {
+    return rsg_gatherv_bytes(ctx, d_send, send_bytes, d_recv, nullptr, root, stream);
+}
+
+rsg_status rsg_gatherv_bytes(rsg_ctx *ctx, const void *d_send, const uint64_t *send_bytes, void *d_recv,
+                             const uint64_t *recv_offsets, int32_t root, void *stream) {
+    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    RSG_HIP(ctx, hipSetDevice(ctx->device));
+    if (!ctx->comm) return fail(ctx, RSG_ERR_INVALID, "rsg_comm_init not called");
+    if (!send_bytes || root < 0 || root >= ctx->nranks) return fail(ctx, RSG_ERR_INVALID, "bad gather arguments");
+    return gatherv(ctx, d_send, send_bytes, d_recv, recv_offsets, root, stream ? (hipStream_t)stream : ctx->stream);
+}
+
+rsg_status rsg_block_sums_gather(rsg_ctx *ctx, const rsg_shard_batch *batches, uint64_t nbatch, const void *d_arena,
+                                 int32_t seed, void *d_records, void *d_recv, int32_t root) {
+    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    RSG_HIP(ctx, hipSetDevice(ctx->device));
+    if (!ctx->comm) return fail(ctx, RSG_ERR_INVALID, "rsg_comm_init not called");
+    if ((nbatch && !batches) || root < 0 || root >= ctx->nranks) return fail(ctx, RSG_ERR_INVALID, "bad arguments");
+    for (uint64_t b = 0; b < nbatch; b++) {
+        if (!batches[b].send_bytes || !batches[b].recv_offsets)
+            return fail(ctx, RSG_ERR_INVALID, "batch %llu: send_bytes / recv_offsets missing", (unsigned long long)b);
+        if (batches[b].send_bytes[ctx->rank] != plan_records(batches[b]) * rsg::kRecordBytes)
+            return fail(ctx, RSG_ERR_INVALID, "batch %llu: send_bytes[%d] = %llu, the plan has %llu records",
+                        (unsigned long long)b, ctx->rank, (unsigned long long)batches[b].send_bytes[ctx->rank],
+                        (unsigned long long)plan_records(batches[b]));
+    }
+    if (ctx->rank == root && !d_recv) return fail(ctx, RSG_ERR_INVALID, "root needs d_recv");
+    return pipeline(ctx, batches, nbatch, d_arena, seed, d_records, [&](uint64_t, const rsg_shard_batch &sb) {
+        return gatherv(ctx, (const uint8_t *)d_records + sb.record_offset * rsg::kRecordBytes, sb.send_bytes, d_recv,
+                       sb.recv_offsets, root, ctx->side[0]);
+    });
+}
+
+rsg_status rsg_block_sums_d2h(rsg_ctx *ctx, const rsg_shard_batch *batches, uint64_t nbatch, const void *d_arena,
+                              int32_t seed, void *d_records, uint8_t *h_records) {
+    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    RSG_HIP(ctx, hipSetDevice(ctx->device));
+    if ((nbatch && !batches) || !h_records) return fail(ctx, RSG_ERR_INVALID, "bad arguments");
+    return pipeline(ctx, batches, nbatch, d_arena, seed, d_records,
+                    [&](uint64_t, const rsg_shard_batch &sb) -> rsg_status {
+                        const uint64_t n = plan_records(sb) * rsg::kRecordBytes;
+                        if (n)
+                            RSG_HIP(ctx, hipMemcpyAsync(h_records + sb.record_offset * rsg::kRecordBytes,
+                                                        (const uint8_t *)d_records + sb.record_offset * rsg::kRecordBytes,
+                                                        n, hipMemcpyDeviceToHost, ctx->side[0]));
+                        return RSG_OK;
+                    });
+}
+
+}  // extern "C"

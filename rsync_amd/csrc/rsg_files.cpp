@@ -44,24 +44,40 @@ std::vector<uint32_t> lane_order(const std::vector<rsg::FileSpan> &spans) {
     return order;
 }
 
-// Upload spans + order to ctx->d_desc[0] and launch on ctx->stream.
-rsg_status launch(rsg_ctx *ctx, const void *d_arena, uint64_t arena_bytes, const std::vector<rsg::FileSpan> &spans,
-                  int32_t mode, int32_t seed, void *d_out) {
+}  // namespace
+
+namespace rsgh {
+
+// Upload spans + order through ctx->h_desc[slot] / d_desc[slot] and launch
+// the whole-file sums on `stream` (asynchronous; the slot's staging must not
+// be reused before the stream has passed this point).
+rsg_status launch_file_sums_async(rsg_ctx *ctx, const void *d_arena, uint64_t arena_bytes,
+                                  const std::vector<rsg::FileSpan> &spans, int32_t mode, int32_t seed, void *d_out,
+                                  int slot, hipStream_t stream) {
     const std::vector<uint32_t> order = lane_order(spans);
     const uint64_t sbytes = spans.size() * sizeof(rsg::FileSpan);
     const uint64_t ooff = (sbytes + 63) & ~63ull;
     rsg_status s;
-    if ((s = ensure_dev(ctx, ctx->d_desc[0], ooff + order.size() * 4 + 64)) != RSG_OK) return s;
-    if ((s = ensure_pin(ctx, ctx->h_desc[0], ooff + order.size() * 4 + 64)) != RSG_OK) return s;
-    uint8_t *hd = (uint8_t *)ctx->h_desc[0].p;
+    if ((s = ensure_dev(ctx, ctx->d_desc[slot], ooff + order.size() * 4 + 64)) != RSG_OK) return s;
+    if ((s = ensure_pin(ctx, ctx->h_desc[slot], ooff + order.size() * 4 + 64)) != RSG_OK) return s;
+    uint8_t *hd = (uint8_t *)ctx->h_desc[slot].p;
     memcpy(hd, spans.data(), sbytes);
     memcpy(hd + ooff, order.data(), order.size() * 4);
-    uint8_t *dd = (uint8_t *)ctx->d_desc[0].p;
-    RSG_HIP(ctx, hipMemcpyAsync(dd, hd, ooff + order.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    uint8_t *dd = (uint8_t *)ctx->d_desc[slot].p;
+    RSG_HIP(ctx, hipMemcpyAsync(dd, hd, ooff + order.size() * 4, hipMemcpyHostToDevice, stream));
     RSG_HIP(ctx, rsg::launch_file_sums((const uint8_t *)d_arena, arena_bytes, (const rsg::FileSpan *)dd,
                                        (const uint32_t *)(dd + ooff), (uint32_t)spans.size(), (uint32_t)mode,
-                                       (uint32_t)seed, (uint8_t *)d_out, ctx->stream));
+                                       (uint32_t)seed, (uint8_t *)d_out, stream));
     return RSG_OK;
+}
+
+}  // namespace rsgh
+
+namespace {
+
+rsg_status launch(rsg_ctx *ctx, const void *d_arena, uint64_t arena_bytes, const std::vector<rsg::FileSpan> &spans,
+                  int32_t mode, int32_t seed, void *d_out) {
+    return launch_file_sums_async(ctx, d_arena, arena_bytes, spans, mode, seed, d_out, 0, ctx->stream);
 }
 
 }  // namespace

@@ -12,6 +12,7 @@
 // 16-byte loads (any alignment, funnel-shifted), eight chunks in flight.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "rsg_internal.h"
 #include "rsg_md4.h"
@@ -104,20 +105,39 @@ __device__ __forceinline__ void fs_ring(const uint8_t *p0, uint32_t sh, uint64_t
     }
 }
 
-__global__ __launch_bounds__(64) void file_sums_kernel(const uint8_t *__restrict__ arena, uint64_t arena_bytes,
-                                                       const FileSpan *__restrict__ files,
-                                                       const uint32_t *__restrict__ order, uint32_t nfiles,
-                                                       uint32_t mode, uint32_t seed, uint8_t *__restrict__ out) {
-    const uint32_t lane_file = blockIdx.x * blockDim.x + threadIdx.x;
-    if (lane_file >= nfiles) return;
-    const uint32_t fi = order[lane_file];
-    const FileSpan F = files[fi];
+// Tail of a message of L bytes whose last chunk's words are in X: r = L % 64
+// message bytes, 0x80, zeros, the 64-bit bit length (RFC 1320); one or two
+// compressions.
+__device__ __forceinline__ void fs_tail(uint32_t X[16], uint64_t L, uint32_t h[4]) {
+    const uint32_t r = (uint32_t)(L & 63u), kd = r >> 2, rb = r & 3u;
+    const uint32_t keep = rb ? ((1u << (8 * rb)) - 1u) : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++)
+        X[k] = k < kd ? X[k] : (k == kd ? ((X[k] & keep) | (0x80u << (8 * rb))) : 0u);
+    const uint64_t bits = L << 3;
+    if (r < 56) {
+        X[14] = (uint32_t)bits;
+        X[15] = (uint32_t)(bits >> 32);
+        md4_compress(h, X);
+    } else {
+        md4_compress(h, X);
+#pragma unroll
+        for (int k = 0; k < 14; k++) X[k] = 0;
+        X[14] = (uint32_t)bits;
+        X[15] = (uint32_t)(bits >> 32);
+        md4_compress(h, X);
+    }
+}
+
+// Whole message of one file with the lane's own loads: MD4(file) (pre = 0) or
+// MD4(int32_LE(seed) || file) (pre = 4).  The ring path for most files; the
+// guarded single-chunk path for a file ending at the arena's very end.
+__device__ __forceinline__ void fs_hash_lane(const uint8_t *__restrict__ arena, uint64_t arena_bytes, FileSpan F,
+                                             uint64_t pre, uint32_t seed, uint32_t h[4]) {
     const uint8_t *d = arena + F.offset;
     const uintptr_t end = (uintptr_t)(arena + arena_bytes);
-    const uint64_t pre = mode == 1 ? 4u : 0u;  // prefix bytes (the seed)
     const uint64_t L = F.len + pre;             // message length
     const uint64_t nfull = L >> 6;
-    uint32_t h[4];
     md4_init(h);
     uint32_t X[16];
     uint64_t c = 0;
@@ -142,25 +162,153 @@ __global__ __launch_bounds__(64) void file_sums_kernel(const uint8_t *__restrict
         if (pre && nfull == 0) fs_seeded_head(d, end, seed, X);
         else fs_load_chunk(d + 64 * nfull - pre, end, X);
     }
-    // tail: r = L % 64 message bytes, 0x80, zeros, 64-bit bit length (RFC 1320)
-    const uint32_t r = (uint32_t)(L & 63u), kd = r >> 2, rb = r & 3u;
-    const uint32_t keep = rb ? ((1u << (8 * rb)) - 1u) : 0u;
-#pragma unroll
-    for (uint32_t k = 0; k < 16; k++)
-        X[k] = k < kd ? X[k] : (k == kd ? ((X[k] & keep) | (0x80u << (8 * rb))) : 0u);
-    const uint64_t bits = L << 3;
-    if (r < 56) {
-        X[14] = (uint32_t)bits;
-        X[15] = (uint32_t)(bits >> 32);
-        md4_compress(h, X);
-    } else {
-        md4_compress(h, X);
-#pragma unroll
-        for (int k = 0; k < 14; k++) X[k] = 0;
-        X[14] = (uint32_t)bits;
-        X[15] = (uint32_t)(bits >> 32);
-        md4_compress(h, X);
+    fs_tail(X, L, h);
+}
+
+__global__ __launch_bounds__(64) void file_sums_kernel(const uint8_t *__restrict__ arena, uint64_t arena_bytes,
+                                                       const FileSpan *__restrict__ files,
+                                                       const uint32_t *__restrict__ order, uint32_t nfiles,
+                                                       uint32_t mode, uint32_t seed, uint8_t *__restrict__ out) {
+    const uint32_t lane_file = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane_file >= nfiles) return;
+    const uint32_t fi = order[lane_file];
+    uint32_t h[4];
+    fs_hash_lane(arena, arena_bytes, files[fi], mode == 1 ? 4u : 0u, seed, h);
+    uint32_t *o = reinterpret_cast<uint32_t *>(out + 16ull * fi);
+    o[0] = h[0]; o[1] = h[1]; o[2] = h[2]; o[3] = h[3];
+}
+
+// ---------------------------------------------------------------- staged variant
+// The ring kernel above gathers every 16-byte load from 64 different files
+// (64 cache lines per wave instruction): the CU's address path, not HBM,
+// bounds it (27 % of 8 TB/s on cfg4's files).  Here a wave's 64 files
+// stream through a private LDS slab, 256 bytes of every file per segment, by
+// LDS DMA: instruction i, lane l fills slab bytes [1024 i + 16 l, +16) =
+// unit u = (64 i + l) % 17 of file j = (64 i + l) / 17, i.e. four files'
+// 272-byte pieces per instruction (a piece starts at the file's first byte
+// rounded down to 4; the 17th unit feeds the funnel shift).
+// global_load_lds takes a 64-bit address per lane, so a wave's files may lie
+// anywhere in an arena of any size (a buffer descriptor's 31-bit offsets
+// would confine them to 2 GiB).  Waves with a file whose needed bytes run
+// past the arena's end hash with the ring path above.  A unit a lane does not need
+// (its file is done) re-reads the unit's segment-0 bytes, which lie inside
+// the arena by that check.
+// Seeded mode: message word 0 is the seed, word w >= 1 is data word w - 1,
+// so message chunk c = (carry, data words 16 c .. 16 c + 14) with carry =
+// the data word before them -- the data stream is read from the file's own
+// start, never before it.
+constexpr uint32_t kFsUnits = 17;
+constexpr uint32_t kFsPiece = 16 * kFsUnits;  // 272 bytes of LDS per file
+constexpr uint32_t kFsSlab = 64 * kFsPiece;   // 17408 bytes per wave
+constexpr uint32_t kFsDma = kFsSlab / 1024;   // 17 DMA instructions per segment (vmcnt(17) below)
+static_assert(kFsDma == 17, "the segment wait counts 17 DMA instructions");
+
+template <bool SEEDED>
+__global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict__ arena, uint64_t arena_bytes,
+                                                       const FileSpan *__restrict__ files,
+                                                       const uint32_t *__restrict__ order, uint32_t nfiles,
+                                                       uint32_t seed, uint8_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab[2 * kFsSlab];  // two segments in flight
+    const uint32_t lane = threadIdx.x;
+    const uint32_t lane_file = blockIdx.x * 64 + lane;
+    const bool active = lane_file < nfiles;
+    const uint32_t fi = active ? order[lane_file] : order[blockIdx.x * 64];
+    const FileSpan F = files[fi];
+    const uint64_t pre = SEEDED ? 4u : 0u;
+    const uint64_t L = F.len + pre;
+    const uint64_t nfull = L >> 6;                 // the tail chunk's index
+    const uint64_t nseg64 = nfull / 4 + 1;         // segments through the tail chunk
+    const uint32_t sh = (uint32_t)(F.offset & 3u);
+    const uint64_t fstart = F.offset - sh;         // data read from here (4-byte aligned)
+    // staged when every lane's needed bytes [fstart, fstart + 256 nseg + 16)
+    // lie inside the arena (segment counts kept to 32 bits)
+    const bool ok = nseg64 < (1ull << 31) && fstart + 256 * nseg64 + 16 <= arena_bytes;
+    if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
+        if (!active) return;
+        uint32_t h[4];
+        fs_hash_lane(arena, arena_bytes, F, pre, seed, h);
+        uint32_t *o = reinterpret_cast<uint32_t *>(out + 16ull * fi);
+        o[0] = h[0]; o[1] = h[1]; o[2] = h[2]; o[3] = h[3];
+        return;
     }
+    const uint32_t nseg = active ? (uint32_t)nseg64 : 0u;
+    uint32_t smax = nseg;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, m, 64));
+    const uint32_t S = rfl32(smax);
+    // per DMA instruction i: this lane's unit (file j, unit u), its address
+    // at segment 0 and the segments it is needed for
+    const uint8_t *ua[kFsDma];
+    uint32_t un[kFsDma];
+#pragma unroll
+    for (uint32_t i = 0; i < kFsDma; i++) {
+        const uint32_t idx = 64u * i + lane, j = idx / kFsUnits, u = idx - kFsUnits * j;
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)fstart, (int)j, 64);
+        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(fstart >> 32), (int)j, 64);
+        ua[i] = arena + (((uint64_t)hi << 32) | lo) + 16u * u;
+        un[i] = (uint32_t)__shfl((int)nseg, (int)j, 64);
+    }
+#define RSG_FS_DMA(S_, SL_)                                                                                    \
+    do {                                                                                                       \
+        uint8_t *d_ = slab + (SL_) * kFsSlab;                                                                  \
+        _Pragma("unroll") for (uint32_t i_ = 0; i_ < kFsDma; i_++) {                                           \
+            const uint8_t *a_ = ua[i_] + ((S_) < un[i_] ? 256ull * (S_) : 0ull);                              \
+            __builtin_amdgcn_global_load_lds((const void *)a_, (__attribute__((address_space(3))) void *)(d_ + 1024u * i_), \
+                                             16, 0, 2);                                                        \
+        }                                                                                                      \
+    } while (0)
+    uint32_t R[4 * kFsUnits];
+#define RSG_FS_READ(SL_)                                                                                       \
+    do {                                                                                                       \
+        const uint8_t *mine = slab + (SL_) * kFsSlab + lane * kFsPiece;                                         \
+        _Pragma("unroll") for (int q_ = 0; q_ < (int)kFsUnits; q_++) {                                         \
+            const uint4 v_ = *reinterpret_cast<const uint4 *>(mine + 16 * q_);                                 \
+            R[4 * q_ + 0] = v_.x; R[4 * q_ + 1] = v_.y; R[4 * q_ + 2] = v_.z; R[4 * q_ + 3] = v_.w;             \
+        }                                                                                                      \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                     \
+    } while (0)
+    // Two segments in flight per wave: segment s + 2 is issued into the slab
+    // segment s was just copied out of (one in flight left only ~1.2 us of
+    // hashing to cover each segment's HBM latency)
+    RSG_FS_DMA(0u, 0u);
+    if (S > 1) RSG_FS_DMA(1u, 1u);
+    uint32_t h[4];
+    md4_init(h);
+    uint32_t carry = seed;  // seeded: the message word before the chunk's data words
+    uint32_t X[16];
+    const uint32_t tail_seg = (uint32_t)(nfull / 4), tail_i = (uint32_t)(nfull % 4);
+#pragma unroll 1
+    for (uint32_t s = 0; s < S; s++) {
+        // segment s has landed once at most the younger segment's 17 DMAs are pending
+        if (s + 1 < S) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        RSG_FS_READ(s & 1u);
+        if (s + 2 < S) RSG_FS_DMA(s + 2, s & 1u);  // in flight while segments s and s + 1 hash
+        if (s <= tail_seg && s < nseg) {
+#pragma unroll
+            for (uint32_t i = 0; i < 4; i++) {
+                if (s == tail_seg && i > tail_i) break;
+                uint32_t D[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) D[k] = __builtin_amdgcn_alignbyte(R[16 * i + k + 1], R[16 * i + k], sh);
+                if (SEEDED) {
+                    X[0] = carry;
+#pragma unroll
+                    for (int k = 1; k < 16; k++) X[k] = D[k - 1];
+                    carry = D[15];
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 16; k++) X[k] = D[k];
+                }
+                if (s == tail_seg && i == tail_i) break;  // the tail chunk's words stay in X
+                md4_compress(h, X);
+            }
+        }
+    }
+#undef RSG_FS_DMA
+#undef RSG_FS_READ
+    if (!active) return;
+    fs_tail(X, L, h);
     uint32_t *o = reinterpret_cast<uint32_t *>(out + 16ull * fi);
     o[0] = h[0]; o[1] = h[1]; o[2] = h[2]; o[3] = h[3];
 }
@@ -170,8 +318,20 @@ hipError_t launch_file_sums(const uint8_t *arena, uint64_t arena_bytes, const Fi
     if (nfiles == 0) return hipSuccess;
     // one-wave workgroups: the longest-first lane order then gives an LPT
     // schedule over the SIMDs (the second round of waves takes the shorter files)
-    hipLaunchKernelGGL(file_sums_kernel, dim3((nfiles + 63) / 64), dim3(64), 0, stream, arena, arena_bytes, files,
-                       order, nfiles, mode, seed, out);
+    static const int variant = [] {  // RSG_FILESUMS_KERNEL: 0 = ring, 1 = staged (default)
+        const char *e = getenv("RSG_FILESUMS_KERNEL");
+        return e ? atoi(e) : 1;
+    }();
+    const dim3 grid((nfiles + 63) / 64), block(64);
+    if (variant == 0)
+        hipLaunchKernelGGL(file_sums_kernel, grid, block, 0, stream, arena, arena_bytes, files, order, nfiles, mode,
+                           seed, out);
+    else if (mode == 1)
+        hipLaunchKernelGGL(file_sums_staged<true>, grid, block, 0, stream, arena, arena_bytes, files, order, nfiles,
+                           seed, out);
+    else
+        hipLaunchKernelGGL(file_sums_staged<false>, grid, block, 0, stream, arena, arena_bytes, files, order, nfiles,
+                           seed, out);
     return hipGetLastError();
 }
 

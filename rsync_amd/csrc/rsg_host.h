@@ -55,6 +55,15 @@ struct rsg_ctx {
     // multi-GPU
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    // kernel timing (rsg_set_kernel_timing): event pairs bracketing the
+    // sender's kernels on the streams they run on, kind 0 = roll, 1 =
+    // confirmation (block sums of the windows + resolve)
+    struct TimedSpan {
+        hipEvent_t a, b;
+        int kind;
+    };
+    bool timing = false;
+    std::vector<TimedSpan> spans;
 };
 
 // Plan of a block-sum batch (host side + resident device copies).
@@ -104,6 +113,17 @@ struct CopyJob {
     uint64_t n;
 };
 void parallel_copy(const std::vector<CopyJob> &jobs);
+
+// Whole-file sums (rsg_files.cpp): descriptors through ctx->h_desc[slot] /
+// d_desc[slot], kernel on `stream`, asynchronous.
+rsg_status launch_file_sums_async(rsg_ctx *ctx, const void *d_arena, uint64_t arena_bytes,
+                                  const std::vector<rsg::FileSpan> &spans, int32_t mode, int32_t seed, void *d_out,
+                                  int slot, hipStream_t stream);
+
+// Kernel timing helpers (no-ops unless ctx->timing): begin records an event
+// on `stream` and returns it; end records the closing event.
+hipEvent_t timed_begin(rsg_ctx *ctx, hipStream_t stream);
+void timed_end(rsg_ctx *ctx, hipEvent_t a, hipStream_t stream, int kind);
 
 // Upload plan descriptors to (grown) device buffers and launch the kernel.
 rsg_status launch_plan(rsg_ctx *ctx, const HostPlan &plan, const void *d_files, const void *d_wg,

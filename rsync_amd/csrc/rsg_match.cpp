@@ -35,6 +35,32 @@ using rsg::kScanTile;
 using rsg::TileAgg;
 using rsg::TilePrefix;
 
+namespace rsgh {
+
+hipEvent_t timed_begin(rsg_ctx *ctx, hipStream_t stream) {
+    if (!ctx->timing) return nullptr;
+    hipEvent_t a = nullptr;
+    if (hipEventCreate(&a) != hipSuccess) return nullptr;
+    if (hipEventRecord(a, stream) != hipSuccess) {
+        hipEventDestroy(a);
+        return nullptr;
+    }
+    return a;
+}
+
+void timed_end(rsg_ctx *ctx, hipEvent_t a, hipStream_t stream, int kind) {
+    if (!a) return;
+    hipEvent_t b = nullptr;
+    if (hipEventCreate(&b) != hipSuccess || hipEventRecord(b, stream) != hipSuccess) {
+        if (b) hipEventDestroy(b);
+        hipEventDestroy(a);
+        return;
+    }
+    ctx->spans.push_back({a, b, kind});
+}
+
+}  // namespace rsgh
+
 namespace {
 
 constexpr uint32_t kCandCap = 1u << 22;      // candidates per roll launch (32 MiB)
@@ -153,6 +179,7 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
     RSG_HIP(ctx, hipMemcpyAsync(ctx->d_wg.p, plan.wg_file.data(), plan.wg_file.size() * sizeof(uint32_t),
                                 hipMemcpyHostToDevice, S.cst));
     if ((s = ensure_dev(ctx, ctx->d_fb[0], rsg::block_sums_scratch_bytes(plan.total_blocks))) != RSG_OK) return s;
+    hipEvent_t t0 = timed_begin(ctx, S.cst);
     if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, S.d_src, S.seed, ctx->d_out[0].p, ctx->d_fb[0].p,
                          S.cst)) != RSG_OK)
         return s;
@@ -164,6 +191,7 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
                                      plan.total_blocks, S.d_groups, S.d_hi16, S.d_sum2,
                                      S.head.count, S.head.block_len, S.head.rem, S.head.s2len,
                                      (int32_t *)ctx->d_res.p, S.cst));
+    timed_end(ctx, t0, S.cst, 1);
     if ((s = ensure_pin(ctx, ctx->h_out[0], plan.total_blocks * 4)) != RSG_OK) return s;
     const int32_t *found = (const int32_t *)ctx->h_out[0].p;
     RSG_HIP(ctx, hipMemcpyAsync(ctx->h_out[0].p, ctx->d_res.p, plan.total_blocks * 4, hipMemcpyDeviceToHost, S.cst));
@@ -382,10 +410,12 @@ rsg_status launch_range(Search &S, uint32_t lo, uint32_t hi) {
     rsg_ctx *ctx = S.ctx;
     SearchSlot &sl = *S.sl;
     RSG_HIP(ctx, hipMemsetAsync(sl.counts.p, 0, 4, S.st));
+    hipEvent_t t0 = timed_begin(ctx, S.st);
     RSG_HIP(ctx, rsg::launch_roll(S.d_src, S.size, (uint32_t)S.head.block_len, (uint32_t)S.head.rem, (uint64_t)S.end,
                                   lo, hi, (const TileAgg *)sl.agg.p, (const TilePrefix *)sl.prefix.p, S.ntiles,
                                   S.d_filter, S.d_table, S.bmask, (uint64_t *)sl.list.p, kCandCap,
                                   (uint32_t *)sl.counts.p, S.cus, S.fused, S.st));
+    timed_end(ctx, t0, S.st, 0);
     RSG_HIP(ctx, hipMemcpyAsync(sl.count.p, sl.counts.p, 4, hipMemcpyDeviceToHost, S.st));
     RSG_HIP(ctx, hipEventRecord(sl.rolled, S.st));
     return RSG_OK;
@@ -599,6 +629,36 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
 }  // namespace
 
 extern "C" {
+
+rsg_status rsg_set_kernel_timing(rsg_ctx *ctx, int32_t on) {
+    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    ctx->timing = on != 0;
+    return RSG_OK;
+}
+
+rsg_status rsg_kernel_times(rsg_ctx *ctx, double out[4], int32_t reset) {
+    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    RSG_HIP(ctx, hipSetDevice(ctx->device));
+    if (!out) return fail(ctx, RSG_ERR_INVALID, "out is NULL");
+    for (int k = 0; k < 4; k++) out[k] = 0;
+    for (const rsg_ctx::TimedSpan &t : ctx->spans) {
+        RSG_HIP(ctx, hipEventSynchronize(t.b));
+        float ms = 0;
+        RSG_HIP(ctx, hipEventElapsedTime(&ms, t.a, t.b));
+        out[2 * t.kind] += ms;
+        out[2 * t.kind + 1] += 1;
+    }
+    if (reset) {
+        for (const rsg_ctx::TimedSpan &t : ctx->spans) {
+            hipEventDestroy(t.a);
+            hipEventDestroy(t.b);
+        }
+        ctx->spans.clear();
+    }
+    return RSG_OK;
+}
 
 rsg_status rsg_hash_search_batch_device(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed) {
     if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");

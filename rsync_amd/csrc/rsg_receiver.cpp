@@ -11,6 +11,11 @@
 // seeded file-sum kernel (rsg_filesums.hip).
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
+#include <thread>
+#include <vector>
+
 #include "rsg_host.h"
 
 using namespace rsgh;
@@ -65,6 +70,39 @@ rsg_status apply(rsg_ctx *ctx, const uint8_t *tokens, uint64_t tokens_len, const
     return RSG_OK;
 }
 
+// Token application of many jobs on a few host threads (byte copying; each
+// job writes only its own output).  Sets every job's out_len / consumed /
+// status; returns nothing (failures are per job).
+void apply_jobs(rsg_recv_job *jobs, uint64_t i0, uint64_t i1, std::vector<uint64_t> &sum_at) {
+    static const int threads = [] {
+        const char *e = getenv("RSG_COPY_THREADS");
+        const int t = e ? atoi(e) : 8;
+        return std::max(1, std::min(t, 64));
+    }();
+    std::atomic<uint64_t> next{i0};
+    auto worker = [&] {
+        for (uint64_t k; (k = next.fetch_add(1)) < i1;) {
+            rsg_recv_job &j = jobs[k];
+            j.out_len = 0;
+            j.consumed = 0;
+            uint64_t at = 0;
+            rsg_status st = apply(nullptr, j.tokens, j.tokens_len, &j.head, j.basis, j.basis_len, j.out, j.out_cap,
+                                  &j.out_len, &at);
+            if (st == RSG_OK && at + 16 > j.tokens_len) st = RSG_ERR_INVALID;  // receiver.go:167-170
+            if (st == RSG_OK && j.out_len && !j.out) st = RSG_ERR_INVALID;
+            sum_at[k - i0] = at;
+            j.status = st;
+        }
+    };
+    uint64_t bytes = 0;
+    for (uint64_t k = i0; k < i1; k++) bytes += jobs[k].tokens_len;
+    const int nt = (int)std::min<uint64_t>((uint64_t)threads, std::min<uint64_t>(i1 - i0, 1 + bytes / (1ull << 20)));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; t++) pool.emplace_back(worker);
+    worker();
+    for (auto &t : pool) t.join();
+}
+
 }  // namespace
 
 extern "C" {
@@ -98,6 +136,118 @@ rsg_status rsg_receive_data(rsg_ctx *ctx, const uint8_t *tokens, uint64_t tokens
     if (consumed) *consumed = sum_at + 16;
     if (memcmp(local, tokens + sum_at, 16) != 0)  // receiver.go:171-173
         return fail(ctx, RSG_ERR_CORRUPT, "file corruption: whole-file sum mismatch");
+    return RSG_OK;
+}
+
+// Batched receiveData (receiver.go:98-188 for every file of a transfer):
+// batches of jobs (<= 256 MiB of rebuilt bytes) alternate between two slots.
+// For batch k: tokens applied on host threads into the callers' out buffers,
+// the rebuilt files staged into pinned memory (or DMA'd straight from out
+// when it is page-locked), H2D, the seeded whole-file sum of every file (one
+// lane per file), digests back -- all on the slot's stream, while the host
+// applies batch k+1.  Each job's status: RSG_OK, RSG_ERR_INVALID /
+// RSG_ERR_TRUNCATED from its token stream, RSG_ERR_CORRUPT on a sum mismatch
+// (receiver.go:171-173).
+rsg_status rsg_receive_data_batch(rsg_ctx *ctx, rsg_recv_job *jobs, uint64_t njobs, int32_t seed) {
+    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    RSG_HIP(ctx, hipSetDevice(ctx->device));
+    if (njobs && !jobs) return fail(ctx, RSG_ERR_INVALID, "jobs is NULL");
+    for (uint64_t q = 0; q < njobs; q++) jobs[q].status = RSG_OK;  // jobs a fatal error stops get its status
+    struct Drain {  // nothing outlives the call
+        rsg_ctx *c;
+        ~Drain() {
+            for (int k = 0; k < 2; k++) (void)hipStreamSynchronize(c->side[k]);
+        }
+    } drain{ctx};
+    const uint64_t kBatchBytes = 256ull << 20;
+    struct Slot {
+        uint64_t i0 = 0, i1 = 0;
+        std::vector<uint64_t> sum_at;
+        std::vector<uint64_t> lane;  // job of digest d, ~0 for jobs that failed before hashing
+        bool busy = false;
+    } slots[2];
+    auto finish = [&](Slot &sl, int k) -> rsg_status {
+        if (!sl.busy) return RSG_OK;
+        RSG_HIP(ctx, hipStreamSynchronize(ctx->side[k]));
+        const uint8_t *dig = (const uint8_t *)ctx->h_out[k].p;
+        for (uint64_t d = 0; d < sl.lane.size(); d++) {
+            rsg_recv_job &j = jobs[sl.lane[d]];
+            j.consumed = sl.sum_at[sl.lane[d] - sl.i0] + 16;
+            if (memcmp(dig + 16 * d, j.tokens + sl.sum_at[sl.lane[d] - sl.i0], 16) != 0) j.status = RSG_ERR_CORRUPT;
+        }
+        sl.busy = false;
+        return RSG_OK;
+    };
+    rsg_status fatal = RSG_OK;
+    uint64_t i = 0;
+    for (int k = 0; i < njobs; k ^= 1) {
+        Slot &sl = slots[k];
+        if ((fatal = finish(sl, k)) != RSG_OK) break;
+        // the batch: jobs until ~kBatchBytes of rebuilt bytes (bounded by
+        // out_cap, known before applying)
+        uint64_t i1 = i, est = 0;
+        while (i1 < njobs && (i1 == i || est + jobs[i1].out_cap <= kBatchBytes)) est += jobs[i1++].out_cap;
+        sl.i0 = i;
+        sl.i1 = i1;
+        sl.sum_at.assign(i1 - i, 0);
+        apply_jobs(jobs, i, i1, sl.sum_at);
+        sl.lane.clear();
+        std::vector<rsg::FileSpan> spans;
+        std::vector<CopyJob> copies;
+        uint64_t off = 0;
+        for (uint64_t q = i; q < i1; q++) {
+            if (jobs[q].status != RSG_OK) continue;
+            sl.lane.push_back(q);
+            spans.push_back({off, jobs[q].out_len});
+            if (jobs[q].out_len) copies.push_back({nullptr, jobs[q].out, jobs[q].out_len});
+            off += (jobs[q].out_len + 15) & ~15ull;
+        }
+        i = i1;
+        if (sl.lane.empty()) continue;
+        if ((fatal = ensure_dev(ctx, ctx->d_in[k], off + 16)) != RSG_OK) break;
+        if ((fatal = ensure_pin(ctx, ctx->h_in[k], off + 16)) != RSG_OK) break;
+        if ((fatal = ensure_dev(ctx, ctx->d_out[k], sl.lane.size() * 16)) != RSG_OK) break;
+        if ((fatal = ensure_pin(ctx, ctx->h_out[k], sl.lane.size() * 16)) != RSG_OK) break;
+        uint8_t *stage = (uint8_t *)ctx->h_in[k].p;
+        uint64_t at = 0;
+        for (size_t c = 0, d = 0; d < sl.lane.size(); d++) {
+            const uint64_t n = jobs[sl.lane[d]].out_len;
+            if (n) copies[c++].dst = stage + at;
+            at += (n + 15) & ~15ull;
+        }
+        parallel_copy(copies);
+        hipStream_t st = ctx->side[k];
+        hipError_t e = hipMemcpyAsync(ctx->d_in[k].p, stage, off, hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) {
+            fatal = hip_fail(ctx, e, "receive batch H2D");
+            break;
+        }
+        if ((fatal = launch_file_sums_async(ctx, ctx->d_in[k].p, off, spans, RSG_FILESUM_SEEDED, seed,
+                                            ctx->d_out[k].p, k, st)) != RSG_OK)
+            break;
+        e = hipMemcpyAsync(ctx->h_out[k].p, ctx->d_out[k].p, sl.lane.size() * 16, hipMemcpyDeviceToHost, st);
+        if (e != hipSuccess) {
+            fatal = hip_fail(ctx, e, "receive batch D2H");
+            break;
+        }
+        sl.busy = true;
+    }
+    for (int k = 0; k < 2 && fatal == RSG_OK; k++) fatal = finish(slots[k], k);
+    if (fatal != RSG_OK) {
+        for (uint64_t q = 0; q < njobs; q++)
+            if (jobs[q].status == RSG_OK) jobs[q].status = fatal;
+        return fatal;
+    }
+    for (uint64_t q = 0; q < njobs; q++) {
+        if (jobs[q].status != RSG_OK) {
+            const int32_t st = jobs[q].status;
+            return fail(ctx, st, "job %llu: %s", (unsigned long long)q,
+                        st == RSG_ERR_CORRUPT ? "file corruption: whole-file sum mismatch"
+                                              : (st == RSG_ERR_TRUNCATED ? "output capacity too small"
+                                                                         : "bad token stream"));
+        }
+    }
     return RSG_OK;
 }
 

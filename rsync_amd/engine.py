@@ -355,6 +355,38 @@ class Engine:
                                    n.value, ctypes.byref(n), ctypes.byref(used)), self.ctx)
         return out[: n.value].tobytes(), used.value
 
+    def receive_data_batch(self, jobs, seed: int, raise_on_error: bool = True):
+        """RecvFiles' per-file receiveData calls (receiver.go:18-188) in one
+        batched call: jobs = [(stream, head, basis)] as receive_data takes
+        them.  The whole-file sums of all files are checked together on the
+        GPU (one lane per file).  Returns [(file bytes, consumed)], or with
+        raise_on_error=False [(status, file bytes, consumed)]."""
+        n = len(jobs)
+        arr = (_lib.RecvJob * max(n, 1))()
+        keep, outs = [], []
+        for k, (stream, head, basis) in enumerate(jobs):
+            t = _u8(stream)
+            b = _u8(basis) if basis is not None else None
+            h = head if isinstance(head, SumHead) else SumHead(*head)
+            need, used = ctypes.c_uint64(), ctypes.c_uint64()
+            bp, bl = (_ptr(b), b.size) if b is not None else (ctypes.c_void_p(0), 0)
+            st = lib.rsg_apply_tokens(_ptr(t), t.size, ctypes.byref(h), bp, bl, None, 0, ctypes.byref(need),
+                                      ctypes.byref(used))
+            cap = need.value if st in (_lib.OK, _lib.ERR_TRUNCATED) else 0
+            out = np.empty(max(cap, 1), dtype=np.uint8)
+            keep += [t, b]
+            outs.append(out)
+            j = arr[k]
+            j.tokens, j.tokens_len, j.head = _ptr(t).value, t.size, h
+            j.basis, j.basis_len = bp.value, bl
+            j.out, j.out_cap = out.ctypes.data, cap
+        st = lib.rsg_receive_data_batch(self.ctx, arr, n, _i32(seed))
+        if raise_on_error:
+            check(st, self.ctx)
+            return [(outs[k][: arr[k].out_len].tobytes(), arr[k].consumed) for k in range(n)]
+        return [(arr[k].status, outs[k][: arr[k].out_len].tobytes() if arr[k].status == _lib.OK else b"",
+                 arr[k].consumed) for k in range(n)]
+
     def file_sums_device(self, arena: DeviceBuffer, files: Sequence[Tuple[int, int]], mode: int = _lib.FILESUM_PLAIN,
                          seed: int = 0, out: Optional[DeviceBuffer] = None) -> DeviceBuffer:
         """Same for files already in device memory: files = [(offset, len)];
@@ -437,6 +469,16 @@ class Engine:
             check(st, self.ctx)
             return [res(k) for k in range(n)]
         return [(arr[k].status, res(k) if arr[k].status == _lib.OK else []) for k in range(n)]
+
+    def set_kernel_timing(self, on: bool = True):
+        """rsg_set_kernel_timing: bracket the sender's kernels with HIP events."""
+        check(lib.rsg_set_kernel_timing(self.ctx, int(on)), self.ctx)
+
+    def kernel_times(self, reset: bool = True) -> dict:
+        """Totals since the last reset: roll_ms, roll_launches, confirm_ms, confirm_batches."""
+        o = (ctypes.c_double * 4)()
+        check(lib.rsg_kernel_times(self.ctx, o, int(reset)), self.ctx)
+        return {"roll_ms": o[0], "roll_launches": int(o[1]), "confirm_ms": o[2], "confirm_batches": int(o[3])}
 
     # ------------------------------------------------------------ multi-GPU
     @staticmethod

@@ -4,7 +4,8 @@
  * A cgo binding (go/rsyncgpu) sees the structs of rsg.h with
  * the C compiler's layout, so this program pins that layout for every struct
  * a caller fills or reads -- rsg_sum_head, rsg_file, rsg_match,
- * rsg_search_job, rsg_fd_file -- at compile time (_Static_assert) and prints
+ * rsg_search_job, rsg_fd_file, rsg_shard_batch, rsg_recv_job --
+ * at compile time (_Static_assert) and prints
  * it as JSON for tests/test_c_abi.py to compare with the ctypes mirror.
  *
  * Modes:
@@ -68,6 +69,25 @@ PIN(rsg_fd_file, len, 16);
 PIN(rsg_fd_file, block_len, 24);
 PIN(rsg_fd_file, reserved, 28);
 
+SIZE(rsg_shard_batch, 32);
+PIN(rsg_shard_batch, plan, 0);
+PIN(rsg_shard_batch, record_offset, 8);
+PIN(rsg_shard_batch, send_bytes, 16);
+PIN(rsg_shard_batch, recv_offsets, 24);
+
+SIZE(rsg_recv_job, 88);
+PIN(rsg_recv_job, tokens, 0);
+PIN(rsg_recv_job, tokens_len, 8);
+PIN(rsg_recv_job, head, 16);
+PIN(rsg_recv_job, basis, 32);
+PIN(rsg_recv_job, basis_len, 40);
+PIN(rsg_recv_job, out, 48);
+PIN(rsg_recv_job, out_cap, 56);
+PIN(rsg_recv_job, out_len, 64);
+PIN(rsg_recv_job, consumed, 72);
+PIN(rsg_recv_job, status, 80);
+PIN(rsg_recv_job, reserved, 84);
+
 #define F(T, M) printf("\"%s\": [%zu, %zu]", #M, offsetof(T, M), sizeof(((T *)0)->M))
 
 static void layout(void) {
@@ -90,6 +110,17 @@ static void layout(void) {
     printf(" \"rsg_fd_file\": {\"size\": %zu, ", sizeof(rsg_fd_file));
     F(rsg_fd_file, fd); printf(", "); F(rsg_fd_file, idx); printf(", "); F(rsg_fd_file, offset); printf(", ");
     F(rsg_fd_file, len); printf(", "); F(rsg_fd_file, block_len); printf(", "); F(rsg_fd_file, reserved);
+    printf("},\n");
+    printf(" \"rsg_shard_batch\": {\"size\": %zu, ", sizeof(rsg_shard_batch));
+    F(rsg_shard_batch, plan); printf(", "); F(rsg_shard_batch, record_offset); printf(", ");
+    F(rsg_shard_batch, send_bytes); printf(", "); F(rsg_shard_batch, recv_offsets);
+    printf("},\n");
+    printf(" \"rsg_recv_job\": {\"size\": %zu, ", sizeof(rsg_recv_job));
+    F(rsg_recv_job, tokens); printf(", "); F(rsg_recv_job, tokens_len); printf(", "); F(rsg_recv_job, head);
+    printf(", "); F(rsg_recv_job, basis); printf(", "); F(rsg_recv_job, basis_len); printf(", ");
+    F(rsg_recv_job, out); printf(", "); F(rsg_recv_job, out_cap); printf(", "); F(rsg_recv_job, out_len);
+    printf(", "); F(rsg_recv_job, consumed); printf(", "); F(rsg_recv_job, status); printf(", ");
+    F(rsg_recv_job, reserved);
     printf("}}\n");
 }
 

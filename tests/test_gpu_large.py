@@ -182,6 +182,13 @@ def test_cfg4_full_set(eng):
         got = recs.download(cnt * 20, offset=plan.first_record[f] * 20).tobytes()
         assert got == orc.block_sums(cases.splitmix64_bytes(f + 1, lengths[f]), 700, cases.SEED), f
     assert fb == (0, 0), fb
+    # the seeded whole-file sums of the same 100 000 files (match.go:52-53)
+    import rsync_amd
+    out = eng.file_sums_device(arena, list(zip(offs, lengths)), rsync_amd.FILESUM_SEEDED, cases.SEED)
+    dig = out.download(16 * NF).reshape(-1, 16)
+    for f in picks:
+        assert dig[f].tobytes() == orc.file_sum(1, cases.SEED, cases.splitmix64_bytes(f + 1, lengths[f])), f
+    out.free()
     arena.free()
     recs.free()
     plan.close()
@@ -236,6 +243,25 @@ def test_fallback_census_counts(eng, variant, kind):
     fb = eng.block_sums_fallbacks(reset=True)
     assert recs.download(total * 20).tobytes() == orc.block_sums(d, 700, cases.SEED)
     assert fb[kind] >= 1 and fb[1 - kind] == 0, fb
+
+
+@pytest.mark.parametrize("unaligned", [False, True])
+def test_file_sums_past_4gib(eng, unaligned):
+    """Whole-file MD4 (both modes, rsyncchecksum.go:60-66 and
+    match.go:52-53) of the ~1000 small files around 2 GiB and 4 GiB of the
+    5 GiB arena in one call: a wave's 64 files (longest first) lie on both
+    sides of 4 GiB, so the staged kernel's per-lane 64-bit DMA addresses span
+    more than 2 GiB."""
+    import rsync_amd
+    arena, files, kinds = _arena(eng, unaligned)
+    small = [f for f, k in zip(files, kinds) if k == "small"]
+    for mode, seed in ((rsync_amd.FILESUM_PLAIN, 0), (rsync_amd.FILESUM_SEEDED, cases.SEED)):
+        out = eng.file_sums_device(arena, small, mode, seed)
+        got = out.download(16 * len(small)).reshape(-1, 16)
+        out.free()
+        for i, (off, n) in enumerate(small):
+            want = orc.file_sum(mode, seed, cases.splitmix64_range(STREAM_SEED, off, n))
+            assert got[i].tobytes() == want, (i, off, n, mode)
 
 
 def test_release_arenas(eng):

@@ -3,6 +3,7 @@ fixtures and the C oracle.  Everything goes through the C-ABI."""
 import hashlib
 import json
 import os
+import struct
 
 import numpy as np
 import pytest
@@ -143,7 +144,7 @@ def test_delta_round_trip_on_gpu(eng, seed_case):
     assert e.value.status == rsync_amd._lib.ERR_CORRUPT
 
 
-def _random_job(k, seed):
+def _random_delta(k, seed):
     rng = np.random.default_rng(500 + k)
     n = int(rng.integers(1, 400_000))
     basis = cases.splitmix64_bytes(510 + k, n)
@@ -151,7 +152,12 @@ def _random_job(k, seed):
                        n_ins=int(rng.integers(0, 4)), n_del=int(rng.integers(0, 4)))
     blen = int(rng.choice([0, 7, 333, 700, 4096, 40000]))
     head, s1, s2 = basis_sums(basis, blen, seed)
-    return src, head, s1, s2, orc.stable_targets(s1)
+    return src, basis, head, s1, s2, orc.stable_targets(s1)
+
+
+def _random_job(k, seed):
+    src, _, head, s1, s2, tg = _random_delta(k, seed)
+    return src, head, s1, s2, tg
 
 
 def test_batch_host_vs_oracle(eng):
@@ -224,3 +230,46 @@ def test_long_blocks_prefix_pass(eng, blen):
     want, _, _ = orc.hash_search(src, head, s1, s2, tg, seed)
     assert len(want) > 0
     assert eng.hash_search(src, head, s1, s2, tg, seed) == want
+
+
+def test_receive_data_batch(eng):
+    """rsg_receive_data_batch over a transfer's worth of files (RecvFiles'
+    per-file receiveData, receiver.go:18-188): 48 random delta streams plus
+    edge jobs -- a flipped whole-file sum byte (RSG_ERR_CORRUPT, receiver.go:
+    171-173), a stream cut before its sum, a match token without a basis
+    (RSG_ERR_INVALID), an empty file -- each job's status and bytes equal the
+    oracle's receive_data; the good jobs are unaffected by the bad ones."""
+    import rsync_amd
+    from rsync_amd import _lib
+    seed = 0x5EED
+    jobs, want = [], []
+    for k in range(48):
+        src, basis, head, s1, s2, tg = _random_delta(700 + k, seed)
+        _, tok, fsum = orc.hash_search(src, head, s1, s2, tg, seed)
+        stream = tok + fsum
+        jobs.append((stream, head, basis))
+        want.append((_lib.OK,) + orc.receive_data(stream, head, basis, seed))
+    # corrupt sum, short stream, match without basis, empty file
+    src, basis, head, s1, s2, tg = _random_delta(800, seed)
+    _, tok, fsum = orc.hash_search(src, head, s1, s2, tg, seed)
+    bad = bytearray(tok + fsum)
+    bad[-3] ^= 1
+    jobs.append((bytes(bad), head, basis))
+    want.append((_lib.ERR_CORRUPT, None, None))
+    jobs.append(((tok + fsum)[:-4], head, basis))
+    want.append((_lib.ERR_INVALID, None, None))
+    jobs.append((struct.pack("<ii", -1, 0) + bytes(16), (1, 700, 16, 0), None))
+    want.append((_lib.ERR_INVALID, None, None))
+    empty_sum = orc.file_sum(1, seed, np.zeros(0, np.uint8))
+    jobs.append((struct.pack("<i", 0) + empty_sum, (0, 700, 16, 0), None))
+    want.append((_lib.OK, b"", 4 + 16))
+    got = eng.receive_data_batch(jobs, seed, raise_on_error=False)
+    for k, ((st, data, used), (wst, wdata, wused)) in enumerate(zip(got, want)):
+        assert st == wst, k
+        if wst == _lib.OK:
+            assert data == wdata and used == wused, k
+    with pytest.raises(rsync_amd.RsgError) as e:
+        eng.receive_data_batch(jobs, seed)
+    assert e.value.status == _lib.ERR_CORRUPT
+    assert [r[:2] for r in eng.receive_data_batch([j for j, w in zip(jobs, want) if w[0] == _lib.OK], seed)] \
+        == [(w[1], w[2]) for w in want if w[0] == _lib.OK]
