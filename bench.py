@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--windows", type=int, default=5,
+                    help="timed windows of exactly --steps steps; the line reports the median window")
     ap.add_argument("--warmup-ms", type=float, default=200.0,
                     help="keep warming up (beyond --warmup steps) until this much time has passed: the "
                          "GPU takes ~15 ms of back-to-back launches to reach its steady memory clock")
@@ -118,28 +120,31 @@ def main():
         if warm % 20 == 0:
             eng.synchronize(sptr)
     eng.synchronize(sptr)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
-        step(i)
-    ev1.record(stream)
-    eng.synchronize(sptr)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    wall = t1 - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps
-    if world > 1:
-        tt = torch.tensor([wall, kernel_ms], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        wall, kernel_ms = float(tt[0]), float(tt[1])
 
+    def window():
+        """EXACTLY args.steps steps, bracketed by a barrier + synchronize on
+        both sides; -> (wall s, HIP-event kernel ms per step), max over ranks."""
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for i in range(args.steps):
+            step(i)
+        ev1.record(stream)
+        eng.synchronize(sptr)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        w, k = time.perf_counter() - t0, ev0.elapsed_time(ev1) / args.steps
+        return max_over_ranks(world, w, k)
+
+    # The headline is the median of --windows timed windows (each exactly K
+    # steps), so one optimistic window cannot set it.
+    wins = sorted(window() for _ in range(max(1, args.windows)))
+    wall, kernel_ms = wins[len(wins) // 2]
     extra = {}
     if args.ab:
         from rsync_amd import _lib
@@ -192,6 +197,7 @@ def main():
             "warmup": args.warmup,
             "warmup_effective": warm,
             "ms_per_step": round(wall * 1e3 / args.steps, 4),
+            "windows_ms_per_step": [round(w * 1e3 / args.steps, 4) for w, _ in wins],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -202,6 +208,8 @@ def main():
                        "records_per_gpu": plan.total_records, "parallelism": f"files sharded, {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": "profiles/traffic.json: rocprofv3 PMC passes of this bench command "
+                                           "(FETCH_SIZE x2 + WRITE_SIZE per launch), not measured in this run",
                          "kernel_ms": round(kernel_ms, 4),
                          "algorithmic_bytes_per_launch": int(in_bytes + out_bytes)},
             "cpu_baseline": cpu,
@@ -568,7 +576,9 @@ def bench_sender(args, rank, world, local):
                                        "launches": kt["roll_launches"],
                                        "algorithmic_bytes_per_launch": int(src_bytes),
                                        "confirm_ms_per_batch": round(confirm_ms, 4),
-                                       "confirm_batches": kt["confirm_batches"]},
+                                       "confirm_batches": kt["confirm_batches"],
+                                       "candidates_per_launch": kt["candidates"] // max(kt["roll_launches"], 1),
+                                       "windows_confirmed_per_launch": kt["windows"] // max(kt["roll_launches"], 1)},
                           "oracle_parity_file0": parity,
                           "cpu_baseline": cpu}), flush=True)
     eng.close()

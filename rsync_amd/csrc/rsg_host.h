@@ -64,6 +64,7 @@ struct rsg_ctx {
     };
     bool timing = false;
     std::vector<TimedSpan> spans;
+    uint64_t stat_candidates = 0, stat_windows = 0;  // roll candidates read back, windows confirmed
 };
 
 // Plan of a block-sum batch (host side + resident device copies).

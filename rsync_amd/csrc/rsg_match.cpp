@@ -180,6 +180,7 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
                                 hipMemcpyHostToDevice, S.cst));
     if ((s = ensure_dev(ctx, ctx->d_fb[0], rsg::block_sums_scratch_bytes(plan.total_blocks))) != RSG_OK) return s;
     hipEvent_t t0 = timed_begin(ctx, S.cst);
+    if (ctx->timing) ctx->stat_windows += idx.size();
     if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, S.d_src, S.seed, ctx->d_out[0].p, ctx->d_fb[0].p,
                          S.cst)) != RSG_OK)
         return s;
@@ -446,6 +447,7 @@ rsg_status finish(Search &S) {
             span = std::max<uint32_t>(1, (hi - lo) / 2);
             continue;
         }
+        if (ctx->timing) ctx->stat_candidates += n;
         C.resize(n);
         if (n) {
             RSG_HIP(ctx, hipMemcpyAsync(C.data(), sl.list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, S.copy));
@@ -637,12 +639,14 @@ rsg_status rsg_set_kernel_timing(rsg_ctx *ctx, int32_t on) {
     return RSG_OK;
 }
 
-rsg_status rsg_kernel_times(rsg_ctx *ctx, double out[4], int32_t reset) {
+rsg_status rsg_kernel_times(rsg_ctx *ctx, double out[6], int32_t reset) {
     if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
     std::lock_guard<std::recursive_mutex> lock(ctx->mu);
     RSG_HIP(ctx, hipSetDevice(ctx->device));
     if (!out) return fail(ctx, RSG_ERR_INVALID, "out is NULL");
-    for (int k = 0; k < 4; k++) out[k] = 0;
+    for (int k = 0; k < 6; k++) out[k] = 0;
+    out[4] = (double)ctx->stat_candidates;
+    out[5] = (double)ctx->stat_windows;
     for (const rsg_ctx::TimedSpan &t : ctx->spans) {
         RSG_HIP(ctx, hipEventSynchronize(t.b));
         float ms = 0;
@@ -656,6 +660,7 @@ rsg_status rsg_kernel_times(rsg_ctx *ctx, double out[4], int32_t reset) {
             hipEventDestroy(t.b);
         }
         ctx->spans.clear();
+        ctx->stat_candidates = ctx->stat_windows = 0;
     }
     return RSG_OK;
 }

@@ -475,10 +475,13 @@ class Engine:
         check(lib.rsg_set_kernel_timing(self.ctx, int(on)), self.ctx)
 
     def kernel_times(self, reset: bool = True) -> dict:
-        """Totals since the last reset: roll_ms, roll_launches, confirm_ms, confirm_batches."""
-        o = (ctypes.c_double * 4)()
+        """Totals since the last reset: roll_ms, roll_launches, confirm_ms,
+        confirm_batches, candidates (offsets the rolls returned), windows
+        (confirmed by the strong-sum kernel)."""
+        o = (ctypes.c_double * 6)()
         check(lib.rsg_kernel_times(self.ctx, o, int(reset)), self.ctx)
-        return {"roll_ms": o[0], "roll_launches": int(o[1]), "confirm_ms": o[2], "confirm_batches": int(o[3])}
+        return {"roll_ms": o[0], "roll_launches": int(o[1]), "confirm_ms": o[2], "confirm_batches": int(o[3]),
+                "candidates": int(o[4]), "windows": int(o[5])}
 
     # ------------------------------------------------------------ multi-GPU
     @staticmethod

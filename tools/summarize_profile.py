@@ -1,44 +1,52 @@
 #!/usr/bin/env python3
 """Summarize a tools/profile.sh run (rocprofv3 kernel trace + PMC passes) into
-profiles/<tag>_summary.json and profiles/traffic.json.
+profiles/<tag>_summary.json (and, for the default cfg2 bench kernel,
+profiles/traffic.json).
 
 HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reports
 half the bytes of wide coalesced reads on gfx950, so it is doubled;
 WRITE_SIZE (KB) is exact for 16-B streaming stores.  Counters come from
-separate --pmc passes (never combined with trace domains)."""
+separate --pmc passes (never combined with trace domains).
+
+    tools/summarize_profile.py <tag> [--kernel SUBSTRING] [--no-traffic]
+"""
+import argparse
 import csv
 import glob
 import json
 import os
-import sys
 from collections import defaultdict
 
-KERNEL = "block_sums"
 
-
-def kernel_rows(path):
-    return [r for r in csv.DictReader(open(path)) if KERNEL in r["Kernel_Name"]]
-
-
-def main(tag, outdir="profiles"):
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--kernel", default="block_sums", help="substring of the kernel name to summarize")
+    ap.add_argument("--no-traffic", action="store_true", help="do not rewrite profiles/traffic.json")
+    ap.add_argument("--outdir", default="profiles")
+    a = ap.parse_args()
+    tag, kernel, outdir = a.tag, a.kernel, a.outdir
     src = f"gpurun_out/prof_{tag}"
+
+    def rows(path):
+        return [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+
     stats = list(csv.DictReader(open(glob.glob(f"{src}/trace/*kernel_stats.csv")[0])))
     trace = [r for r in csv.DictReader(open(glob.glob(f"{src}/trace/*kernel_trace.csv")[0]))]
     counters = defaultdict(list)
-    names = {}
     for f in glob.glob(f"{src}/pmc_*/*counter_collection.csv"):
-        for r in kernel_rows(f):
+        for r in rows(f):
             counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
-            names[r["Counter_Name"]] = r["Kernel_Name"]
     avg = {k: sum(v) / len(v) for k, v in counters.items()}
-    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in trace if KERNEL in r["Kernel_Name"]]
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in trace if kernel in r["Kernel_Name"]]
     steady = sorted(durs)[len(durs) // 4: 3 * len(durs) // 4] if len(durs) >= 8 else durs
     out = {
         "tag": tag,
+        "kernel_filter": kernel,
         "kernel_stats": [{k: r[k] for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs")} for r in stats],
-        "block_sums_dispatches": len(durs),
-        "block_sums_us_mean": round(sum(durs) / max(len(durs), 1), 2),
-        "block_sums_us_interquartile_mean": round(sum(steady) / max(len(steady), 1), 2),
+        "dispatches": len(durs),
+        "us_mean": round(sum(durs) / max(len(durs), 1), 2),
+        "us_interquartile_mean": round(sum(steady) / max(len(steady), 1), 2),
         "pmc_mean_per_dispatch": {k: round(v, 1) for k, v in sorted(avg.items())},
     }
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
@@ -47,14 +55,16 @@ def main(tag, outdir="profiles"):
         out["hbm_bytes_per_launch"] = {"fetch_corrected": int(fetch), "write": int(write), "total": int(fetch + write),
                                        "note": "FETCH_SIZE*2 (gfx950 wide-read correction) + WRITE_SIZE, KB->B"}
     if "GRBM_GUI_ACTIVE" in avg and durs:
-        out["effective_clock_ghz"] = round(avg["GRBM_GUI_ACTIVE"] / 8 / (out["block_sums_us_mean"] * 1e3), 3)
+        out["effective_clock_ghz"] = round(avg["GRBM_GUI_ACTIVE"] / 8 / (out["us_mean"] * 1e3), 3)
+    if "SQ_ACTIVE_INST_VALU" in avg and "SQ_BUSY_CYCLES" in avg:
+        out["note_units"] = "SQ_* wave/active counters count quad-cycles (MI355X_MICROARCH.md constants table)"
     os.makedirs(outdir, exist_ok=True)
     json.dump(out, open(f"{outdir}/{tag}_summary.json", "w"), indent=1)
-    if "hbm_bytes_per_launch" in out:
+    if "hbm_bytes_per_launch" in out and kernel == "block_sums" and not a.no_traffic:
         json.dump({"block_sums_kernel_cfg2_bytes_per_launch": out["hbm_bytes_per_launch"]["total"],
                    "source": f"profiles/{tag}_summary.json"}, open(f"{outdir}/traffic.json", "w"), indent=1)
     print(json.dumps(out, indent=1)[:3000])
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:])
+    main()
