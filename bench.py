@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--no-delivery", action="store_true", help="skip the pipelined gather / D2H delivery modes")
     ap.add_argument("--ab", action="store_true", help="A/B the block-sum kernel variants (interleaved rounds)")
-    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5", "filesums"],
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5", "filesums", "receive"],
                     help="cfg2 = receiver block sums (the metric); cfg3 = sender match, reported separately")
     ap.add_argument("--cfg3-files", type=int, default=10)
     ap.add_argument("--batches", type=int, default=4,
@@ -93,6 +93,8 @@ def main():
         return bench_long(args, rank, world, local)
     if args.workload == "filesums":
         return bench_filesums(args, rank, world, local)
+    if args.workload == "receive":
+        return bench_receive(args, rank, world, local)
 
     eng = rsync_amd.Engine(local)
     stream = torch.cuda.Stream(device=local)
@@ -873,6 +875,68 @@ def bench_filesums(args, rank, world, local):
         "cpu_baseline": {"value": round(done / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
                          "sample": f"{k} random files of the set, oracle/rsg_oracle.c orc_file_sum (plain), "
                                    f"1 thread, {t_cpu:.1f} s"}}), flush=True)
+    eng.close()
+
+
+def bench_receive(args, rank, world, local):
+    """receiveData (receiver.go:98-188) latency and batch
+    rate: token application on the host, the seeded whole-file MD4
+    (receiver.go:117-120) on the GPU.  MD4 is one serial chain per file, so a
+    single file runs on ONE GPU lane: its latency is measured for a 1 MiB and
+    a 1 GiB file next to the one-core host MD4 rate (the C restatement); the
+    batched call (rsg_receive_data_batch) hashes many files in parallel.
+    Streams: every block of an identical basis matched (all tokens are
+    matches), i.e. the whole file is rebuilt from the basis."""
+    import rsync_amd
+    import cases
+    from oracle import oracle as orc
+    eng = rsync_amd.Engine(local)
+    seed = SEED
+    res = {}
+
+    def stream_for(data):
+        head = rsync_amd.sum_sizes_sqroot(data.size)
+        B = head.block_len
+        matches = [(i * B, i) for i in range(head.count)]
+        c0 = time.perf_counter()
+        fsum = orc.file_sum(1, seed, data)  # the sender's whole-file sum; also the CPU MD4 baseline
+        t_cpu = time.perf_counter() - c0
+        return rsync_amd.encode_tokens(data, head, matches) + fsum, head, t_cpu
+
+    for name, size in (("1MiB", 1 << 20), ("1GiB", 1 << 30)):
+        data = cases.splitmix64_bytes(77, size)
+        stream, head, t_cpu = stream_for(data)
+        if size <= (1 << 20):
+            eng.receive_data(stream, head, data, seed)  # warm-up
+        t0 = time.perf_counter()
+        out, used = eng.receive_data(stream, head, data, seed)
+        dt = time.perf_counter() - t0
+        res[f"single_{name}"] = {"s": round(dt, 4), "gib_s": round(size / dt / GIB, 4),
+                                 "equal": out == data.tobytes() and used == len(stream),
+                                 "cpu_md4_1core_s": round(t_cpu, 4),
+                                 "cpu_md4_1core_gib_s": round(size / t_cpu / GIB, 4)}
+        del data, stream, out
+    # batch: 1024 files of 1 MiB (one lane each)
+    n, size = 1024, 1 << 20
+    files = [cases.splitmix64_bytes(1000 + f, size) for f in range(n)]
+    jobs, t_cpu = [], 0.0
+    for d in files:
+        st, head, tc = stream_for(d)
+        jobs.append((st, head, d))
+        t_cpu += tc
+    eng.receive_data_batch(jobs[:16], seed)
+    t0 = time.perf_counter()
+    got = eng.receive_data_batch(jobs, seed)
+    dt = time.perf_counter() - t0
+    res["batch_1024x1MiB"] = {"s": round(dt, 4), "gib_s": round(n * size / dt / GIB, 3),
+                              "equal": all(g[0] == d.tobytes() for g, d in zip(got, files)),
+                              "cpu_md4_1core_gib_s": round(n * size / t_cpu / GIB, 4)}
+    print(json.dumps({"metric": "receiveData (token application + seeded whole-file MD4 check)",
+                      "value": res["batch_1024x1MiB"]["gib_s"], "unit": "GiB/s", "n_gpus": 1,
+                      "higher_is_better": True, "dtype": "u32",
+                      "data": "synthetic (splitmix64 files, identical basis: every block a match token)",
+                      "config": {"workload": "receive: single 1 MiB / 1 GiB files (latency), 1024 x 1 MiB batch"},
+                      "results": res}), flush=True)
     eng.close()
 
 

@@ -203,7 +203,7 @@ constexpr uint32_t kFsSlab = 64 * kFsPiece;   // 17408 bytes per wave
 constexpr uint32_t kFsDma = kFsSlab / 1024;   // 17 DMA instructions per segment (vmcnt(17) below)
 static_assert(kFsDma == 17, "the segment wait counts 17 DMA instructions");
 
-template <bool SEEDED>
+template <bool SEEDED, int AUX>
 __global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict__ arena, uint64_t arena_bytes,
                                                        const FileSpan *__restrict__ files,
                                                        const uint32_t *__restrict__ order, uint32_t nfiles,
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict
         _Pragma("unroll") for (uint32_t i_ = 0; i_ < kFsDma; i_++) {                                           \
             const uint8_t *a_ = ua[i_] + ((S_) < un[i_] ? 256ull * (S_) : 0ull);                              \
             __builtin_amdgcn_global_load_lds((const void *)a_, (__attribute__((address_space(3))) void *)(d_ + 1024u * i_), \
-                                             16, 0, 2);                                                        \
+                                             16, 0, AUX);                                                      \
         }                                                                                                      \
     } while (0)
     uint32_t R[4 * kFsUnits];
@@ -318,20 +318,28 @@ hipError_t launch_file_sums(const uint8_t *arena, uint64_t arena_bytes, const Fi
     if (nfiles == 0) return hipSuccess;
     // one-wave workgroups: the longest-first lane order then gives an LPT
     // schedule over the SIMDs (the second round of waves takes the shorter files)
-    static const int variant = [] {  // RSG_FILESUMS_KERNEL: 0 = ring, 1 = staged (default)
+    // RSG_FILESUMS_KERNEL: 0 = ring, 1 = staged with nt DMA, 2 = staged with
+    // the default cache policy (A/B)
+    static const int variant = [] {
         const char *e = getenv("RSG_FILESUMS_KERNEL");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 2;
     }();
     const dim3 grid((nfiles + 63) / 64), block(64);
     if (variant == 0)
         hipLaunchKernelGGL(file_sums_kernel, grid, block, 0, stream, arena, arena_bytes, files, order, nfiles, mode,
                            seed, out);
+    else if (variant == 1 && mode == 1)
+        hipLaunchKernelGGL((file_sums_staged<true, 2>), grid, block, 0, stream, arena, arena_bytes, files, order,
+                           nfiles, seed, out);
+    else if (variant == 1)
+        hipLaunchKernelGGL((file_sums_staged<false, 2>), grid, block, 0, stream, arena, arena_bytes, files, order,
+                           nfiles, seed, out);
     else if (mode == 1)
-        hipLaunchKernelGGL(file_sums_staged<true>, grid, block, 0, stream, arena, arena_bytes, files, order, nfiles,
-                           seed, out);
+        hipLaunchKernelGGL((file_sums_staged<true, 0>), grid, block, 0, stream, arena, arena_bytes, files, order,
+                           nfiles, seed, out);
     else
-        hipLaunchKernelGGL(file_sums_staged<false>, grid, block, 0, stream, arena, arena_bytes, files, order, nfiles,
-                           seed, out);
+        hipLaunchKernelGGL((file_sums_staged<false, 0>), grid, block, 0, stream, arena, arena_bytes, files, order,
+                           nfiles, seed, out);
     return hipGetLastError();
 }
 

@@ -89,6 +89,29 @@ __device__ __forceinline__ void vec_sums(const uint32_t w[4], int32_t &v1, int32
     }
 }
 
+// Inclusive wave64 prefix sum with DPP (row_shr 1/2/4/8 inside each 16-lane
+// row, then row_bcast 15 / 31 across rows): VALU only, where __shfl_up
+// lowers to one ds_bpermute (an LDS instruction) per step.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
+// Sum over the 16 lanes of each row (every row holds the same 16 values):
+// DPP row scan, then lane 15's value, wave-uniform.
+__device__ __forceinline__ uint32_t row16_sum(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
+}
+
 template <typename T>
 __device__ __forceinline__ T block_reduce_add(T v, T *scratch) {
 #pragma unroll
@@ -378,23 +401,19 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         // own and shifted byte sums, sum x and sum (local index) * x
         uint32_t v[4] = {(uint32_t)o1, (uint32_t)o2 + lo * (uint32_t)o1, (uint32_t)s1,
                          (uint32_t)s2 + lo * (uint32_t)s1};
-        uint32_t incl[4] = {v[0], v[1], v[2], v[3]};
+        uint32_t incl[4];
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const uint32_t o = __shfl_up(incl[c], d, 64);
-                if (lane >= (uint32_t)d) incl[c] += o;
-            }
-        }
+        for (int c = 0; c < 4; c++) incl[c] = wave_incl_scan(v[c]);
         if (lane == 63) wsum[parity][wave] = make_uint4(incl[0], incl[1], incl[2], incl[3]);
         __syncthreads();
-        // all 16 partials at once (broadcast reads, no dependent chain)
-        uint4 add = make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (uint32_t w = 0; w < kWaves; w++) {
-            const uint4 p = wsum[parity][w];
-            if (w < wave) { add.x += p.x; add.y += p.y; add.z += p.z; add.w += p.w; }
+        // the partials of the waves before this one: lane l of every row
+        // reads wave l's (zero for l >= wave), each row sums its 16 lanes
+        uint4 add;
+        {
+            const uint32_t w = lane & 15u;
+            uint4 p = wsum[parity][w];
+            if (w >= wave) p = make_uint4(0, 0, 0, 0);
+            add = make_uint4(row16_sum(p.x), row16_sum(p.y), row16_sum(p.z), row16_sum(p.w));
         }
         if (fused && t != t_begin) {  // the previous tile's last lane left this tile's start window
             const uint2 c = carry[parity];
