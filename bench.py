@@ -151,9 +151,8 @@ def main():
     if args.ab:
         from rsync_amd import _lib
         # (product variant, diagnostic) pairs; diagnostics write meaningless records
-        names = {(1, 0): "staged", (2, 0): "park", (1, 1): "diag_staged_memory_only",
-                 (1, 2): "diag_staged_hash_only", (1, 3): "diag_park_memory_only", (1, 4): "diag_park_hash_only",
-                 (1, 6): "diag_linear_read_ldsdma"}
+        names = {(2, 0): "park", (1, 3): "diag_park_memory_only", (1, 4): "diag_park_hash_only",
+                 (1, 6): "diag_linear_read_ldsdma", (1, 5): "diag_linear_read_plain"}
         res = {v: [] for v in names}
         for _ in range(5):
             for v in names:
@@ -847,8 +846,19 @@ def bench_filesums(args, rank, world, local):
         for i in range(steps):
             call(i)
         dt = (time.perf_counter() - t0) / steps
+        # the kernel alone: HIP events around each launch on its stream (a
+        # separate pass, so the per-call time above carries no event cost)
+        eng.set_kernel_timing(True)
+        eng.kernel_times(reset=True)
+        for i in range(steps):
+            call(i)
+        kt = eng.kernel_times(reset=True)
+        eng.set_kernel_timing(False)
+        kms = kt["filesums_ms"] / max(kt["filesums_launches"], 1)
         res[name] = {"ms_per_call": round(dt * 1e3, 4), "gib_s": round(total / dt / GIB, 2),
-                     "hbm_frac_8tbs": round(total / dt / 1e9 / HBM_PEAK_GBS, 4)}
+                     "hbm_frac_8tbs": round(total / dt / 1e9 / HBM_PEAK_GBS, 4),
+                     "kernel_ms": round(kms, 4),
+                     "kernel_hbm_frac_8tbs": round(total / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     # parity (plain mode is the last one run, on arena (steps - 1) & 1) and the CPU baseline
     from oracle import oracle as orc
     last = arenas[(steps - 1) & 1]
@@ -872,6 +882,12 @@ def bench_filesums(args, rank, world, local):
         "config": {"workload": "whole-file MD4 over cfg4's 100k files (4-64 KiB)", "files": NF, "total_bytes": total,
                    "call": "rsg_file_sums_device, descriptors uploaded and waited on per call"},
         "modes": res, "spot_parity": {"files": min(k, 256), "equal": parity},
+        "roofline": {"bound": "hbm", "kernel": "file_sums_staged<seeded>",
+                     "achieved": round(total / (res["seeded"]["kernel_ms"] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": res["seeded"]["kernel_hbm_frac_8tbs"], "traffic": None,
+                     "kernel_ms": res["seeded"]["kernel_ms"], "algorithmic_bytes_per_launch": int(total),
+                     "note": "value = per call (descriptor staging + lane order + upload + launch + wait); "
+                             "roofline = the kernel alone (HIP events)"},
         "cpu_baseline": {"value": round(done / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
                          "sample": f"{k} random files of the set, oracle/rsg_oracle.c orc_file_sum (plain), "
                                    f"1 thread, {t_cpu:.1f} s"}}), flush=True)

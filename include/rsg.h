@@ -272,16 +272,17 @@ typedef struct rsg_search_job {
 rsg_status rsg_hash_search_batch_device(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed);
 rsg_status rsg_hash_search_batch_host(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed);
 
-/* Kernel timing of the sender path for roofline measurements (bench.py):
- * while on, every roll launch and every confirmation batch (block sums of the
- * windows + resolve) of ctx is bracketed by HIP events on the stream it runs
- * on.  rsg_kernel_times waits for them and returns out[0] = total roll ms,
- * out[1] = roll launches, out[2] = total confirmation ms, out[3] =
- * confirmation batches, out[4] = candidate offsets the rolls returned,
- * out[5] = windows confirmed; reset != 0 drops the recorded events and
- * zeroes the counts. */
+/* Kernel timing for roofline measurements (bench.py): while on, every roll
+ * launch and confirmation batch (block sums of the windows + resolve) of the
+ * sender and every whole-file-sum launch of ctx is bracketed by HIP events on
+ * the stream it runs on.  rsg_kernel_times waits for them and returns
+ * out[0] = total roll ms, out[1] = roll launches, out[2] = total confirmation
+ * ms, out[3] = confirmation batches, out[4] = candidate offsets the rolls
+ * returned, out[5] = windows confirmed, out[6] = total whole-file-sum kernel
+ * ms, out[7] = its launches; reset != 0 drops the recorded events and zeroes
+ * the counts. */
 rsg_status rsg_set_kernel_timing(rsg_ctx *ctx, int32_t on);
-rsg_status rsg_kernel_times(rsg_ctx *ctx, double out[6], int32_t reset);
+rsg_status rsg_kernel_times(rsg_ctx *ctx, double out[8], int32_t reset);
 
 /* Token stream of simpleSendToken (token.go:4-31) as matched() emits it
  * (match.go:233-282): literal runs in <= 256 KiB pieces (int32 LE n + n bytes),

@@ -9,7 +9,9 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librsg.so")
+# RSG_LIB_PATH: another in-tree build of the same ABI (same-box A/B of kernel
+# revisions, tools/); default the package's own librsg.so
+LIB_PATH = os.environ.get("RSG_LIB_PATH") or os.path.join(HERE, "librsg.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

@@ -27,48 +27,70 @@ rsg_status check_mode(rsg_ctx *ctx, int32_t mode) {
 
 // Longest first, so the 64 lanes of a wave hash similar numbers of chunks
 // (and the one-wave workgroups form an LPT schedule).  Only approximate order
-// matters: a counting sort on the length in KiB (capped), stable, O(n).
-std::vector<uint32_t> lane_order(const std::vector<rsg::FileSpan> &spans) {
-    constexpr uint64_t kKeys = 1u << 16;
-    auto key = [](uint64_t len) { return (uint32_t)std::min<uint64_t>(len >> 10, kKeys - 1); };
-    std::vector<uint32_t> count(kKeys + 1, 0);
-    for (const rsg::FileSpan &f : spans) count[kKeys - 1 - key(f.len)]++;  // descending length
+// matters: a counting sort on the length in KiB (capped), stable, O(n),
+// written straight into the pinned staging.
+void lane_order(const rsg::FileSpan *spans, uint32_t n, uint32_t *order) {
+    constexpr uint32_t kKeys = 1u << 16;
+    auto key = [](uint64_t len) { return kKeys - 1 - (uint32_t)std::min<uint64_t>(len >> 10, kKeys - 1); };
+    static thread_local std::vector<uint32_t> count;
+    count.assign(kKeys + 1, 0);
+    uint32_t kmin = kKeys, kmax = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t k = key(spans[i].len);  // descending length
+        count[k]++;
+        kmin = std::min(kmin, k);
+        kmax = std::max(kmax, k);
+    }
     uint32_t at = 0;
-    for (uint64_t k = 0; k <= kKeys; k++) {
+    for (uint32_t k = kmin; k <= kmax && n; k++) {
         const uint32_t c = count[k];
         count[k] = at;
         at += c;
     }
-    std::vector<uint32_t> order(spans.size());
-    for (uint32_t i = 0; i < (uint32_t)spans.size(); i++) order[count[kKeys - 1 - key(spans[i].len)]++] = i;
-    return order;
+    for (uint32_t i = 0; i < n; i++) order[count[key(spans[i].len)]++] = i;
 }
 
 }  // namespace
 
 namespace rsgh {
 
-// Upload spans + order through ctx->h_desc[slot] / d_desc[slot] and launch
-// the whole-file sums on `stream` (asynchronous; the slot's staging must not
-// be reused before the stream has passed this point).
+// Pinned staging for n spans (and their lane order) in ctx->h_desc[slot]:
+// callers write the spans there directly.
+rsg_status file_spans_stage(rsg_ctx *ctx, uint64_t n, int slot, rsg::FileSpan **spans) {
+    const uint64_t ooff = (n * sizeof(rsg::FileSpan) + 63) & ~63ull;
+    rsg_status s;
+    if ((s = ensure_dev(ctx, ctx->d_desc[slot], ooff + n * 4 + 64)) != RSG_OK) return s;
+    if ((s = ensure_pin(ctx, ctx->h_desc[slot], ooff + n * 4 + 64)) != RSG_OK) return s;
+    *spans = (rsg::FileSpan *)ctx->h_desc[slot].p;
+    return RSG_OK;
+}
+
+// The n spans staged in ctx->h_desc[slot]: lane order next to them, one
+// upload to d_desc[slot], the whole-file sums on `stream` (asynchronous; the
+// slot's staging must not be reused before the stream has passed this point).
+rsg_status launch_file_sums_staged(rsg_ctx *ctx, const void *d_arena, uint64_t arena_bytes, uint64_t n,
+                                   int32_t mode, int32_t seed, void *d_out, int slot, hipStream_t stream) {
+    const uint64_t ooff = (n * sizeof(rsg::FileSpan) + 63) & ~63ull;
+    uint8_t *hd = (uint8_t *)ctx->h_desc[slot].p;
+    lane_order((const rsg::FileSpan *)hd, (uint32_t)n, (uint32_t *)(hd + ooff));
+    uint8_t *dd = (uint8_t *)ctx->d_desc[slot].p;
+    RSG_HIP(ctx, hipMemcpyAsync(dd, hd, ooff + n * 4, hipMemcpyHostToDevice, stream));
+    hipEvent_t t0 = timed_begin(ctx, stream);
+    RSG_HIP(ctx, rsg::launch_file_sums((const uint8_t *)d_arena, arena_bytes, (const rsg::FileSpan *)dd,
+                                       (const uint32_t *)(dd + ooff), (uint32_t)n, (uint32_t)mode, (uint32_t)seed,
+                                       (uint8_t *)d_out, stream));
+    timed_end(ctx, t0, stream, 2);
+    return RSG_OK;
+}
+
 rsg_status launch_file_sums_async(rsg_ctx *ctx, const void *d_arena, uint64_t arena_bytes,
                                   const std::vector<rsg::FileSpan> &spans, int32_t mode, int32_t seed, void *d_out,
                                   int slot, hipStream_t stream) {
-    const std::vector<uint32_t> order = lane_order(spans);
-    const uint64_t sbytes = spans.size() * sizeof(rsg::FileSpan);
-    const uint64_t ooff = (sbytes + 63) & ~63ull;
+    rsg::FileSpan *st = nullptr;
     rsg_status s;
-    if ((s = ensure_dev(ctx, ctx->d_desc[slot], ooff + order.size() * 4 + 64)) != RSG_OK) return s;
-    if ((s = ensure_pin(ctx, ctx->h_desc[slot], ooff + order.size() * 4 + 64)) != RSG_OK) return s;
-    uint8_t *hd = (uint8_t *)ctx->h_desc[slot].p;
-    memcpy(hd, spans.data(), sbytes);
-    memcpy(hd + ooff, order.data(), order.size() * 4);
-    uint8_t *dd = (uint8_t *)ctx->d_desc[slot].p;
-    RSG_HIP(ctx, hipMemcpyAsync(dd, hd, ooff + order.size() * 4, hipMemcpyHostToDevice, stream));
-    RSG_HIP(ctx, rsg::launch_file_sums((const uint8_t *)d_arena, arena_bytes, (const rsg::FileSpan *)dd,
-                                       (const uint32_t *)(dd + ooff), (uint32_t)spans.size(), (uint32_t)mode,
-                                       (uint32_t)seed, (uint8_t *)d_out, stream));
-    return RSG_OK;
+    if ((s = file_spans_stage(ctx, spans.size(), slot, &st)) != RSG_OK) return s;
+    if (!spans.empty()) memcpy(st, spans.data(), spans.size() * sizeof(rsg::FileSpan));
+    return launch_file_sums_staged(ctx, d_arena, arena_bytes, spans.size(), mode, seed, d_out, slot, stream);
 }
 
 }  // namespace rsgh
@@ -94,13 +116,15 @@ rsg_status rsg_file_sums_device(rsg_ctx *ctx, const void *d_arena, uint64_t aren
     if (nfiles == 0) return RSG_OK;
     if (nfiles > 0xFFFFFFFFull) return fail(ctx, RSG_ERR_INVALID, "too many files");
     if (!files || !d_out || (arena_bytes && !d_arena)) return fail(ctx, RSG_ERR_INVALID, "NULL argument");
-    std::vector<rsg::FileSpan> spans(nfiles);
+    rsg::FileSpan *spans = nullptr;
+    if ((s = file_spans_stage(ctx, nfiles, 0, &spans)) != RSG_OK) return s;
     for (uint64_t i = 0; i < nfiles; i++) {
         if (files[i].offset > arena_bytes || files[i].len > arena_bytes - files[i].offset)
             return fail(ctx, RSG_ERR_INVALID, "file %llu lies outside the arena", (unsigned long long)i);
         spans[i] = {files[i].offset, files[i].len};
     }
-    if ((s = launch(ctx, d_arena, arena_bytes, spans, mode, seed, d_out)) != RSG_OK) return s;
+    if ((s = launch_file_sums_staged(ctx, d_arena, arena_bytes, nfiles, mode, seed, d_out, 0, ctx->stream)) != RSG_OK)
+        return s;
     RSG_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return RSG_OK;
 }

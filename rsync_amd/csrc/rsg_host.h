@@ -55,9 +55,9 @@ struct rsg_ctx {
     // multi-GPU
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
-    // kernel timing (rsg_set_kernel_timing): event pairs bracketing the
-    // sender's kernels on the streams they run on, kind 0 = roll, 1 =
-    // confirmation (block sums of the windows + resolve)
+    // kernel timing (rsg_set_kernel_timing): event pairs bracketing kernels
+    // on the streams they run on, kind 0 = roll, 1 = confirmation (block
+    // sums of the windows + resolve), 2 = whole-file sums
     struct TimedSpan {
         hipEvent_t a, b;
         int kind;

@@ -64,6 +64,9 @@ struct TilePrefix {  // at a tile start: P = sum_{i<j} x_i, Q = sum_{i<j} i * x_
 __host__ __device__ inline uint32_t filter_hash(uint32_t sum) { return ((sum << 13) | (sum >> 19)) ^ sum; }
 __host__ __device__ inline uint32_t filter_word(uint32_t h) { return (h >> 2) & 0x7fffu; }  // 2^15 words
 __host__ __device__ inline uint32_t filter_mask(uint32_t h) { return (1u << ((h >> 22) & 31u)) | (1u << (h >> 27)); }
+// k = 3 variant (RSG_FILTER_K3=1, A/B): a third bit from h[17..21]
+__host__ __device__ inline uint32_t filter_mask3(uint32_t h) { return filter_mask(h) | (1u << ((h >> 17) & 31u)); }
+bool roll_filter_k3();  // the filter's bits per sum: 3 when RSG_FILTER_K3=1 (read once), else 2
 
 // Exact table of basis weak sums: buckets of kBucketWays u64 entries
 // {sum1 << 32 | flags}; a sum lives in bucket hash1 or hash2.

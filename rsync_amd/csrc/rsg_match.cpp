@@ -310,9 +310,10 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
         else keys.push_back({S.groups[i].first, f});
     }
     std::vector<uint32_t> bitmap(rsg::kFilterBits / 32, 0);
+    const bool k3 = rsg::roll_filter_k3();
     for (auto &kv : keys) {
         const uint32_t h = rsg::filter_hash(kv.first);
-        bitmap[rsg::filter_word(h)] |= rsg::filter_mask(h);
+        bitmap[rsg::filter_word(h)] |= k3 ? rsg::filter_mask3(h) : rsg::filter_mask(h);
     }
     uint32_t nb = 16;
     while (nb < keys.size() / 2) nb <<= 1;
@@ -639,20 +640,21 @@ rsg_status rsg_set_kernel_timing(rsg_ctx *ctx, int32_t on) {
     return RSG_OK;
 }
 
-rsg_status rsg_kernel_times(rsg_ctx *ctx, double out[6], int32_t reset) {
+rsg_status rsg_kernel_times(rsg_ctx *ctx, double out[8], int32_t reset) {
     if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
     std::lock_guard<std::recursive_mutex> lock(ctx->mu);
     RSG_HIP(ctx, hipSetDevice(ctx->device));
     if (!out) return fail(ctx, RSG_ERR_INVALID, "out is NULL");
-    for (int k = 0; k < 6; k++) out[k] = 0;
+    for (int k = 0; k < 8; k++) out[k] = 0;
     out[4] = (double)ctx->stat_candidates;
     out[5] = (double)ctx->stat_windows;
     for (const rsg_ctx::TimedSpan &t : ctx->spans) {
         RSG_HIP(ctx, hipEventSynchronize(t.b));
         float ms = 0;
         RSG_HIP(ctx, hipEventElapsedTime(&ms, t.a, t.b));
-        out[2 * t.kind] += ms;
-        out[2 * t.kind + 1] += 1;
+        const int slot = t.kind == 2 ? 6 : 2 * t.kind;  // out[4..5] are the sender's counts
+        out[slot] += ms;
+        out[slot + 1] += 1;
     }
     if (reset) {
         for (const rsg_ctx::TimedSpan &t : ctx->spans) {

@@ -21,6 +21,7 @@
 //              greedy order of match.go (rsg_match.cpp).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "rsg_internal.h"
 
@@ -246,6 +247,11 @@ __device__ __forceinline__ uint32_t table_flags(const uint64_t *__restrict__ tab
 
 constexpr uint32_t kQueueCap = 96;  // bitmap hits parked per wave and tile before the exact probes
 
+// PIPE: the interior offsets go in groups of 4 whose filter-word reads are
+// issued one group ahead of their tests (the reads of group g+1 are in flight
+// while group g is tested and parked); otherwise groups of 8, each read, then
+// waited for, then tested.  K3: three filter bits per sum (filter_mask3).
+template <bool PIPE, bool K3>
 __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
     uint32_t tile_hi, const TileAgg *__restrict__ agg, const TilePrefix *__restrict__ pre, uint32_t ntiles,
@@ -482,7 +488,38 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         // computed and fetched first (one LDS wait per group, not per offset),
         // then the hits are parked.
         constexpr int G = 8;
-        if (q0 + kScanTile <= end && q0 + kScanTile + B <= size) {
+        if (PIPE && q0 + kScanTile <= end && q0 + kScanTile + B <= size) {
+            const int32_t negB16 = -(int32_t)(B & 0xffffu);
+            constexpr int H = 4;
+            uint32_t sA[H], wA[H];
+            auto issue = [&](int g0, uint32_t *sm, uint32_t *wd) {
+#pragma unroll
+                for (int jj = 0; jj < H; jj++) {
+                    const int j = g0 + jj;
+                    sm[jj] = __builtin_amdgcn_perm(W2, W1, 0x05040100u);  // match.go:106
+                    wd[jj] = bitmap[filter_word(filter_hash(sm[jj]))];
+                    W1 += (uint32_t)sub_sx8(S[j >> 2], O[j >> 2], j & 3);
+                    W2 = W2 + (uint32_t)mul_sx8(negB16, O[j >> 2], j & 3) + W1;
+                }
+            };
+            issue(0, sA, wA);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int g0 = 0; g0 < (int)kRollPerThread; g0 += H) {
+                uint32_t sB[H], wB[H];
+                if (g0 + H < (int)kRollPerThread) issue(g0 + H, sB, wB);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int jj = 0; jj < H; jj++) {
+                    const uint32_t hA = filter_hash(sA[jj]);
+                    const uint32_t m = K3 ? filter_mask3(hA) : filter_mask(hA);
+                    park((wA[jj] & m) == m, (uint32_t)(g0 + jj), sA[jj]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int jj = 0; jj < H; jj++) { sA[jj] = sB[jj]; wA[jj] = wB[jj]; }
+            }
+        } else if (q0 + kScanTile <= end && q0 + kScanTile + B <= size) {
             // Interior tile: every offset is visited and every window has its
             // full length B and a byte entering (match.go:175-191 "more").
             // S2 only matters mod 2^16, so B*x uses B mod 2^16 (24-bit mul).
@@ -502,7 +539,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                 }
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
-                    const uint32_t m = filter_mask(fh[jj]);
+                    const uint32_t m = (K3 ? filter_mask3(fh[jj]) : filter_mask(fh[jj]));
                     const bool hit = (word[jj] & m) == m;
                     park(hit, (uint32_t)(g0 + jj), sum[jj]);
                 }
@@ -532,7 +569,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                 }
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
-                    const uint32_t m = filter_mask(fh[jj]);
+                    const uint32_t m = (K3 ? filter_mask3(fh[jj]) : filter_mask(fh[jj]));
                     const bool hit = ((word[jj] & m) == m) && (lol + g0 + jj < end_rel);
                     park(hit, (uint32_t)(g0 + jj), sum[jj]);
                 }
@@ -615,14 +652,28 @@ hipError_t launch_tile_scan(const TileAgg *agg, uint32_t ntiles, TilePrefix *pre
     return hipGetLastError();
 }
 
+bool roll_filter_k3() {
+    static const bool k3 = [] {
+        const char *e = getenv("RSG_FILTER_K3");
+        return e && e[0] == '1';
+    }();
+    return k3;
+}
+
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
                        const uint32_t *bitmap, const uint64_t *table, uint32_t bmask, uint64_t *cand,
                        uint32_t cap, uint32_t *count, uint32_t grid, bool fused, hipStream_t stream) {
     if (tile_hi <= tile_lo) return hipSuccess;
     const uint32_t g = min(grid, tile_hi - tile_lo);
-    hipLaunchKernelGGL(roll_kernel, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, tile_hi,
-                       agg, pre, ntiles, bitmap, table, bmask, cand, cap, count, fused ? 1u : 0u);
+    static const bool pipe = [] {
+        const char *e = getenv("RSG_ROLL_PIPE");  // A/B switch: 1 = filter reads one group ahead
+        return e && e[0] == '1';
+    }();
+    auto kern = pipe ? (roll_filter_k3() ? roll_kernel<true, true> : roll_kernel<true, false>)
+                     : (roll_filter_k3() ? roll_kernel<false, true> : roll_kernel<false, false>);
+    hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, tile_hi, agg,
+                       pre, ntiles, bitmap, table, bmask, cand, cap, count, fused ? 1u : 0u);
     return hipGetLastError();
 }
 

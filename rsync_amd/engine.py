@@ -477,11 +477,11 @@ class Engine:
     def kernel_times(self, reset: bool = True) -> dict:
         """Totals since the last reset: roll_ms, roll_launches, confirm_ms,
         confirm_batches, candidates (offsets the rolls returned), windows
-        (confirmed by the strong-sum kernel)."""
-        o = (ctypes.c_double * 6)()
+        (confirmed by the strong-sum kernel), filesums_ms, filesums_launches."""
+        o = (ctypes.c_double * 8)()
         check(lib.rsg_kernel_times(self.ctx, o, int(reset)), self.ctx)
         return {"roll_ms": o[0], "roll_launches": int(o[1]), "confirm_ms": o[2], "confirm_batches": int(o[3]),
-                "candidates": int(o[4]), "windows": int(o[5])}
+                "candidates": int(o[4]), "windows": int(o[5]), "filesums_ms": o[6], "filesums_launches": int(o[7])}
 
     # ------------------------------------------------------------ multi-GPU
     @staticmethod
