@@ -266,11 +266,12 @@ void rsg_ctx_destroy(rsg_ctx *c) {
     for (DevBuf *b : dbs)
         if (b->p) hipFree(b->p);
     for (SearchSlot &sl : c->search) {
-        DevBuf *sbs[] = {&sl.agg, &sl.prefix, &sl.counts, &sl.list, &sl.blob, &sl.src};
+        DevBuf *sbs[] = {&sl.agg, &sl.prefix, &sl.counts, &sl.list, &sl.blob, &sl.src, &sl.res};
         for (DevBuf *b : sbs)
             if (b->p) hipFree(b->p);
         if (sl.count.p) hipHostFree(sl.count.p);
         if (sl.stage.p) hipHostFree(sl.stage.p);
+        if (sl.hres.p) hipHostFree(sl.hres.p);
         if (sl.scanned) hipEventDestroy(sl.scanned);
         if (sl.rolled) hipEventDestroy(sl.rolled);
         if (sl.confirmed) hipEventDestroy(sl.confirmed);

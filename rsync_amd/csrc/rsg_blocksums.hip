@@ -150,8 +150,7 @@ __device__ __forceinline__ void store_record(uint8_t *out, uint64_t g, uint32_t 
 // Returns the block's arena offset and length (generator.go:334).
 __device__ __forceinline__ void locate_block(const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file,
                                              uint64_t g, uint64_t &off, uint32_t &n) {
-    const uint32_t w = (uint32_t)(g / kBlockSumThreads);  // g's group of 256 blocks
-    uint32_t lo = wg_file[w], hi = wg_file[w + 1];
+    uint32_t lo = wg_file[blockIdx.x], hi = wg_file[blockIdx.x + 1];
     while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
         if (files[mid].first_block <= g) lo = mid; else hi = mid - 1;
@@ -380,14 +379,7 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     // the buffer descriptor in SGPRs (no waterfall loops around the DMA).
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint8_t *slab = slab_all + wave * kWaveSlab;
-    // Waves take the batch's 64-block groups LAST FIRST: the waves that cannot
-    // be staged (the partial last wave, blocks ending at the arena's end) hash
-    // with latency-bound per-lane loads, so they start with the first
-    // workgroups instead of trailing the last ones.
-    const uint64_t nw = (total_blocks + 63) / 64;
-    const uint64_t widx = (uint64_t)blockIdx.x * (kBlockSumThreads / 64) + wave;
-    if (widx >= nw) return;  // wave-uniform: the grid's spare waves
-    const uint64_t wave_first = (nw - 1 - widx) * 64;
+    const uint64_t wave_first = (uint64_t)blockIdx.x * kBlockSumThreads + wave * 64u;
     const uint64_t g = wave_first + lane;
     uint64_t off = 0;
     uint32_t n = 0;
@@ -811,17 +803,12 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
         uint32_t k = 0;
         while (!owned(k)) k++;
         PkDesc cur;
-        // tickets map to tiles last first (tile_of): the batch's tiles that
-        // cannot be staged (its partial last tile, a last file ending at the
-        // arena's end) run with per-lane loads at the start, not as a tail
-        auto tile_of = [&](uint32_t kk) { return ntiles - 1 - (blockIdx.x + (uint64_t)kk * G); };
-        auto has = [&](uint32_t kk) { return blockIdx.x + (uint64_t)kk * G < ntiles; };
-        uint64_t t = has(k) ? tile_of(k) : ~0ull;
-        if (has(k)) pk_locate(t, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+        uint64_t t = blockIdx.x + (uint64_t)k * G;
+        if (t < ntiles) pk_locate(t, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
         bool have_prev = false;
         uint32_t prev = 0;
 #pragma unroll 1
-        while (has(k)) {
+        while (t < ntiles) {
             const uint32_t slot = k % kPkSlots;
             // the slot's previous tile must have been copied out by its hasher
             while (pk_load(&sh.freeq[slot]) != k) __builtin_amdgcn_s_sleep(1);
@@ -831,11 +818,10 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             if (staged && MODE != 2) pk_issue<AUX, true>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
             uint32_t kn = k + 1;
             while (!owned(kn)) kn++;
-            const bool hn = has(kn);
-            const uint64_t tn = hn ? tile_of(kn) : ~0ull;
+            const uint64_t tn = blockIdx.x + (uint64_t)kn * G;
             // next tile's descriptor (scalar loads) while this one and the
             // previous one are in flight
-            if (hn) pk_locate(tn, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+            if (tn < ntiles) pk_locate(tn, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
             if (single) {
                 // one slot: publish this tile before waiting for the slot again
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -867,8 +853,8 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
         uint32_t k = 0;
         if (lane == 0) k = __hip_atomic_fetch_add(&sh.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         k = __builtin_amdgcn_readfirstlane(k);
-        if (blockIdx.x + (uint64_t)k * G >= ntiles) break;
-        const uint64_t t = ntiles - 1 - (blockIdx.x + (uint64_t)k * G);  // the loaders' tile_of(k)
+        const uint64_t t = blockIdx.x + (uint64_t)k * G;
+        if (t >= ntiles) break;
         const uint32_t slot = k % kPkSlots;
         while (pk_load(&sh.full[slot]) != k) __builtin_amdgcn_s_sleep(1);
         const uint32_t n = sh.n[slot][lane];

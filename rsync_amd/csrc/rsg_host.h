@@ -31,11 +31,13 @@ struct SearchSlot {
     DevBuf src;                        // realigned or uploaded source
     PinBuf stage;                      // pinned staging of the blob
     PinBuf count;                      // candidate count read back
+    DevBuf res;                        // confirmation results (block index per window)
+    PinBuf hres;                       // ... read back; the job's walk reads them on a worker thread
     hipEvent_t scanned = nullptr;      // prefix pass done (side stream)
     hipEvent_t rolled = nullptr;       // roll kernel + count read-back done
     hipEvent_t confirmed = nullptr;    // confirmation batch + result read-back done
 };
-constexpr int kSearchSlots = 3;  // jobs i (walking), i+1 (rolled or rolling), i+2 (being issued)
+constexpr int kSearchSlots = 4;  // jobs i-1 (walk on a worker), i (confirming), i+1 (rolling), i+2 (being issued)
 
 struct rsg_ctx {
     int device = 0;

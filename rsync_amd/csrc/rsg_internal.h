@@ -64,9 +64,14 @@ struct TilePrefix {  // at a tile start: P = sum_{i<j} x_i, Q = sum_{i<j} i * x_
 __host__ __device__ inline uint32_t filter_hash(uint32_t sum) { return ((sum << 13) | (sum >> 19)) ^ sum; }
 __host__ __device__ inline uint32_t filter_word(uint32_t h) { return (h >> 2) & 0x7fffu; }  // 2^15 words
 __host__ __device__ inline uint32_t filter_mask(uint32_t h) { return (1u << ((h >> 22) & 31u)) | (1u << (h >> 27)); }
-// k = 3 variant (RSG_FILTER_K3=1, A/B): a third bit from h[17..21]
-__host__ __device__ inline uint32_t filter_mask3(uint32_t h) { return filter_mask(h) | (1u << ((h >> 17) & 31u)); }
-bool roll_filter_k3();  // the filter's bits per sum: 3 when RSG_FILTER_K3=1 (read once), else 2
+// Bit-selection layout (the default): no hash arithmetic.  Word
+// sum[2..16] (byte address sum & 0x1fffc), bits sum[24..28] and
+// rotr(sum, 29)[0..4] = {sum[29..31], sum[0..1]}: 25 disjoint bits of the sum.
+__host__ __device__ inline uint32_t sel_word(uint32_t s) { return (s >> 2) & 0x7fffu; }
+__host__ __device__ inline uint32_t sel_mask(uint32_t s) {
+    return (1u << ((s >> 24) & 31u)) | (1u << (((s >> 29) | (s << 3)) & 31u));
+}
+bool roll_filter_sel();  // the bit-selection layout (default; RSG_FILTER_SEL=0, read once, selects the hash)
 
 // Exact table of basis weak sums: buckets of kBucketWays u64 entries
 // {sum1 << 32 | flags}; a sum lives in bucket hash1 or hash2.
@@ -81,6 +86,8 @@ hipError_t launch_tile_scan(const TileAgg *agg, uint32_t ntiles, TilePrefix *pre
 // length files[i].len) -> the first block in targets order with equal Sum1,
 // equal length and equal sum2[:s2len], or -1.  groups = (sum1, block) sorted
 // by sum1 (stable in targets order), hi16[h] = first group with sum1 >> 16 == h.
+hipError_t launch_confirm_plan(const uint64_t *cand, uint32_t n, uint64_t size, uint32_t B, DevFile *files,
+                               uint32_t *wg_file, uint32_t nwg, hipStream_t stream);
 hipError_t launch_resolve(const uint8_t *records, const DevFile *files, uint64_t n, const uint2 *groups,
                           const uint32_t *hi16, const uint8_t *sum2, int32_t count, int32_t blen, int32_t rem,
                           int32_t s2len, int32_t *res, hipStream_t stream);

@@ -21,6 +21,7 @@
 #include <chrono>
 #include <climits>
 #include <functional>
+#include <future>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -101,7 +102,9 @@ struct Search {
     hipStream_t cst = nullptr;   // confirmation batches (the compute stream)
     // Called once, right after the first confirmation batch is issued (or at
     // the end of finish() if none is): the batch issues a later job there.
-    std::function<rsg_status()> hook;
+    std::function<rsg_status()> hook;        // issues the next job's stage 1 (may wait for its tables)
+    std::function<bool()> hook_ready;        // hook() would not wait
+    std::function<rsg_status()> tail;        // set by finish(): the rest of the job (wait + walk), any thread
     // device tables inside the slot's blob
     uint64_t off_hi16 = 0, off_sum2 = 0, off_filter = 0, off_table = 0, blob_bytes = 0;
     const uint2 *d_groups = nullptr;
@@ -124,7 +127,8 @@ struct Search {
 
 // Candidate offsets arrive in atomic-append order: LSD radix sort on 16-bit
 // digits (as many passes as the largest offset needs), std::sort for few.
-void sort_offsets(std::vector<uint64_t> &C) {
+// Bits below `lowbit` are a payload the order need not respect.
+void sort_offsets(std::vector<uint64_t> &C, int lowbit = 0) {
     if (C.size() < 4096) {
         std::sort(C.begin(), C.end());
         return;
@@ -133,13 +137,36 @@ void sort_offsets(std::vector<uint64_t> &C) {
     for (uint64_t c : C) mx = std::max(mx, c);
     std::vector<uint64_t> tmp(C.size());
     std::vector<uint32_t> cnt(65537);
-    for (int shift = 0; shift < 64 && (mx >> shift) != 0; shift += 16) {
+    for (int shift = lowbit; shift < 64 && (mx >> shift) != 0; shift += 16) {
         std::fill(cnt.begin(), cnt.end(), 0u);
         for (uint64_t c : C) cnt[((c >> shift) & 0xffffu) + 1]++;
         for (size_t h = 1; h < cnt.size(); h++) cnt[h] += cnt[h - 1];
         for (uint64_t c : C) tmp[cnt[(c >> shift) & 0xffffu]++] = c;
         C.swap(tmp);
     }
+}
+
+// Flags of the events the host waits on.  RSG_BLOCKING_SYNC=1 (A/B): the
+// waiting thread sleeps instead of spinning, leaving its core to the table
+// builders and walks on the worker threads.
+unsigned sync_event_flags() {
+    static const unsigned f = [] {
+        const char *e = getenv("RSG_BLOCKING_SYNC");
+        return (unsigned)hipEventDisableTiming | ((e && e[0] == '1') ? (unsigned)hipEventBlockingSync : 0u);
+    }();
+    return f;
+}
+
+// Issue the next job's stage 1 (its roll queues behind this job's on the
+// compute stream) once its tables, built on a worker thread, are ready;
+// block = wait for them.  Called at several points of a job's finish so the
+// compute stream never runs dry and this thread never idles on the worker.
+rsg_status run_hook(Search &S, bool block) {
+    if (!S.hook) return RSG_OK;
+    if (!block && S.hook_ready && !S.hook_ready()) return RSG_OK;
+    const std::function<rsg_status()> h = std::move(S.hook);
+    S.hook = nullptr;
+    return h();
 }
 
 // Confirm a batch of candidates (indices into C): Checksum1 + MD4(window ||
@@ -196,13 +223,9 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
     if ((s = ensure_pin(ctx, ctx->h_out[0], plan.total_blocks * 4)) != RSG_OK) return s;
     const int32_t *found = (const int32_t *)ctx->h_out[0].p;
     RSG_HIP(ctx, hipMemcpyAsync(ctx->h_out[0].p, ctx->d_res.p, plan.total_blocks * 4, hipMemcpyDeviceToHost, S.cst));
-    if (!S.sl->confirmed) RSG_HIP(ctx, hipEventCreateWithFlags(&S.sl->confirmed, hipEventDisableTiming));
+    if (!S.sl->confirmed) RSG_HIP(ctx, hipEventCreateWithFlags(&S.sl->confirmed, sync_event_flags()));
     RSG_HIP(ctx, hipEventRecord(S.sl->confirmed, S.cst));
-    if (S.hook) {  // the next job's work queues behind this batch, and the host builds its tables meanwhile
-        const std::function<rsg_status()> h = std::move(S.hook);
-        S.hook = nullptr;
-        if ((s = h()) != RSG_OK) return s;
-    }
+    if ((s = run_hook(S, false)) != RSG_OK) return s;  // the next job's roll, if its tables are built
     RSG_HIP(ctx, hipEventSynchronize(S.sl->confirmed));
     S.pt.mark("v.kernel");
     for (size_t i = 0; i < idx.size(); i++) res[idx[i]] = found[i];
@@ -212,8 +235,8 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
 
 // Greedy walk over one range's sorted candidates (match.go:93-210 reduced to
 // the offsets where the weak sum can hit).
-rsg_status walk(Search &S, const std::vector<uint64_t> &C, uint64_t &pos) {
-    std::vector<int32_t> res(C.size(), -2);
+rsg_status walk(Search &S, const std::vector<uint64_t> &C, uint64_t &pos, std::vector<int32_t> *known = nullptr) {
+    std::vector<int32_t> res = known ? std::move(*known) : std::vector<int32_t>(C.size(), -2);
     size_t i = std::lower_bound(C.begin(), C.end(), pos) - C.begin();
     std::vector<uint32_t> batch;
     while (i < C.size()) {
@@ -267,6 +290,77 @@ rsg_status walk(Search &S, const std::vector<uint64_t> &C, uint64_t &pos) {
 
 rsg_status launch_range(Search &S, uint32_t lo, uint32_t hi);
 
+// A sparse range's candidates all confirmed at once (what walk() batches for
+// a sparse range anyway), with the plan built on the GPU from the roll's own
+// list: the confirmation starts as soon as the count is known.  The host
+// reads the list back and sorts it while the GPU hashes; C = the sorted
+// distinct offsets, res = their results (the walk's input).
+rsg_status confirm_all(Search &S, uint32_t n, std::vector<uint64_t> &key) {
+    rsg_ctx *ctx = S.ctx;
+    SearchSlot &sl = *S.sl;
+    HostPlan plan;
+    plan.total_blocks = n;
+    plan.nwg = (n + rsg::kBlockSumThreads - 1) / rsg::kBlockSumThreads;
+    plan.aligned = false;
+    plan.arena_bytes = S.size;
+    plan.max_blen = (uint32_t)S.head.block_len;  // windows are at most B long
+    plan.lds_reserve = S.confirm_lds;
+    rsg_status s;
+    if ((s = ensure_dev(ctx, ctx->d_files, (uint64_t)n * sizeof(DevFile) + 32)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_wg, ((uint64_t)plan.nwg + 1) * sizeof(uint32_t) + 4)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_out[0], (uint64_t)n * kRecordBytes)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, ctx->d_fb[0], rsg::block_sums_scratch_bytes(n))) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, sl.res, (uint64_t)n * 4)) != RSG_OK) return s;
+    if ((s = ensure_pin(ctx, sl.hres, (uint64_t)n * 4)) != RSG_OK) return s;
+    RSG_HIP(ctx, rsg::launch_confirm_plan((const uint64_t *)sl.list.p, n, S.size, (uint32_t)S.head.block_len,
+                                          (DevFile *)ctx->d_files.p, (uint32_t *)ctx->d_wg.p, plan.nwg, S.cst));
+    hipEvent_t t0 = timed_begin(ctx, S.cst);
+    if (ctx->timing) ctx->stat_windows += n;
+    if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, S.d_src, S.seed, ctx->d_out[0].p, ctx->d_fb[0].p,
+                         S.cst)) != RSG_OK)
+        return s;
+    RSG_HIP(ctx, rsg::launch_resolve((const uint8_t *)ctx->d_out[0].p, (const DevFile *)ctx->d_files.p, n,
+                                     S.d_groups, S.d_hi16, S.d_sum2, S.head.count, S.head.block_len, S.head.rem,
+                                     S.head.s2len, (int32_t *)sl.res.p, S.cst));
+    timed_end(ctx, t0, S.cst, 1);
+    RSG_HIP(ctx, hipMemcpyAsync(sl.hres.p, sl.res.p, (uint64_t)n * 4, hipMemcpyDeviceToHost, S.cst));
+    if (!sl.confirmed) RSG_HIP(ctx, hipEventCreateWithFlags(&sl.confirmed, sync_event_flags()));
+    RSG_HIP(ctx, hipEventRecord(sl.confirmed, S.cst));
+    if ((s = run_hook(S, false)) != RSG_OK) return s;  // the next job's roll, if its tables are built
+    // the list, keyed (offset << 22 | list index) so the sort carries each
+    // offset's record index (offsets < 2^42, indices < kCandCap = 2^22)
+    key.resize(n);
+    RSG_HIP(ctx, hipMemcpyAsync(key.data(), sl.list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, S.copy));
+    RSG_HIP(ctx, hipStreamSynchronize(S.copy));
+    for (uint32_t i = 0; i < n; i++) key[i] = (key[i] << 22) | i;
+    sort_offsets(key, 22);
+    S.pt.mark("c.sort");
+    return run_hook(S, false);
+}
+
+// The rest of a confirm_all job, after its confirmation was queued: wait for
+// the results, pair them with the sorted distinct offsets, walk.  Touches only
+// S and its slot's pinned results (no HIP call but an event wait), so it can
+// run on a worker thread while the next jobs are confirmed and rolled.
+rsg_status confirm_all_tail(Search &S, const std::vector<uint64_t> &key, uint64_t &pos) {
+    if (hipEventSynchronize(S.sl->confirmed) != hipSuccess) return RSG_ERR_HIP;
+    S.pt.mark("c.kernel");
+    const int32_t *found = (const int32_t *)S.sl->hres.p;
+    std::vector<uint64_t> C;
+    std::vector<int32_t> res;
+    C.reserve(key.size());
+    res.reserve(key.size());
+    for (uint64_t k : key) {
+        const uint64_t off = k >> 22;
+        if (!C.empty() && C.back() == off) continue;
+        C.push_back(off);
+        res.push_back(found[k & ((1u << 22) - 1)]);
+    }
+    rsg_status s = walk(S, C, pos, &res);
+    S.pt.mark("walk");
+    return s;
+}
+
 // Stage 1 of a search, host part: the basis tables, packed into the slot's
 // pinned staging blob.  Basis sums grouped by Sum1 in targets order (resolve
 // tables); Bloom filter of every Sum1 + a 2-choice bucketed table {Sum1,
@@ -310,10 +404,14 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
         else keys.push_back({S.groups[i].first, f});
     }
     std::vector<uint32_t> bitmap(rsg::kFilterBits / 32, 0);
-    const bool k3 = rsg::roll_filter_k3();
+    const bool sel = rsg::roll_filter_sel();
     for (auto &kv : keys) {
-        const uint32_t h = rsg::filter_hash(kv.first);
-        bitmap[rsg::filter_word(h)] |= k3 ? rsg::filter_mask3(h) : rsg::filter_mask(h);
+        if (sel) {
+            bitmap[rsg::sel_word(kv.first)] |= rsg::sel_mask(kv.first);
+        } else {
+            const uint32_t h = rsg::filter_hash(kv.first);
+            bitmap[rsg::filter_word(h)] |= rsg::filter_mask(h);
+        }
     }
     uint32_t nb = 16;
     while (nb < keys.size() / 2) nb <<= 1;
@@ -355,8 +453,8 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
     return RSG_OK;
 }
 
-// Stage 1, GPU part.  Side stream: (realigning copy,) prefix pass; compute
-// stream: blob upload, then after the prefix pass the roll over the whole
+// Stage 1, GPU part.  Side stream: (realigning copy,) prefix pass, blob
+// upload; compute stream: after those the roll over the whole
 // scan range and its candidate count read-back (event `rolled`).  The roll
 // queues behind whatever the compute stream holds (the previous file's roll),
 // never beside it.
@@ -365,7 +463,7 @@ rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
     SearchSlot &sl = *S.sl;
     rsg_status s;
     if (!sl.scanned) RSG_HIP(ctx, hipEventCreateWithFlags(&sl.scanned, hipEventDisableTiming));
-    if (!sl.rolled) RSG_HIP(ctx, hipEventCreateWithFlags(&sl.rolled, hipEventDisableTiming));
+    if (!sl.rolled) RSG_HIP(ctx, hipEventCreateWithFlags(&sl.rolled, sync_event_flags()));
     if ((s = ensure_dev(ctx, sl.agg, (uint64_t)S.ntiles * sizeof(TileAgg) + 64)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, sl.prefix, ((uint64_t)S.ntiles + 1) * sizeof(TilePrefix) + 64)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, sl.list, (uint64_t)kCandCap * 8)) != RSG_OK) return s;
@@ -385,9 +483,11 @@ rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
         RSG_HIP(ctx, rsg::launch_tile_agg(S.d_src, S.size, r, (TileAgg *)sl.agg.p, S.ntiles, S.side));
         RSG_HIP(ctx, rsg::launch_tile_scan((const TileAgg *)sl.agg.p, S.ntiles, (TilePrefix *)sl.prefix.p, S.side));
     }
-    RSG_HIP(ctx, hipEventRecord(sl.scanned, S.side));  // also orders the realigning copy
-
-    RSG_HIP(ctx, hipMemcpyAsync(sl.blob.p, sl.stage.p, S.blob_bytes, hipMemcpyHostToDevice, S.st));
+    // The tables' upload (~1.7 MB for a 32 768-block basis) goes on the side
+    // stream too: on the compute stream it sat between two files' rolls
+    // (≈ 50 µs of PCIe per file in the batch timeline).
+    RSG_HIP(ctx, hipMemcpyAsync(sl.blob.p, sl.stage.p, S.blob_bytes, hipMemcpyHostToDevice, S.side));
+    RSG_HIP(ctx, hipEventRecord(sl.scanned, S.side));  // also orders the realigning copy and the upload
     const uint8_t *blob = (const uint8_t *)sl.blob.p;
     S.d_groups = (const uint2 *)blob;
     S.d_hi16 = (const uint32_t *)(blob + S.off_hi16);
@@ -449,23 +549,45 @@ rsg_status finish(Search &S) {
             continue;
         }
         if (ctx->timing) ctx->stat_candidates += n;
+        S.pt.mark("roll");
+        if ((s = run_hook(S, false)) != RSG_OK) return s;
+        // sparse range (the hashing of every candidate stays below twice the
+        // range, walk()'s own batching rule): confirm them all at once
+        const uint64_t range = std::min<uint64_t>((uint64_t)hi * kScanTile, S.size) - (uint64_t)lo * kScanTile;
+        static const bool all_env = [] {
+            const char *e = getenv("RSG_CONFIRM_ALL");  // A/B switch: 0 = host-built confirmation batches
+            return !(e && e[0] == '0');
+        }();
+        if (all_env && n > 0 && n <= kSparseBatch && S.size < (1ull << 42) &&
+            (uint64_t)n * (uint64_t)S.head.block_len <= 2 * range + (1u << 20)) {
+            auto key = std::make_shared<std::vector<uint64_t>>();
+            if ((s = confirm_all(S, n, *key)) != RSG_OK) return s;
+            if (hi == S.tile_end) {
+                // the job's last range: the caller may run the rest anywhere
+                Search *Sp = &S;
+                const uint64_t p0 = pos;
+                S.tail = [Sp, key, p0]() {
+                    uint64_t p = p0;
+                    return confirm_all_tail(*Sp, *key, p);
+                };
+                break;
+            }
+            if ((s = confirm_all_tail(S, *key, pos)) != RSG_OK) return s;
+            lo = hi;
+            continue;
+        }
         C.resize(n);
         if (n) {
             RSG_HIP(ctx, hipMemcpyAsync(C.data(), sl.list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, S.copy));
             RSG_HIP(ctx, hipStreamSynchronize(S.copy));
         }
-        S.pt.mark("roll");
         sort_offsets(C);
         C.erase(std::unique(C.begin(), C.end()), C.end());
         if ((s = walk(S, C, pos)) != RSG_OK) return s;
         S.pt.mark("walk");
         lo = hi;
     }
-    if (S.hook) {
-        const std::function<rsg_status()> h = std::move(S.hook);
-        S.hook = nullptr;
-        return h();
-    }
+    if ((s = run_hook(S, true)) != RSG_OK) return s;
     return RSG_OK;
 }
 
@@ -533,9 +655,51 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
     const int spare = std::max(0, std::min(cc ? atoi(cc) : kConfirmCus, dev_cus - 1));
     const bool split = spare > 0 && njobs > 1;  // one job: nothing to overlap its confirmation with
     std::unique_ptr<Search> live[kSearchSlots];
-    // Validate job i and issue its stage 1.  Returns only fatal statuses; a
-    // job-local failure is recorded on the job, which then holds no search.
-    auto start = [&](uint64_t i) -> rsg_status {
+    // Job i's stage 1 in two steps.  prepare(i): validate the job and start
+    // building its basis tables (host sorting and hashing, ~0.3-0.8 ms for a
+    // 32 768-block basis) on a worker thread.  issue(): wait for those tables
+    // and queue the job's GPU work.  Job i+2 is prepared while job i is
+    // finished on this thread, and issued once job i's confirmation is queued.
+    // Both return only fatal statuses; a job-local failure is recorded on
+    // the job, which then holds no search.
+    std::future<rsg_status> tails[kSearchSlots];  // job i's walk (confirm_all_tail) on a worker
+    bool tail_live[kSearchSlots] = {};
+    // Job i's results into the caller's job record once its search is done
+    // (finish() and, if it handed one back, its tail).
+    auto complete = [&](uint64_t i, rsg_status s) -> rsg_status {
+        Search *S = live[i % kSearchSlots].get();
+        if (s == RSG_OK) {
+            rsg_search_job &j = jobs[i];
+            j.n_matches = S->out.size();
+            const uint64_t ncopy = std::min<uint64_t>(S->out.size(), j.match_cap);
+            if (ncopy) memcpy(j.matches, S->out.data(), ncopy * sizeof(rsg_match));
+            if (S->out.size() > j.match_cap)
+                note(i, fail(ctx, RSG_ERR_TRUNCATED, "%llu matches, capacity %llu",
+                             (unsigned long long)S->out.size(), (unsigned long long)j.match_cap));
+            return RSG_OK;
+        }
+        if (job_local(s)) return note(i, s), RSG_OK;
+        if (s == RSG_ERR_HIP) return fail(ctx, RSG_ERR_HIP, "confirmation wait failed");
+        return s;
+    };
+    // join job i's tail (if any) and finish its record; its slot is free after
+    auto join = [&](uint64_t i) -> rsg_status {
+        const int slot = (int)(i % kSearchSlots);
+        rsg_status f = RSG_OK;
+        if (tail_live[slot]) {
+            tail_live[slot] = false;
+            f = complete(i, tails[slot].get());
+        }
+        live[slot].reset();
+        return f;
+    };
+    struct Pending {
+        bool valid = false;
+        uint64_t i = 0;
+        std::unique_ptr<Search> S;
+        std::future<rsg_status> tab;
+    } pends[2];  // job i is prepared into pends[i & 1]
+    auto prepare = [&](uint64_t i) -> rsg_status {
         rsg_search_job &j = jobs[i];
         const int slot = (int)(i % kSearchSlots);
         live[slot].reset();  // job i - 3 of this slot was finished, its GPU work waited for
@@ -564,14 +728,32 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
         S->size = j.src_len;
         S->head = j.head;
         S->seed = seed;
-        if ((s = tables(*S, j.sum1, j.sum2, j.targets)) == RSG_OK) s = enqueue_scan(*S, (const uint8_t *)j.src, host_src);
+        Search *raw = S.get();
+        Pending &pend = pends[i & 1];
+        pend.tab = std::async(std::launch::async, [raw, &j] { return tables(*raw, j.sum1, j.sum2, j.targets); });
+        pend.S = std::move(S);
+        pend.i = i;
+        pend.valid = true;
+        return RSG_OK;
+    };
+    auto issue = [&](uint64_t i) -> rsg_status {
+        Pending &pend = pends[i & 1];
+        if (!pend.valid || pend.i != i) return RSG_OK;  // job i holds no search
+        pend.valid = false;
+        rsg_status s = pend.tab.get();
+        std::unique_ptr<Search> S = std::move(pend.S);
+        if (s == RSG_OK) s = enqueue_scan(*S, (const uint8_t *)jobs[i].src, host_src);
         if (s != RSG_OK) {
             if (!job_local(s)) return s;
             note(i, s);
             return RSG_OK;
         }
-        live[slot] = std::move(S);
+        live[i % kSearchSlots] = std::move(S);
         return RSG_OK;
+    };
+    auto start = [&](uint64_t i) -> rsg_status {
+        rsg_status s = prepare(i);
+        return s != RSG_OK ? s : issue(i);
     };
     // RSG_SEARCH_OVERLAP=0: issue job i+1 only after job i is finished (A/B measurement)
     const char *ov = getenv("RSG_SEARCH_OVERLAP");
@@ -579,37 +761,56 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
     const bool overlap = !(ov && ov[0] == '0');
     rsg_status fatal = RSG_OK;
     uint64_t i = 0;
-    if (njobs) fatal = start(0);
-    if (fatal == RSG_OK && overlap && njobs > 1) fatal = start(1);
+    if (!overlap) {
+        if (njobs) fatal = start(0);
+    } else {  // the first two jobs' tables build side by side
+        for (uint64_t k = 0; k < std::min<uint64_t>(njobs, 2) && fatal == RSG_OK; k++) fatal = prepare(k);
+        for (uint64_t k = 0; k < std::min<uint64_t>(njobs, 2) && fatal == RSG_OK; k++) fatal = issue(k);
+    }
     for (; fatal == RSG_OK && i < njobs; i++) {
         const uint64_t ahead = overlap ? i + 2 : i + 1;
-        auto next = [&, ahead]() -> rsg_status { return ahead < njobs ? start(ahead) : RSG_OK; };
-        Search *S = live[i % kSearchSlots].get();
+        // job i+2 takes job i-2's slot: that job's walk (a worker) is done by
+        // now; then job i+2's tables build on a worker while job i finishes
+        // here.  With RSG_SEARCH_OVERLAP=0 job i+1 is prepared and issued
+        // after job i instead.
+        if (overlap && i >= 2 && (fatal = join(i - 2)) != RSG_OK) break;
+        if (overlap && ahead < njobs && (fatal = prepare(ahead)) != RSG_OK) break;
+        auto next = [&, ahead]() -> rsg_status {
+            if (!overlap) return ahead < njobs ? start(ahead) : RSG_OK;
+            return ahead < njobs ? issue(ahead) : RSG_OK;
+        };
+        const int slot = (int)(i % kSearchSlots);
+        Search *S = live[slot].get();
         if (!S) {
             if ((fatal = next()) != RSG_OK) break;
             continue;
         }
         S->hook = next;
+        S->hook_ready = [&, ahead]() {
+            const Pending &pend = pends[ahead & 1];
+            return !overlap || ahead >= njobs || !pend.valid || pend.i != ahead ||
+                   pend.tab.wait_for(std::chrono::seconds(0)) == std::future_status::ready;
+        };
         rsg_status s = finish(*S);
-        if (s == RSG_OK) {
-            rsg_search_job &j = jobs[i];
-            j.n_matches = S->out.size();
-            const uint64_t ncopy = std::min<uint64_t>(S->out.size(), j.match_cap);
-            if (ncopy) memcpy(j.matches, S->out.data(), ncopy * sizeof(rsg_match));
-            if (S->out.size() > j.match_cap)
-                note(i, fail(ctx, RSG_ERR_TRUNCATED, "%llu matches, capacity %llu",
-                             (unsigned long long)S->out.size(), (unsigned long long)j.match_cap));
-        } else if (job_local(s)) {
-            note(i, s);
-        } else {
-            fatal = s;
-            break;
+        if (s == RSG_OK && S->tail) {
+            if (overlap) {  // the walk runs beside the next jobs' confirmations and rolls
+                tails[slot] = std::async(std::launch::async, S->tail);
+                tail_live[slot] = true;
+            } else {
+                s = S->tail();
+            }
         }
+        if (!tail_live[slot] && (fatal = complete(i, s)) != RSG_OK) break;
         if (S->hook && (fatal = S->hook()) != RSG_OK) {  // finish() stopped early on a job-local error
             i++;
             break;
         }
-        live[i % kSearchSlots].reset();
+        if (!overlap) live[slot].reset();
+    }
+    // the last jobs' walks (and, after a fatal error, any still running)
+    for (uint64_t k = i >= kSearchSlots ? i - kSearchSlots : 0; k < i; k++) {
+        const rsg_status f = join(k);
+        if (fatal == RSG_OK) fatal = f;
     }
     if (fatal != RSG_OK) {
         const std::string msg = ctx->err;

@@ -36,26 +36,8 @@ __device__ __forceinline__ int32_t sx8(uint32_t w, int b) {
 // sx8(a, b) - sx8(c, b) and k * sx8(c, b) (k a 24-bit signed value) in one
 // VALU instruction each: SDWA operand byte selects with sign extension
 // (SignExtend, rsyncchecksum.go:24-27).  b must fold to a constant.
-__device__ __forceinline__ int32_t sub_sx8(uint32_t a, uint32_t c, int b) {
-    int32_t d;
-    switch (b) {
-        case 0: asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0" : "=v"(d) : "v"(a), "v"(c)); break;
-        case 1: asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_1" : "=v"(d) : "v"(a), "v"(c)); break;
-        case 2: asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:BYTE_2" : "=v"(d) : "v"(a), "v"(c)); break;
-        default: asm("v_sub_u32_sdwa %0, sext(%1), sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3" : "=v"(d) : "v"(a), "v"(c)); break;
-    }
-    return d;
-}
-__device__ __forceinline__ int32_t mul_sx8(int32_t k, uint32_t c, int b) {
-    int32_t m;
-    switch (b) {
-        case 0: asm("v_mul_i32_i24_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(m) : "v"(k), "v"(c)); break;
-        case 1: asm("v_mul_i32_i24_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(m) : "v"(k), "v"(c)); break;
-        case 2: asm("v_mul_i32_i24_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(m) : "v"(k), "v"(c)); break;
-        default: asm("v_mul_i32_i24_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(m) : "v"(k), "v"(c)); break;
-    }
-    return m;
-}
+__device__ __forceinline__ int32_t sub_sx8(uint32_t a, uint32_t c, int b) { return sx8(a, b) - sx8(c, b); }
+__device__ __forceinline__ int32_t mul_sx8(int32_t k, uint32_t c, int b) { return k * sx8(c, b); }
 
 
 // Four little-endian words of src[pos, pos+16); bytes at or past `size` read 0.
@@ -245,19 +227,40 @@ __device__ __forceinline__ uint32_t table_flags(const uint64_t *__restrict__ tab
     return fl;
 }
 
+// The filter word of sum s, and whether both of s's bits are set in it.
+template <bool SEL>
+__device__ __forceinline__ uint32_t filt_index(uint32_t s) {
+    return SEL ? sel_word(s) : filter_word(filter_hash(s));
+}
+template <bool SEL>
+__device__ __forceinline__ bool filt_hit(uint32_t word, uint32_t s) {
+    if constexpr (SEL) {
+        const uint32_t x = word >> ((s >> 24) & 31u);
+        const uint32_t y = word >> (__builtin_amdgcn_alignbit(s, s, 29) & 31u);  // rotr(s, 29)[0..4]
+        uint32_t z = x & y & 1u;
+        asm("" : "+v"(z));  // one compare serves both the ballot and the lane's own test
+        return z != 0;
+    } else {
+        const uint32_t m = filter_mask(filter_hash(s));
+        return (word & m) == m;
+    }
+}
+
 constexpr uint32_t kQueueCap = 96;  // bitmap hits parked per wave and tile before the exact probes
 
-// PIPE: the interior offsets go in groups of 4 whose filter-word reads are
-// issued one group ahead of their tests (the reads of group g+1 are in flight
-// while group g is tested and parked); otherwise groups of 8, each read, then
-// waited for, then tested.  K3: three filter bits per sum (filter_mask3).
-template <bool PIPE, bool K3>
+// SEL: the filter's bit-selection layout (sel_word / sel_mask: 5 VALU per
+// test) instead of the rotate-xor hash (8).
+template <bool SEL>
 __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
     uint32_t tile_hi, const TileAgg *__restrict__ agg, const TilePrefix *__restrict__ pre, uint32_t ntiles,
     const uint32_t *__restrict__ bitmap_g, const uint64_t *__restrict__ table, uint32_t bmask,
     uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count, uint32_t fused) {
     constexpr uint32_t kWaves = kRollThreads / 64;
+    constexpr uint32_t P = kRollPerThread;     // offsets per lane
+    constexpr int OW = (int)P / 4;             // words of a lane's own bytes
+    constexpr int NV = (int)P / 16;            // 16-byte vectors of them
+    static_assert(P % 16 == 0 && kWaves <= 16, "lane layout");
     __shared__ uint32_t bitmap[kFilterBits / 32];       // 128 KiB
     __shared__ uint2 queue[kWaves][2][kQueueCap];        // (tile-local offset, sum), per tile parity
     __shared__ uint4 wsum[2][kWaves];                     // scan partials, double-buffered per tile
@@ -299,7 +302,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     const uint32_t per = (tile_hi - tile_lo + gridDim.x - 1) / gridDim.x;
     const uint32_t t_begin = tile_lo + blockIdx.x * per;
     const uint32_t t_end = min(tile_hi, t_begin + per);
-    const uint32_t lo = threadIdx.x * kRollPerThread;  // local offset of this lane's first offset
+    const uint32_t lo = threadIdx.x * P;  // local offset of this lane's first offset
     const uint32_t sh = B & 3u;  // (q0 + lo + B) & 3: q0, lo are multiples of 32
     // Fused prefix (B <= kFusedMaxB, no tile_agg / tile_scan passes): the
     // window at tile start q0 needs only D1 = sum x and DM = sum i*x (absolute
@@ -344,19 +347,19 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     // own bytes [qt, qt+32) and the 4-byte aligned shifted bytes around
     // [qt+B, qt+B+32) of tile t; the next tile's are loaded while this one
     // is scanned (one workgroup per CU: nothing else would hide the latency)
-    uint32_t O[8], A[12], On[8];
+    uint32_t O[OW], A[OW + 4], On[OW];
     // Plain 16-byte loads (no end-of-source guards): for tiles whose own and
     // shifted bytes lie inside the source.
     auto fetch_plain = [&](uint32_t tt, uint32_t *o, uint32_t *a) {
         const uint8_t *p = src + (uint64_t)tt * kScanTile + lo;
 #pragma unroll
-        for (int q = 0; q < 2; q++) {
+        for (int q = 0; q < NV; q++) {
             const u32x4a4m v = *reinterpret_cast<const u32x4a4m *>(p + 16 * q);
             o[4 * q] = v.x; o[4 * q + 1] = v.y; o[4 * q + 2] = v.z; o[4 * q + 3] = v.w;
         }
         const uint8_t *pa = p + B - sh;
 #pragma unroll
-        for (int q = 0; q < 3; q++) {
+        for (int q = 0; q < NV + 1; q++) {
             const u32x4a4m v = *reinterpret_cast<const u32x4a4m *>(pa + 16 * q);
             a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
         }
@@ -368,16 +371,15 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         if (q0 >= end) break;  // uniform
         const uint64_t qt = q0 + lo;
         if (!have) {
-            load_vec(src, size, qt, O);
-            load_vec(src, size, qt + 16, O + 4);
-            const uint64_t pa = qt + B - sh;
-            load_vec(src, size, pa, A);
-            load_vec(src, size, pa + 16, A + 4);
-            load_vec(src, size, pa + 32, A + 8);
-        }
-        uint32_t S[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) S[k] = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sh);
+            for (int q = 0; q < NV; q++) load_vec(src, size, qt + 16 * q, O + 4 * q);
+            const uint64_t pa = qt + B - sh;
+#pragma unroll
+            for (int q = 0; q < NV + 1; q++) load_vec(src, size, pa + 16 * q, A + 4 * q);
+        }
+        uint32_t S[OW];
+#pragma unroll
+        for (int k = 0; k < OW; k++) S[k] = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sh);
         // the next tile's bytes load while this one is scanned (one workgroup
         // per CU: nothing else would hide the latency); A is dead once S is
         // built, so it takes the next tile's shifted bytes
@@ -396,13 +398,16 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         }
         int32_t o1, o2, s1, s2, v1, v2;
         vec_sums(O, o1, o2);
-        vec_sums(O + 4, v1, v2);
-        o2 += v2 + 16 * v1;
-        o1 += v1;
         vec_sums(S, s1, s2);
-        vec_sums(S + 4, v1, v2);
-        s2 += v2 + 16 * v1;
-        s1 += v1;
+#pragma unroll
+        for (int c = 1; c < NV; c++) {
+            vec_sums(O + 4 * c, v1, v2);
+            o2 += v2 + 16 * c * v1;
+            o1 += v1;
+            vec_sums(S + 4 * c, v1, v2);
+            s2 += v2 + 16 * c * v1;
+            s1 += v1;
+        }
         // one workgroup scan of four values: prefixes (within the tile) of the
         // own and shifted byte sums, sum x and sum (local index) * x
         uint32_t v[4] = {(uint32_t)o1, (uint32_t)o2 + lo * (uint32_t)o1, (uint32_t)s1,
@@ -417,7 +422,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         uint4 add;
         {
             const uint32_t w = lane & 15u;
-            uint4 p = wsum[parity][w];
+            uint4 p = wsum[parity][min(w, kWaves - 1)];
             if (w >= wave) p = make_uint4(0, 0, 0, 0);
             add = make_uint4(row16_sum(p.x), row16_sum(p.y), row16_sum(p.z), row16_sum(p.w));
         }
@@ -488,59 +493,29 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         // computed and fetched first (one LDS wait per group, not per offset),
         // then the hits are parked.
         constexpr int G = 8;
-        if (PIPE && q0 + kScanTile <= end && q0 + kScanTile + B <= size) {
-            const int32_t negB16 = -(int32_t)(B & 0xffffu);
-            constexpr int H = 4;
-            uint32_t sA[H], wA[H];
-            auto issue = [&](int g0, uint32_t *sm, uint32_t *wd) {
-#pragma unroll
-                for (int jj = 0; jj < H; jj++) {
-                    const int j = g0 + jj;
-                    sm[jj] = __builtin_amdgcn_perm(W2, W1, 0x05040100u);  // match.go:106
-                    wd[jj] = bitmap[filter_word(filter_hash(sm[jj]))];
-                    W1 += (uint32_t)sub_sx8(S[j >> 2], O[j >> 2], j & 3);
-                    W2 = W2 + (uint32_t)mul_sx8(negB16, O[j >> 2], j & 3) + W1;
-                }
-            };
-            issue(0, sA, wA);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int g0 = 0; g0 < (int)kRollPerThread; g0 += H) {
-                uint32_t sB[H], wB[H];
-                if (g0 + H < (int)kRollPerThread) issue(g0 + H, sB, wB);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int jj = 0; jj < H; jj++) {
-                    const uint32_t hA = filter_hash(sA[jj]);
-                    const uint32_t m = K3 ? filter_mask3(hA) : filter_mask(hA);
-                    park((wA[jj] & m) == m, (uint32_t)(g0 + jj), sA[jj]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int jj = 0; jj < H; jj++) { sA[jj] = sB[jj]; wA[jj] = wB[jj]; }
-            }
-        } else if (q0 + kScanTile <= end && q0 + kScanTile + B <= size) {
+        if (q0 + kScanTile <= end && q0 + kScanTile + B <= size) {
             // Interior tile: every offset is visited and every window has its
             // full length B and a byte entering (match.go:175-191 "more").
-            // S2 only matters mod 2^16, so B*x uses B mod 2^16 (24-bit mul).
-            const int32_t negB16 = -(int32_t)(B & 0xffffu);
+            // S2 only matters mod 2^16, so -B*x uses (2^16 - B) mod 2^16, a
+            // non-negative 24-bit factor (one v_mul_i32_i24 with an SDWA byte
+            // operand, then v_add3: no negation for the compiler to turn into
+            // a subtraction).
+            const int32_t negB16 = (int32_t)((0x10000u - (B & 0xffffu)) & 0xffffu);
 #pragma unroll
-            for (int g0 = 0; g0 < (int)kRollPerThread; g0 += G) {
-                uint32_t sum[G], word[G], fh[G];
+            for (int g0 = 0; g0 < (int)P; g0 += G) {
+                uint32_t sum[G], word[G];
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
                     const int j = g0 + jj;
                     sum[jj] = __builtin_amdgcn_perm(W2, W1, 0x05040100u);  // (W1 & 0xffff) | W2 << 16, match.go:106
-                    fh[jj] = filter_hash(sum[jj]);
-                    word[jj] = bitmap[filter_word(fh[jj])];
+                    word[jj] = bitmap[filt_index<SEL>(sum[jj])];
                     // W1 += xi - xo; W2 += W1 - B * xo (4 VALU, SDWA byte selects)
                     W1 += (uint32_t)sub_sx8(S[j >> 2], O[j >> 2], j & 3);
                     W2 = W2 + (uint32_t)mul_sx8(negB16, O[j >> 2], j & 3) + W1;
                 }
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
-                    const uint32_t m = (K3 ? filter_mask3(fh[jj]) : filter_mask(fh[jj]));
-                    const bool hit = (word[jj] & m) == m;
+                    const bool hit = filt_hit<SEL>(word[jj], sum[jj]);
                     park(hit, (uint32_t)(g0 + jj), sum[jj]);
                 }
                 __builtin_amdgcn_sched_barrier(0);  // groups stay apart: registers for the next tile's bytes
@@ -550,15 +525,14 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
             const uint32_t end_rel = (uint32_t)min<uint64_t>(end - q0, 0xFFFFFFFFull);
             const uint32_t size_rel = (uint32_t)min<uint64_t>(size > q0 ? size - q0 : 0, 0xFFFFFFFFull);
 #pragma unroll
-            for (int g0 = 0; g0 < (int)kRollPerThread; g0 += G) {
-                uint32_t sum[G], word[G], fh[G];
+            for (int g0 = 0; g0 < (int)P; g0 += G) {
+                uint32_t sum[G], word[G];
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
                     const int j = g0 + jj;
                     const uint32_t qr = lol + j;
                     sum[jj] = __builtin_amdgcn_perm(W2, W1, 0x05040100u);
-                    fh[jj] = filter_hash(sum[jj]);
-                    word[jj] = bitmap[filter_word(fh[jj])];
+                    word[jj] = bitmap[filt_index<SEL>(sum[jj])];
                     // rolling update, match.go:171-196
                     const int32_t xo = sx8(O[j >> 2], j & 3);
                     const bool more = qr + k < size_rel;
@@ -569,8 +543,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
                 }
 #pragma unroll
                 for (int jj = 0; jj < G; jj++) {
-                    const uint32_t m = (K3 ? filter_mask3(fh[jj]) : filter_mask(fh[jj]));
-                    const bool hit = ((word[jj] & m) == m) && (lol + g0 + jj < end_rel);
+                    const bool hit = filt_hit<SEL>(word[jj], sum[jj]) && (lol + g0 + jj < end_rel);
                     park(hit, (uint32_t)(g0 + jj), sum[jj]);
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -594,11 +567,37 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         qh ^= 1u;
         if (next) {
 #pragma unroll
-            for (int k = 0; k < 8; k++) O[k] = On[k];
+            for (int k = 0; k < OW; k++) O[k] = On[k];
         }
         have = next;
     }
     drain_rest(qh ^ 1, prev_q0, 0, prev_n);  // the last tile's hits
+}
+
+// --------------------------------------------------------------- confirm plan
+// One DevFile per candidate window, in the roll's append order: window
+// [q, q + min(B, size - q)) is record i (match.go:114-117).  The confirmation
+// of a sparse range starts as soon as the roll's count is known, without the
+// candidates' round trip through the host (rsg_match.cpp: confirm_all).
+__global__ __launch_bounds__(256) void confirm_plan_kernel(const uint64_t *__restrict__ cand, uint32_t n,
+                                                           uint64_t size, uint32_t B, DevFile *__restrict__ files,
+                                                           uint32_t *__restrict__ wg_file, uint32_t nwg) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n) {
+        const uint64_t q = cand[i];
+        const uint32_t k = (uint32_t)min<uint64_t>((uint64_t)B, size - q);
+        files[i] = DevFile{q, k, i, k, 1};
+    }
+    if (i <= nwg) wg_file[i] = min(i * 256u, n - 1);  // plan layout of rsg_match.cpp verify()
+}
+
+hipError_t launch_confirm_plan(const uint64_t *cand, uint32_t n, uint64_t size, uint32_t B, DevFile *files,
+                               uint32_t *wg_file, uint32_t nwg, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint32_t threads = max(n, nwg + 1);
+    hipLaunchKernelGGL(confirm_plan_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream, cand, n, size, B, files,
+                       wg_file, nwg);
+    return hipGetLastError();
 }
 
 // --------------------------------------------------------------- resolve
@@ -652,12 +651,12 @@ hipError_t launch_tile_scan(const TileAgg *agg, uint32_t ntiles, TilePrefix *pre
     return hipGetLastError();
 }
 
-bool roll_filter_k3() {
-    static const bool k3 = [] {
-        const char *e = getenv("RSG_FILTER_K3");
-        return e && e[0] == '1';
+bool roll_filter_sel() {
+    static const bool sel = [] {
+        const char *e = getenv("RSG_FILTER_SEL");  // A/B switch: 0 = the rotate-xor hash layout
+        return !(e && e[0] == '0');
     }();
-    return k3;
+    return sel;
 }
 
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
@@ -666,12 +665,7 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                        uint32_t cap, uint32_t *count, uint32_t grid, bool fused, hipStream_t stream) {
     if (tile_hi <= tile_lo) return hipSuccess;
     const uint32_t g = min(grid, tile_hi - tile_lo);
-    static const bool pipe = [] {
-        const char *e = getenv("RSG_ROLL_PIPE");  // A/B switch: 1 = filter reads one group ahead
-        return e && e[0] == '1';
-    }();
-    auto kern = pipe ? (roll_filter_k3() ? roll_kernel<true, true> : roll_kernel<true, false>)
-                     : (roll_filter_k3() ? roll_kernel<false, true> : roll_kernel<false, false>);
+    auto kern = roll_filter_sel() ? roll_kernel<true> : roll_kernel<false>;
     hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, tile_hi, agg,
                        pre, ntiles, bitmap, table, bmask, cand, cap, count, fused ? 1u : 0u);
     return hipGetLastError();
