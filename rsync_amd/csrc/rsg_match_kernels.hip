@@ -412,53 +412,75 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         // own and shifted byte sums, sum x and sum (local index) * x
         uint32_t v[4] = {(uint32_t)o1, (uint32_t)o2 + lo * (uint32_t)o1, (uint32_t)s1,
                          (uint32_t)s2 + lo * (uint32_t)s1};
-        uint32_t incl[4];
-#pragma unroll
-        for (int c = 0; c < 4; c++) incl[c] = wave_incl_scan(v[c]);
-        if (lane == 63) wsum[parity][wave] = make_uint4(incl[0], incl[1], incl[2], incl[3]);
-        __syncthreads();
-        // the partials of the waves before this one: lane l of every row
-        // reads wave l's (zero for l >= wave), each row sums its 16 lanes
-        uint4 add;
+        // Only two combinations of the four prefixes enter an interior window
+        // (W1 = exA + a tile constant, M = exB + a tile constant):
+        //   exA = ex(s1) - ex(o1),  exB = ex(s2') + (q0+B) ex(s1) - ex(o2') - q0 ex(o1)
+        // so a tile whose windows are all interior (always, with the fused
+        // prefix) scans two values; only a long-block tile near the source's
+        // end scans all four (its last windows need the own prefix alone).
+        uint32_t exA, exB, ex0 = 0, ex1 = 0;
+        const bool two = fused || q0 + kScanTile + B <= size;  // tile-uniform
         {
+            const uint32_t a = v[2] - v[0];
+            const uint32_t b = (v[3] + (uint32_t)(q0 + B) * v[2]) - (v[1] + (uint32_t)q0 * v[0]);
+            uint32_t incl[4];
+            if (two) {
+                incl[0] = wave_incl_scan(a);
+                incl[1] = wave_incl_scan(b);
+                if (lane == 63) wsum[parity][wave] = make_uint4(incl[0], incl[1], 0, 0);
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; c++) incl[c] = wave_incl_scan(v[c]);
+                if (lane == 63) wsum[parity][wave] = make_uint4(incl[0], incl[1], incl[2], incl[3]);
+            }
+            __syncthreads();
+            // the partials of the waves before this one: lane l of every row
+            // reads wave l's (zero for l >= wave), each row sums its 16 lanes
             const uint32_t w = lane & 15u;
             uint4 p = wsum[parity][min(w, kWaves - 1)];
             if (w >= wave) p = make_uint4(0, 0, 0, 0);
-            add = make_uint4(row16_sum(p.x), row16_sum(p.y), row16_sum(p.z), row16_sum(p.w));
+            if (two) {
+                exA = incl[0] - a + row16_sum(p.x);
+                exB = incl[1] - b + row16_sum(p.y);
+            } else {
+                uint32_t ex[4];
+                const uint32_t add[4] = {row16_sum(p.x), row16_sum(p.y), row16_sum(p.z), row16_sum(p.w)};
+#pragma unroll
+                for (int c = 0; c < 4; c++) ex[c] = incl[c] - v[c] + add[c];
+                exA = ex[2] - ex[0];
+                exB = (ex[3] + (uint32_t)(q0 + B) * ex[2]) - (ex[1] + (uint32_t)q0 * ex[0]);
+                ex0 = ex[0];
+                ex1 = ex[1];
+            }
         }
         if (fused && t != t_begin) {  // the previous tile's last lane left this tile's start window
             const uint2 c = carry[parity];
             D1 = __builtin_amdgcn_readfirstlane(c.x);
             DM = __builtin_amdgcn_readfirstlane(c.y);
         }
-        const uint32_t ex[4] = {incl[0] - v[0] + add.x, incl[1] - v[1] + add.y, incl[2] - v[2] + add.z,
-                                incl[3] - v[3] + add.w};
         parity ^= 1u;
         // Lanes past `end` stay in the loop (they never hit): the probes spread the
         // wave's parked hits over all 64 lanes.
         uint32_t W1, W2, k;
         if (fused) {
             // window [qt, qt + B) = [q0, q0 + B) - [q0, qt) + [q0 + B, qt + B)
-            W1 = D1 - ex[0] + ex[2];
-            const uint32_t M = DM + (ex[3] + (uint32_t)(q0 + B) * ex[2]) - (ex[1] + (uint32_t)q0 * ex[0]);
+            W1 = D1 + exA;
+            const uint32_t M = DM + exB;
             k = qt + B <= size ? B : (qt < size ? (uint32_t)(size - qt) : 0u);
             W2 = (uint32_t)(qt + k) * W1 - M;
         } else if (qt + B <= size) {
-            // P, Q at qt
-            const uint32_t Pq = pre[t].p + ex[0];
-            const uint32_t Qq = pre[t].q + ex[1] + (uint32_t)q0 * ex[0];
+            // W1 = P[qt + B] - P[qt], Q likewise: the tile constants P[q0 + B] -
+            // P[q0] (Q[...]) plus the in-tile prefix differences exA (exB)
             const uint32_t u = min(t + Bt, ntiles);  // tile holding q0 + B
             const uint32_t ur1 = u < ntiles ? agg[u].r1 : 0u, ur2 = u < ntiles ? agg[u].r2 : 0u;
             const uint32_t Pb = pre[u].p + ur1;                                              // P[q0 + B]
             const uint32_t Qb = pre[u].q + ur2 + (uint32_t)((uint64_t)u * kScanTile) * ur1;  // Q[q0 + B]
-            const uint32_t Pe = Pb + ex[2];
-            const uint32_t Qe = Qb + ex[3] + (uint32_t)(q0 + B) * ex[2];
-            W1 = Pe - Pq;
-            W2 = (uint32_t)(qt + B) * W1 - (Qe - Qq);
+            W1 = (Pb - pre[t].p) + exA;
+            W2 = (uint32_t)(qt + B) * W1 - ((Qb - pre[t].q) + exB);
             k = B;
         } else {
-            const uint32_t Pq = pre[t].p + ex[0];
-            const uint32_t Qq = pre[t].q + ex[1] + (uint32_t)q0 * ex[0];
+            const uint32_t Pq = pre[t].p + ex0;
+            const uint32_t Qq = pre[t].q + ex1 + (uint32_t)q0 * ex0;
             W1 = tot.p - Pq;
             W2 = (uint32_t)size * W1 - (tot.q - Qq);
             k = qt < size ? (uint32_t)(size - qt) : 0u;
