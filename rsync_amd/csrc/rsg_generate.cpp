@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -92,14 +93,24 @@ int64_t parallel_read(const std::vector<ReadJob> &jobs, int *code) {
     std::atomic<size_t> next{0};
     std::atomic<int64_t> bad{-1};
     std::atomic<int> bad_code{0};
+    std::mutex bad_mu;
     auto worker = [&] {
         for (size_t k; (k = next.fetch_add(1)) < jobs.size();) {
-            if (bad.load() >= 0) return;
+            // jobs are taken in index order, so every job below a recorded
+            // failure is already running: finish those, skip the rest
+            const int64_t b0 = bad.load();
+            if (b0 >= 0 && (int64_t)k > b0) return;
             const ReadJob &j = jobs[k];
             const int r = read_full(j.fd, j.dst, j.n, j.off);
             if (r != 0) {
-                int64_t exp = -1;
-                if (bad.compare_exchange_strong(exp, (int64_t)k)) bad_code = r;
+                // keep the LOWEST failing job, as the reference's sequential
+                // loop (generator.go:332-348) would report the first file
+                std::lock_guard<std::mutex> lk(bad_mu);
+                const int64_t cur = bad.load();
+                if (cur < 0 || (int64_t)k < cur) {
+                    bad = (int64_t)k;
+                    bad_code = r;
+                }
             }
         }
     };
