@@ -93,8 +93,17 @@ hipError_t launch_resolve(const uint8_t *records, const DevFile *files, uint64_t
                           int32_t s2len, int32_t *res, hipStream_t stream);
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
-                       const uint32_t *bitmap, const uint64_t *table, uint32_t bmask, uint64_t *cand,
-                       uint32_t cap, uint32_t *count, uint32_t grid, bool fused, hipStream_t stream);
+                       const uint32_t *bitmap, const uint16_t *filter16, const uint64_t *table, uint32_t bmask,
+                       uint64_t *cand, uint32_t cap, uint32_t *count, uint32_t grid, bool fused,
+                       hipStream_t stream);
+// The packed roll's filter (roll_packed_kernel, fused mode, interior tiles):
+// 2^16 16-bit words, word (s1 + 128 B) mod 2^16, bits s2[0..3] and s2[4..7].
+constexpr uint32_t kFilter16Words = 1u << 16;
+__host__ __device__ inline uint32_t f16_word(uint32_t sum, uint32_t B) { return (sum + 128u * B) & 0xffffu; }
+__host__ __device__ inline uint32_t f16_mask(uint32_t sum) {
+    return (1u << ((sum >> 16) & 15u)) | (1u << ((sum >> 20) & 15u));
+}
+int roll_packed();  // RSG_ROLL_PACKED (read once): 0 roll_kernel only, 1 packed + ballots, 2 packed + lane slots
 // Block lengths up to which roll derives its window sums itself (no tile_agg
 // / tile_scan passes): each workgroup reads B extra bytes once.
 constexpr uint32_t kFusedMaxB = 4 * kScanTile;

@@ -106,9 +106,10 @@ struct Search {
     std::function<bool()> hook_ready;        // hook() would not wait
     std::function<rsg_status()> tail;        // set by finish(): the rest of the job (wait + walk), any thread
     // device tables inside the slot's blob
-    uint64_t off_hi16 = 0, off_sum2 = 0, off_filter = 0, off_table = 0, blob_bytes = 0;
+    uint64_t off_hi16 = 0, off_sum2 = 0, off_filter = 0, off_filter16 = 0, off_table = 0, blob_bytes = 0;
     const uint2 *d_groups = nullptr;
     const uint32_t *d_hi16 = nullptr, *d_filter = nullptr;
+    const uint16_t *d_filter16 = nullptr;  // packed roll (nullptr: not built)
     const uint8_t *d_sum2 = nullptr;
     const uint64_t *d_table = nullptr;
     uint32_t ntiles = 0, tile_end = 0, bmask = 0, cus = 256;
@@ -413,6 +414,12 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
             bitmap[rsg::filter_word(h)] |= rsg::filter_mask(h);
         }
     }
+    // the packed roll's filter (interior tiles of the fused mode)
+    std::vector<uint16_t> filter16;
+    if ((uint32_t)B <= rsg::kFusedMaxB && rsg::roll_packed()) {
+        filter16.assign(rsg::kFilter16Words, 0);
+        for (auto &kv : keys) filter16[rsg::f16_word(kv.first, (uint32_t)B)] |= (uint16_t)rsg::f16_mask(kv.first);
+    }
     uint32_t nb = 16;
     while (nb < keys.size() / 2) nb <<= 1;
     std::vector<uint64_t> table;
@@ -435,11 +442,12 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
     static_assert(sizeof(S.groups[0]) == 8, "(sum1, block) pair must be 8 bytes");
     auto up = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
     const uint64_t n_groups = S.groups.size() * 8, n_hi16 = S.hi16.size() * 4, n_sum2 = (uint64_t)count * 16;
-    const uint64_t n_filter = bitmap.size() * 4, n_table = table.size() * 8;
+    const uint64_t n_filter = bitmap.size() * 4, n_table = table.size() * 8, n_filter16 = filter16.size() * 2;
     S.off_hi16 = up(n_groups);
     S.off_sum2 = S.off_hi16 + up(n_hi16);
     S.off_filter = S.off_sum2 + up(n_sum2);
-    S.off_table = S.off_filter + up(n_filter);
+    S.off_filter16 = S.off_filter + up(n_filter);
+    S.off_table = S.off_filter16 + up(n_filter16);
     S.blob_bytes = S.off_table + up(n_table);
     rsg_status s;
     if ((s = ensure_pin(ctx, sl.stage, S.blob_bytes)) != RSG_OK) return s;
@@ -448,6 +456,7 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
     memcpy(st + S.off_hi16, S.hi16.data(), n_hi16);
     if (n_sum2) memcpy(st + S.off_sum2, sum2, n_sum2);
     memcpy(st + S.off_filter, bitmap.data(), n_filter);
+    if (n_filter16) memcpy(st + S.off_filter16, filter16.data(), n_filter16);
     memcpy(st + S.off_table, table.data(), n_table);
     S.pt.mark("tables");
     return RSG_OK;
@@ -493,6 +502,7 @@ rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
     S.d_hi16 = (const uint32_t *)(blob + S.off_hi16);
     S.d_sum2 = blob + S.off_sum2;
     S.d_filter = (const uint32_t *)(blob + S.off_filter);
+    S.d_filter16 = S.off_table > S.off_filter16 ? (const uint16_t *)(blob + S.off_filter16) : nullptr;
     S.d_table = (const uint64_t *)(blob + S.off_table);
     RSG_HIP(ctx, hipStreamWaitEvent(S.st, sl.scanned, 0));
 
@@ -515,7 +525,7 @@ rsg_status launch_range(Search &S, uint32_t lo, uint32_t hi) {
     hipEvent_t t0 = timed_begin(ctx, S.st);
     RSG_HIP(ctx, rsg::launch_roll(S.d_src, S.size, (uint32_t)S.head.block_len, (uint32_t)S.head.rem, (uint64_t)S.end,
                                   lo, hi, (const TileAgg *)sl.agg.p, (const TilePrefix *)sl.prefix.p, S.ntiles,
-                                  S.d_filter, S.d_table, S.bmask, (uint64_t *)sl.list.p, kCandCap,
+                                  S.d_filter, S.d_filter16, S.d_table, S.bmask, (uint64_t *)sl.list.p, kCandCap,
                                   (uint32_t *)sl.counts.p, S.cus, S.fused, S.st));
     timed_end(ctx, t0, S.st, 0);
     RSG_HIP(ctx, hipMemcpyAsync(sl.count.p, sl.counts.p, 4, hipMemcpyDeviceToHost, S.st));

@@ -23,6 +23,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+#include <type_traits>
+
 #include "rsg_internal.h"
 
 namespace rsg {
@@ -596,6 +599,563 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     drain_rest(qh ^ 1, prev_q0, 0, prev_n);  // the last tile's hits
 }
 
+// --------------------------------------------------------------- roll, packed
+// Interior tiles of the fused mode (every window has length B, every offset
+// is visited), two offsets per VALU instruction.  S1 and S2 only matter mod
+// 2^16 (match.go:106), so a lane rolls two windows at once in 16-bit halves:
+// stream a = its offsets 0..15, stream b = its offsets 16..31.
+//   P1 = (W1_a + 128B, W1_b + 128B)   P2 = (W2_a, W2_b)          (mod 2^16)
+// over bytes u = x ^ 0x80 (SignExtend(x) = u - 128, rsyncchecksum.go:24-27):
+//   P1 += u_in - u_out;  P2 += P1 - B u_out      (= match.go:175-191's update:
+//   W1 += x_in - x_out;  W2 += W1 - B x_out, the 128B in P1 absorbs the -128s)
+// one v_perm per operand pair and four v_pk_* per two offsets.  The filter is
+// 2^16 16-bit words indexed by P1's half itself (word (W1 + 128B) mod 2^16,
+// the host builds it shifted), bits W2[0..3] and W2[4..7]: a 16-bit shift of
+// both halves at once (v_pk_lshrrev_b16) per bit.  1.0 % of non-matching
+// offsets pass with 32768 basis sums (0.7 % for roll_kernel's 32-bit words,
+// which cost a full-width test per offset).
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// v_pk_lshrrev_b16: each half of w shifted right by the low 4 bits of the
+// same half of s (the hardware's own masking; a C shift needs an explicit
+// `& 15` the compiler keeps).
+__device__ __forceinline__ u16x2 pk_shr(u16x2 w, u16x2 s) {
+    uint32_t d;
+    asm("v_pk_lshrrev_b16 %0, %1, %2" : "=v"(d) : "v"(as_u32(s)), "v"(as_u32(w)));
+    return as_u16x2(d);
+}
+
+// Byte p of wa in the low half, byte p of wb in the high half (zero-extended).
+__device__ __forceinline__ u16x2 pair_bytes(uint32_t wa, uint32_t wb, int p) {
+    const uint32_t sel = 0x0c000c00u | ((4u + (uint32_t)p) << 16) | (uint32_t)p;
+    return as_u16x2(__builtin_amdgcn_perm(wb, wa, sel));
+}
+
+__global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
+    const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t tile_lo, uint32_t tile_hi,
+    const uint16_t *__restrict__ filter_g, const uint64_t *__restrict__ table, uint32_t bmask,
+    uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count) {
+    constexpr uint32_t kWaves = kRollThreads / 64;
+    constexpr uint32_t P = kRollPerThread;  // offsets per lane (2 streams of P/2)
+    constexpr int OW = (int)P / 4;
+    constexpr int NV = (int)P / 16;
+    constexpr int H = (int)P / 2;           // offsets per stream
+    static_assert(P == 32 && kWaves <= 16, "two streams of 16 offsets per lane");
+    __shared__ uint16_t filt[1u << 16];                   // 128 KiB
+    __shared__ uint2 queue[kWaves][2][kQueueCap];        // (tile-local offset, raw packed sum), per tile parity
+    __shared__ uint2 wsum[2][kWaves];                     // scan partials, double-buffered per tile
+    __shared__ uint2 carry[2];                            // next tile's (D1, DM), per tile parity
+    {
+        const uint4 *fg = reinterpret_cast<const uint4 *>(filter_g);
+        uint4 *fl = reinterpret_cast<uint4 *>(filt);
+        for (uint32_t i = threadIdx.x; i < (1u << 16) / 8; i += kRollThreads) fl[i] = fg[i];
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t C128 = (128u * B) & 0xffffu;  // the filter index offset of P1
+    uint32_t parity = 0;
+
+    // Exact probes of a wave's parked hits, as roll_kernel (every window here
+    // has length B: a block of length B must carry the sum).
+    auto probe = [&](uint64_t q, uint32_t fl) {
+        if (fl & 2u) {
+            const uint32_t at = atomicAdd(count, 1u);
+            if (at < cap) cand[at] = q;
+        }
+    };
+    auto unraw = [&](uint32_t raw) { return (raw & 0xffff0000u) | ((raw - C128) & 0xffffu); };
+    auto drain_rest = [&](uint32_t qh, uint64_t q0, uint32_t from, uint32_t n) {
+        for (uint32_t i = from + lane; i < n; i += 64) {
+            const uint2 e = queue[wave][qh][i];
+            probe(q0 + e.x, table_flags(table, bmask, unraw(e.y)));
+        }
+    };
+    uint32_t prev_n = 0, qh = 0;
+    uint64_t prev_q0 = 0;
+    const uint32_t per = (tile_hi - tile_lo + gridDim.x - 1) / gridDim.x;
+    const uint32_t t_begin = tile_lo + blockIdx.x * per;
+    const uint32_t t_end = min(tile_hi, t_begin + per);
+    const uint32_t lo = threadIdx.x * P;
+    const uint32_t sh = B & 3u;
+    // The run's first window [q0, q0 + B): D1 = sum x, DM = sum i*x (absolute i).
+    uint32_t D1 = 0, DM = 0;
+    if (t_begin < t_end) {
+        const uint64_t qb = (uint64_t)t_begin * kScanTile;
+        uint32_t a1 = 0, a2 = 0;
+        for (uint32_t off = threadIdx.x * 16u; off < B; off += kRollThreads * 16u) {
+            uint32_t w[4];
+            load_vec(src, size, qb + off, w);
+            if (off + 16u > B) {
+                const uint32_t keep = B - off;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++) {
+                    const uint32_t nb = keep > 4 * q ? min(keep - 4 * q, 4u) : 0u;
+                    w[q] &= nb >= 4 ? 0xffffffffu : ((1u << (8 * nb)) - 1u);
+                }
+            }
+            int32_t v1, v2;
+            vec_sums(w, v1, v2);
+            a1 += (uint32_t)v1;
+            a2 += (uint32_t)v2 + (uint32_t)(qb + off) * (uint32_t)v1;
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            a1 += __shfl_xor(a1, m, 64);
+            a2 += __shfl_xor(a2, m, 64);
+        }
+        if (lane == 0) wsum[0][wave] = make_uint2(a1, a2);
+        __syncthreads();
+#pragma unroll
+        for (uint32_t w = 0; w < kWaves; w++) {
+            D1 += __builtin_amdgcn_readfirstlane(wsum[0][w].x);
+            DM += __builtin_amdgcn_readfirstlane(wsum[0][w].y);
+        }
+        __syncthreads();
+    }
+    uint32_t O[OW], A[OW + 4], On[OW];
+    auto fetch_plain = [&](uint32_t tt, uint32_t *o, uint32_t *a) {
+        const uint8_t *p = src + (uint64_t)tt * kScanTile + lo;
+#pragma unroll
+        for (int q = 0; q < NV; q++) {
+            const u32x4a4m v = *reinterpret_cast<const u32x4a4m *>(p + 16 * q);
+            o[4 * q] = v.x; o[4 * q + 1] = v.y; o[4 * q + 2] = v.z; o[4 * q + 3] = v.w;
+        }
+        const uint8_t *pa = p + B - sh;
+#pragma unroll
+        for (int q = 0; q < NV + 1; q++) {
+            const u32x4a4m v = *reinterpret_cast<const u32x4a4m *>(pa + 16 * q);
+            a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
+        }
+    };
+    if (t_begin < t_end) fetch_plain(t_begin, O, A);
+    const u16x2 negB = as_u16x2(((0x10000u - (B & 0xffffu)) & 0xffffu) * 0x10001u);
+    for (uint32_t t = t_begin; t < t_end; t++) {
+        const uint64_t q0 = (uint64_t)t * kScanTile;
+        const uint64_t qt = q0 + lo;
+        uint32_t S[OW];
+#pragma unroll
+        for (int k = 0; k < OW; k++) S[k] = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sh);
+        const bool next = t + 1 < t_end;
+        if (next) fetch_plain(t + 1, On, A);
+        uint2 pe = make_uint2(0, 0);
+        uint64_t pb[2 * kBucketWays];
+        const bool pv = lane < prev_n;
+        if (pv) {
+            pe = queue[wave][qh ^ 1][lane];
+            pe.y = unraw(pe.y);
+            const uint64_t *b1 = table + (uint64_t)(bucket_hash1(pe.y) & bmask) * kBucketWays;
+            const uint64_t *b2 = table + (uint64_t)(bucket_hash2(pe.y) & bmask) * kBucketWays;
+#pragma unroll
+            for (uint32_t i = 0; i < kBucketWays; i++) { pb[i] = b1[i]; pb[kBucketWays + i] = b2[i]; }
+        }
+        // lane totals, and the first 16 bytes' own (stream a's range) for
+        // stream b's start window
+        int32_t o1, o2, s1, s2, v1, v2;
+        vec_sums(O, o1, o2);
+        vec_sums(S, s1, s2);
+        const int32_t o1a = o1, o2a = o2, s1a = s1, s2a = s2;
+#pragma unroll
+        for (int c = 1; c < NV; c++) {
+            vec_sums(O + 4 * c, v1, v2);
+            o2 += v2 + 16 * c * v1;
+            o1 += v1;
+            vec_sums(S + 4 * c, v1, v2);
+            s2 += v2 + 16 * c * v1;
+            s1 += v1;
+        }
+        // one workgroup scan of exA = ex(s1) - ex(o1), exB (roll_kernel's
+        // two-value form: every window here is interior)
+        uint32_t exA, exB;
+        {
+            const uint32_t so2 = (uint32_t)s2 + lo * (uint32_t)s1, oo2 = (uint32_t)o2 + lo * (uint32_t)o1;
+            const uint32_t a = (uint32_t)s1 - (uint32_t)o1;
+            const uint32_t b = (so2 + (uint32_t)(q0 + B) * (uint32_t)s1) - (oo2 + (uint32_t)q0 * (uint32_t)o1);
+            const uint32_t ia = wave_incl_scan(a), ib = wave_incl_scan(b);
+            if (lane == 63) wsum[parity][wave] = make_uint2(ia, ib);
+            __syncthreads();
+            const uint32_t w = lane & 15u;
+            uint2 p = wsum[parity][min(w, kWaves - 1)];
+            if (w >= wave) p = make_uint2(0, 0);
+            exA = ia - a + row16_sum(p.x);
+            exB = ib - b + row16_sum(p.y);
+        }
+        if (t != t_begin) {
+            const uint2 c = carry[parity];
+            D1 = __builtin_amdgcn_readfirstlane(c.x);
+            DM = __builtin_amdgcn_readfirstlane(c.y);
+        }
+        parity ^= 1u;
+        // window at the lane's first offset, then at its 17th (16 rolling
+        // steps in closed form: W1 + sum d, W2 + 16 W1 + sum (16 - j) d_j - B sum x_out)
+        const uint32_t W1 = D1 + exA;
+        const uint32_t W2 = (uint32_t)(qt + B) * W1 - (DM + exB);
+        const uint32_t da = (uint32_t)(s1a - o1a);
+        const uint32_t W1b = W1 + da;
+        const uint32_t W2b = W2 + 16u * W1 + 16u * da - (uint32_t)(s2a - o2a) - B * (uint32_t)o1a;
+        u16x2 P1 = as_u16x2(((W1 + C128) & 0xffffu) | ((W1b + C128) << 16));
+        u16x2 P2 = as_u16x2((W2 & 0xffffu) | (W2b << 16));
+        uint32_t Ox[OW], Sx[OW];
+#pragma unroll
+        for (int k = 0; k < OW; k++) {
+            Ox[k] = O[k] ^ 0x80808080u;
+            Sx[k] = S[k] ^ 0x80808080u;
+        }
+        uint32_t lol = lo;
+        asm volatile("" : "+v"(lol));
+        uint32_t nq = 0;
+        auto park = [&](bool hit, uint32_t j, uint32_t raw) {
+            const uint64_t bal = __ballot(hit);
+            if (bal) {
+                const uint32_t nb = __popcll(bal);
+                if (nq + nb <= kQueueCap) {
+                    if (hit) {
+                        const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                            (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                        queue[wave][qh][nq + below] = make_uint2(lol + j, raw);
+                    }
+                    nq += nb;
+                } else if (hit) {
+                    const uint32_t at = atomicAdd(count, 1u);
+                    if (at < cap) cand[at] = q0 + lol + j;
+                }
+            }
+        };
+        constexpr int G = 4;  // pair steps per group: 8 filter reads in flight
+#pragma unroll
+        for (int g0 = 0; g0 < H; g0 += G) {
+            u16x2 p1[G], p2[G], wd[G];
+#pragma unroll
+            for (int jj = 0; jj < G; jj++) {
+                const int j = g0 + jj;
+                p1[jj] = P1;
+                p2[jj] = P2;
+                wd[jj] = u16x2{filt[P1.x], filt[P1.y]};
+                const u16x2 uo = pair_bytes(Ox[j >> 2], Ox[(j >> 2) + OW / 2], j & 3);
+                const u16x2 ui = pair_bytes(Sx[j >> 2], Sx[(j >> 2) + OW / 2], j & 3);
+                P1 = P1 + ui - uo;
+                P2 = P2 + uo * negB + P1;
+            }
+#pragma unroll
+            for (int jj = 0; jj < G; jj++) {
+                const int j = g0 + jj;
+                const u16x2 x = pk_shr(wd[jj], p2[jj]);
+                const u16x2 y = pk_shr(wd[jj], p2[jj] >> (uint16_t)4);
+                uint32_t z = as_u32(x & y) & 0x00010001u;
+                asm("" : "+v"(z));
+                const uint32_t r1 = as_u32(p1[jj]), r2 = as_u32(p2[jj]);
+                park((z & 0xffffu) != 0, (uint32_t)j, __builtin_amdgcn_perm(r2, r1, 0x05040100u));
+                park(z > 0xffffu, (uint32_t)(H + j), __builtin_amdgcn_perm(r2, r1, 0x07060302u));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // the tile's last lane ends at the next tile's first window
+        if (threadIdx.x == kRollThreads - 1) {
+            const uint32_t w1 = ((as_u32(P1) >> 16) - C128) & 0xffffu, w2 = as_u32(P2) >> 16;
+            carry[parity] = make_uint2(w1, (uint32_t)(q0 + kScanTile + B) * w1 - w2);
+        }
+        if (pv) {
+            uint32_t fl = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 2 * kBucketWays; i++)
+                if ((uint32_t)(pb[i] >> 32) == pe.y && (uint32_t)pb[i] != 0) fl |= (uint32_t)pb[i];
+            probe(prev_q0 + pe.x, fl);
+        }
+        if (prev_n > 64) drain_rest(qh ^ 1, prev_q0, 64, prev_n);
+        prev_n = nq;
+        prev_q0 = q0;
+        qh ^= 1u;
+        if (next) {
+#pragma unroll
+            for (int k = 0; k < OW; k++) O[k] = On[k];
+        }
+    }
+    drain_rest(qh ^ 1, prev_q0, 0, prev_n);
+}
+
+// --------------------------------------------------------------- roll, packed, lane slots
+// roll_packed_kernel's arithmetic and filter with lane-private parking: the
+// offset loop has no ballot and no scalar bookkeeping.  A pair step with a
+// filter hit stores the lane's (P1, P2) in its next LDS slot (c += hit, an
+// exec-masked store); the hit bits go to a per-lane mask
+// (bit j: stream a at step j, bit 16 + j: stream b).  A lane keeps up to
+// kLaneSlots entries per tile; a wave in which some lane parked more (its
+// writes ran into its neighbours' slots, never past the wave's padded region)
+// rolls the tile again with synchronous exact probes (rare: about 1.6 % of
+// wave-tiles at the 1 % filter rate; every tile on repetitive data).  The
+// exact probes of tile t run during tile t + 1: its first item's bucket loads
+// are issued before the offset loop and compared after it, further items
+// probed in place.
+constexpr uint32_t kLaneSlots = 3;
+constexpr uint32_t kLanePad = 16;  // a lane advances at most once per pair step
+
+template <bool DIAG>  // DIAG: timing only, no redo and no in-place probes (results incomplete)
+__global__ __launch_bounds__(kRollThreads) void roll_lane_kernel(
+    const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t tile_lo, uint32_t tile_hi,
+    const uint16_t *__restrict__ filter_g, const uint64_t *__restrict__ table, uint32_t bmask,
+    uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count) {
+    constexpr uint32_t kWaves = kRollThreads / 64;
+    constexpr uint32_t P = kRollPerThread;
+    constexpr int OW = (int)P / 4;
+    constexpr int NV = (int)P / 16;
+    constexpr int H = (int)P / 2;
+    static_assert(P == 32 && kWaves <= 16 && H <= kLanePad, "two streams of 16 offsets per lane");
+    __shared__ uint16_t filt[1u << 16];                                 // 128 KiB
+    __shared__ uint2 slots[kWaves][64 * kLaneSlots + kLanePad];         // 26 KiB
+    __shared__ uint2 wsum[2][kWaves];
+    __shared__ uint2 carry[2];
+    {
+        const uint4 *fg = reinterpret_cast<const uint4 *>(filter_g);
+        uint4 *fl = reinterpret_cast<uint4 *>(filt);
+        for (uint32_t i = threadIdx.x; i < (1u << 16) / 8; i += kRollThreads) fl[i] = fg[i];
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t C128 = (128u * B) & 0xffffu;
+    uint2 *const myslot = &slots[wave][lane * kLaneSlots];
+    uint32_t parity = 0;
+
+    auto unraw = [&](uint32_t raw) { return (raw & 0xffff0000u) | ((raw - C128) & 0xffffu); };
+    auto emit = [&](uint64_t q) {
+        const uint32_t at = atomicAdd(count, 1u);
+        if (at < cap) cand[at] = q;
+    };
+    // item = lowest set bit of a hit mask m (bit j: stream a, step j; bit
+    // 16 + j: stream b), its entry = the number of steps below j with a hit
+    auto item = [&](uint32_t m, uint32_t mall, uint2 e0, uint2 e1, uint2 e2, uint32_t &off, uint32_t &sum) {
+        const uint32_t b = __builtin_ctz(m);
+        const uint32_t j = b & 15u;
+        const uint32_t any = (mall | (mall >> 16)) & ((1u << j) - 1u);
+        const uint32_t k = __builtin_popcount(any);
+        const uint2 e = k == 0 ? e0 : (k == 1 ? e1 : e2);
+        const uint32_t raw = b >= 16 ? __builtin_amdgcn_perm(e.y, e.x, 0x07060302u)
+                                     : __builtin_amdgcn_perm(e.y, e.x, 0x05040100u);
+        off = b >= 16 ? j + (uint32_t)H : j;
+        sum = unraw(raw);
+    };
+    const uint32_t per = (tile_hi - tile_lo + gridDim.x - 1) / gridDim.x;
+    const uint32_t t_begin = tile_lo + blockIdx.x * per;
+    const uint32_t t_end = min(tile_hi, t_begin + per);
+    const uint32_t lo = threadIdx.x * P;
+    const uint32_t sh = B & 3u;
+    uint32_t D1 = 0, DM = 0;
+    if (t_begin < t_end) {
+        const uint64_t qb = (uint64_t)t_begin * kScanTile;
+        uint32_t a1 = 0, a2 = 0;
+        for (uint32_t off = threadIdx.x * 16u; off < B; off += kRollThreads * 16u) {
+            uint32_t w[4];
+            load_vec(src, size, qb + off, w);
+            if (off + 16u > B) {
+                const uint32_t keep = B - off;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++) {
+                    const uint32_t nb = keep > 4 * q ? min(keep - 4 * q, 4u) : 0u;
+                    w[q] &= nb >= 4 ? 0xffffffffu : ((1u << (8 * nb)) - 1u);
+                }
+            }
+            int32_t v1, v2;
+            vec_sums(w, v1, v2);
+            a1 += (uint32_t)v1;
+            a2 += (uint32_t)v2 + (uint32_t)(qb + off) * (uint32_t)v1;
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            a1 += __shfl_xor(a1, m, 64);
+            a2 += __shfl_xor(a2, m, 64);
+        }
+        if (lane == 0) wsum[0][wave] = make_uint2(a1, a2);
+        __syncthreads();
+#pragma unroll
+        for (uint32_t w = 0; w < kWaves; w++) {
+            D1 += __builtin_amdgcn_readfirstlane(wsum[0][w].x);
+            DM += __builtin_amdgcn_readfirstlane(wsum[0][w].y);
+        }
+        __syncthreads();
+    }
+    uint32_t O[OW], A[OW + 4], On[OW];
+    auto fetch_plain = [&](uint32_t tt, uint32_t *o, uint32_t *a) {
+        const uint8_t *p = src + (uint64_t)tt * kScanTile + lo;
+#pragma unroll
+        for (int q = 0; q < NV; q++) {
+            const u32x4a4m v = *reinterpret_cast<const u32x4a4m *>(p + 16 * q);
+            o[4 * q] = v.x; o[4 * q + 1] = v.y; o[4 * q + 2] = v.z; o[4 * q + 3] = v.w;
+        }
+        const uint8_t *pa = p + B - sh;
+#pragma unroll
+        for (int q = 0; q < NV + 1; q++) {
+            const u32x4a4m v = *reinterpret_cast<const u32x4a4m *>(pa + 16 * q);
+            a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
+        }
+    };
+    if (t_begin < t_end) fetch_plain(t_begin, O, A);
+    const u16x2 negB = as_u16x2(((0x10000u - (B & 0xffffu)) & 0xffffu) * 0x10001u);
+    // the previous tile's hit mask (its entries are still in the lane's slots)
+    uint32_t pmall = 0;
+    uint64_t pq = 0;  // q0 + lo of the previous tile
+    for (uint32_t t = t_begin; t < t_end; t++) {
+        const uint64_t q0 = (uint64_t)t * kScanTile;
+        const uint64_t qt = q0 + lo;
+        uint32_t S[OW];
+#pragma unroll
+        for (int k = 0; k < OW; k++) S[k] = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sh);
+        const bool next = t + 1 < t_end;
+        if (next) fetch_plain(t + 1, On, A);
+        // The previous tile's items, before this tile's offset loop reuses the
+        // slots: the first item's bucket loads now (they land during the sums
+        // and the scan below), the rest after the scan, in place.
+        const uint2 pe0 = myslot[0], pe1 = myslot[1], pe2 = myslot[2];
+        uint32_t pm = pmall;
+        uint32_t poff = 0, psum = 0;
+        uint64_t pb[2 * kBucketWays];
+        const bool pv = pm != 0;
+        if (pv) {
+            item(pm, pmall, pe0, pe1, pe2, poff, psum);
+            pm &= pm - 1u;
+            const uint64_t *b1 = table + (uint64_t)(bucket_hash1(psum) & bmask) * kBucketWays;
+            const uint64_t *b2 = table + (uint64_t)(bucket_hash2(psum) & bmask) * kBucketWays;
+#pragma unroll
+            for (uint32_t i = 0; i < kBucketWays; i++) { pb[i] = b1[i]; pb[kBucketWays + i] = b2[i]; }
+        }
+        int32_t o1, o2, s1, s2, v1, v2;
+        vec_sums(O, o1, o2);
+        vec_sums(S, s1, s2);
+        const int32_t o1a = o1, o2a = o2, s1a = s1, s2a = s2;
+#pragma unroll
+        for (int c = 1; c < NV; c++) {
+            vec_sums(O + 4 * c, v1, v2);
+            o2 += v2 + 16 * c * v1;
+            o1 += v1;
+            vec_sums(S + 4 * c, v1, v2);
+            s2 += v2 + 16 * c * v1;
+            s1 += v1;
+        }
+        uint32_t exA, exB;
+        {
+            const uint32_t so2 = (uint32_t)s2 + lo * (uint32_t)s1, oo2 = (uint32_t)o2 + lo * (uint32_t)o1;
+            const uint32_t a = (uint32_t)s1 - (uint32_t)o1;
+            const uint32_t b = (so2 + (uint32_t)(q0 + B) * (uint32_t)s1) - (oo2 + (uint32_t)q0 * (uint32_t)o1);
+            const uint32_t ia = wave_incl_scan(a), ib = wave_incl_scan(b);
+            if (lane == 63) wsum[parity][wave] = make_uint2(ia, ib);
+            __syncthreads();
+            const uint32_t w = lane & 15u;
+            uint2 p = wsum[parity][min(w, kWaves - 1)];
+            if (w >= wave) p = make_uint2(0, 0);
+            exA = ia - a + row16_sum(p.x);
+            exB = ib - b + row16_sum(p.y);
+        }
+        if (t != t_begin) {
+            const uint2 c = carry[parity];
+            D1 = __builtin_amdgcn_readfirstlane(c.x);
+            DM = __builtin_amdgcn_readfirstlane(c.y);
+        }
+        parity ^= 1u;
+        if (pv) {
+            uint32_t fl = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 2 * kBucketWays; i++)
+                if ((uint32_t)(pb[i] >> 32) == psum && (uint32_t)pb[i] != 0) fl |= (uint32_t)pb[i];
+            if (fl & 2u) emit(pq + poff);
+        }
+        while (!DIAG && pm != 0) {
+            uint32_t off, sum;
+            item(pm, pmall, pe0, pe1, pe2, off, sum);
+            pm &= pm - 1u;
+            if (table_flags(table, bmask, sum) & 2u) emit(pq + off);
+        }
+        const uint32_t W1 = D1 + exA;
+        const uint32_t W2 = (uint32_t)(qt + B) * W1 - (DM + exB);
+        const uint32_t da = (uint32_t)(s1a - o1a);
+        const uint32_t W1b = W1 + da;
+        const uint32_t W2b = W2 + 16u * W1 + 16u * da - (uint32_t)(s2a - o2a) - B * (uint32_t)o1a;
+        const u16x2 P10 = as_u16x2(((W1 + C128) & 0xffffu) | ((W1b + C128) << 16));
+        const u16x2 P20 = as_u16x2((W2 & 0xffffu) | (W2b << 16));
+        uint32_t Ox[OW], Sx[OW];
+#pragma unroll
+        for (int k = 0; k < OW; k++) {
+            Ox[k] = O[k] ^ 0x80808080u;
+            Sx[k] = S[k] ^ 0x80808080u;
+        }
+        // One pass over the lane's 16 pair steps; `sink(j, p1, p2, z)` gets
+        // each step's packed sums and its filter bits (bit 0: a, bit 16: b).
+        auto steps = [&](auto g_tag, auto &&sink) {
+            u16x2 P1 = P10, P2 = P20;
+            constexpr int G = decltype(g_tag)::value;
+#pragma unroll
+            for (int g0 = 0; g0 < H; g0 += G) {
+                u16x2 p1[G], p2[G], wd[G];
+#pragma unroll
+                for (int jj = 0; jj < G; jj++) {
+                    const int j = g0 + jj;
+                    p1[jj] = P1;
+                    p2[jj] = P2;
+                    wd[jj] = u16x2{filt[P1.x], filt[P1.y]};
+                    const u16x2 uo = pair_bytes(Ox[j >> 2], Ox[(j >> 2) + OW / 2], j & 3);
+                    const u16x2 ui = pair_bytes(Sx[j >> 2], Sx[(j >> 2) + OW / 2], j & 3);
+                    P1 = P1 + ui - uo;
+                    P2 = P2 + uo * negB + P1;
+                }
+#pragma unroll
+                for (int jj = 0; jj < G; jj++) {
+                    const u16x2 x = pk_shr(wd[jj], p2[jj]);
+                    const u16x2 y = pk_shr(wd[jj], p2[jj] >> (uint16_t)4);
+                    const uint32_t z = as_u32(x & y) & 0x00010001u;
+                    sink(g0 + jj, as_u32(p1[jj]), as_u32(p2[jj]), z);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            return make_uint2(as_u32(P1), as_u32(P2));
+        };
+        uint32_t m = 0, c = 0;
+        const uint2 fin = steps(std::integral_constant<int, 4>{}, [&](int j, uint32_t r1, uint32_t r2, uint32_t z) {
+            // a hit takes the lane's next slot (an exec-masked store: a lane
+            // with all its slots taken never writes past them on a miss)
+            if (z != 0) myslot[c] = make_uint2(r1, r2);
+            m |= z << j;
+            c += z != 0 ? 1u : 0u;
+        });
+        if (!DIAG && __ballot(c > kLaneSlots)) {
+            // Some lane of this wave parked more than its slots hold: roll the
+            // tile again, probing every hit in place (the slots are dropped).
+            // (one pair step per group: its probes are not hoisted together)
+            (void)steps(std::integral_constant<int, 1>{}, [&](int j, uint32_t r1, uint32_t r2, uint32_t z) {
+                if (__ballot(z != 0)) {
+                    if (z & 1u) {
+                        if (table_flags(table, bmask, unraw(__builtin_amdgcn_perm(r2, r1, 0x05040100u))) & 2u)
+                            emit(qt + (uint32_t)j);
+                    }
+                    if (z >> 16) {
+                        if (table_flags(table, bmask, unraw(__builtin_amdgcn_perm(r2, r1, 0x07060302u))) & 2u)
+                            emit(qt + (uint32_t)(H + j));
+                    }
+                }
+            });
+            m = 0;
+        }
+        if (threadIdx.x == kRollThreads - 1) {
+            const uint32_t w1 = ((fin.x >> 16) - C128) & 0xffffu, w2 = fin.y >> 16;
+            carry[parity] = make_uint2(w1, (uint32_t)(q0 + kScanTile + B) * w1 - w2);
+        }
+        // this tile's entries become the next tile's items
+        pmall = m;
+        pq = qt;
+        if (next) {
+#pragma unroll
+            for (int k = 0; k < OW; k++) O[k] = On[k];
+        }
+    }
+    const uint2 pe0 = myslot[0], pe1 = myslot[1], pe2 = myslot[2];
+    for (uint32_t pm = pmall; pm != 0;) {  // the last tile's items
+        uint32_t off, sum;
+        item(pm, pmall, pe0, pe1, pe2, off, sum);
+        pm &= pm - 1u;
+        if (table_flags(table, bmask, sum) & 2u) emit(pq + off);
+    }
+}
+
 // --------------------------------------------------------------- confirm plan
 // One DevFile per candidate window, in the roll's append order: window
 // [q, q + min(B, size - q)) is record i (match.go:114-117).  The confirmation
@@ -673,6 +1233,16 @@ hipError_t launch_tile_scan(const TileAgg *agg, uint32_t ntiles, TilePrefix *pre
     return hipGetLastError();
 }
 
+int roll_packed() {
+    // A/B switch RSG_ROLL_PACKED: 0 = roll_kernel for every tile, 1
+    // (default) = the packed roll with ballot parking, 2 = with lane slots
+    static const int v = [] {
+        const char *e = getenv("RSG_ROLL_PACKED");
+        return e ? std::max(0, std::min(3, atoi(e))) : 1;  // 3: lane slots without slow paths (timing only)
+    }();
+    return v;
+}
+
 bool roll_filter_sel() {
     static const bool sel = [] {
         const char *e = getenv("RSG_FILTER_SEL");  // A/B switch: 0 = the rotate-xor hash layout
@@ -683,9 +1253,29 @@ bool roll_filter_sel() {
 
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
-                       const uint32_t *bitmap, const uint64_t *table, uint32_t bmask, uint64_t *cand,
-                       uint32_t cap, uint32_t *count, uint32_t grid, bool fused, hipStream_t stream) {
+                       const uint32_t *bitmap, const uint16_t *filter16, const uint64_t *table, uint32_t bmask,
+                       uint64_t *cand, uint32_t cap, uint32_t *count, uint32_t grid, bool fused,
+                       hipStream_t stream) {
     if (tile_hi <= tile_lo) return hipSuccess;
+    if (fused && filter16) {
+        // Interior tiles [tile_lo, t_int) take the packed kernel: every offset
+        // of tile t visited ((t+1) T <= end) and its window and shifted-byte
+        // loads inside the source ((t+1) T + B + 48 <= size); the rest (the
+        // source's last B bytes or so) roll_kernel's edge path.
+        const uint64_t lim = std::min<uint64_t>(end, size >= (uint64_t)B + 48 ? size - B - 48 : 0);
+        const uint32_t t_int = (uint32_t)std::max<uint64_t>(tile_lo, std::min<uint64_t>(tile_hi, lim / kScanTile));
+        if (t_int > tile_lo) {
+            const uint32_t g = min(grid, t_int - tile_lo);
+            auto kern = roll_packed() == 1 ? roll_packed_kernel
+                        : roll_packed() == 3 ? roll_lane_kernel<true> : roll_lane_kernel<false>;
+            hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, tile_lo, t_int, filter16,
+                               table, bmask, cand, cap, count);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        tile_lo = t_int;
+        if (tile_hi <= tile_lo) return hipSuccess;
+    }
     const uint32_t g = min(grid, tile_hi - tile_lo);
     auto kern = roll_filter_sel() ? roll_kernel<true> : roll_kernel<false>;
     hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, tile_hi, agg,

@@ -98,6 +98,24 @@ def test_cfg3_shape_vs_oracle(eng):
     assert got == want
 
 
+@pytest.mark.parametrize("blen", [700, 4097, 32768, 65539, 131072])
+def test_packed_roll_runs_vs_oracle(eng, blen):
+    """The packed roll (interior tiles, two offsets per VALU op) over sources
+    of 12-20 MiB: every workgroup rolls a run of several 32 KiB tiles (the
+    carried start window), block lengths with every shifted-byte alignment
+    (B mod 4 = 0..3) up to kFusedMaxB, and the hand-off to roll_kernel's edge
+    path for the source's last tiles (match.go:93-210)."""
+    n = (12 << 20) + 12345 + 997 * (blen % 7)
+    basis = cases.splitmix64_bytes(4000 + blen, n)
+    src = cases.mutate(basis, 4100 + blen, 0.4, 1, 3 * blen, n_ins=6, n_del=6)
+    seed = 1234567 + blen
+    head, s1, s2 = basis_sums(basis, blen, seed)
+    tg = orc.stable_targets(s1)
+    want, _, _ = orc.hash_search(src, head, s1, s2, tg, seed)
+    assert len(want) > 20
+    assert eng.hash_search(src, head, s1, s2, tg, seed) == want
+
+
 def test_identical_large_property(eng):
     """1 GiB source identical to its basis (B = 32768): every block matches at
     its own offset, in order (size-independent property at full cfg3 file size)."""
