@@ -94,12 +94,21 @@ hipError_t launch_resolve(const uint8_t *records, const DevFile *files, uint64_t
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
                        const uint32_t *bitmap, const uint16_t *filter16, const uint64_t *table, uint32_t bmask,
-                       uint64_t *cand, uint32_t cap, uint32_t *count, uint32_t grid, bool fused,
-                       hipStream_t stream);
+                       uint64_t *cand, uint32_t cap, uint32_t *count, uint32_t grid, bool fused, uint2 *spill,
+                       uint32_t *spill_n, hipStream_t stream);
+// Spill regions of the lane-slot packed roll: kRollSpillCap (offset, sum)
+// items per roll wave (grid x 16 waves), and one count per wave.
+constexpr uint32_t kRollSpillCap = 1024;
+inline uint64_t roll_spill_bytes(uint32_t grid) { return (uint64_t)grid * (kRollThreads / 64) * kRollSpillCap * 8; }
 // The packed roll's filter (roll_packed_kernel, fused mode, interior tiles):
-// 2^16 16-bit words, word (s1 + 128 B) mod 2^16, bits s2[0..3] and s2[4..7].
+// 2^16 16-bit words, word ((s1 + 128 B) xor s2) mod 2^16, bits s2[0..3] and
+// s2[4..7].  s1 of a long window of random bytes is a sum of B terms (near-
+// Gaussian mod 2^16): a word indexed by s1 alone passed 1.9 % of real window
+// sums, the xor with s2 ~1.0 %.
 constexpr uint32_t kFilter16Words = 1u << 16;
-__host__ __device__ inline uint32_t f16_word(uint32_t sum, uint32_t B) { return (sum + 128u * B) & 0xffffu; }
+__host__ __device__ inline uint32_t f16_word(uint32_t sum, uint32_t B) {
+    return ((sum + 128u * B) ^ (sum >> 16)) & 0xffffu;
+}
 __host__ __device__ inline uint32_t f16_mask(uint32_t sum) {
     return (1u << ((sum >> 16) & 15u)) | (1u << ((sum >> 20) & 15u));
 }

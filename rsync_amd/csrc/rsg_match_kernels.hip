@@ -609,11 +609,10 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
 //   P1 += u_in - u_out;  P2 += P1 - B u_out      (= match.go:175-191's update:
 //   W1 += x_in - x_out;  W2 += W1 - B x_out, the 128B in P1 absorbs the -128s)
 // one v_perm per operand pair and four v_pk_* per two offsets.  The filter is
-// 2^16 16-bit words indexed by P1's half itself (word (W1 + 128B) mod 2^16,
-// the host builds it shifted), bits W2[0..3] and W2[4..7]: a 16-bit shift of
-// both halves at once (v_pk_lshrrev_b16) per bit.  1.0 % of non-matching
-// offsets pass with 32768 basis sums (0.7 % for roll_kernel's 32-bit words,
-// which cost a full-width test per offset).
+// 2^16 16-bit words indexed by P1 ^ P2 (word ((W1 + 128B) ^ W2) mod 2^16, the
+// host builds it shifted; one v_xor for both windows), bits W2[0..3] and
+// W2[4..7]: a 16-bit shift of both halves at once (v_pk_lshrrev_b16) per bit.
+// About 1 % of non-matching window sums pass with 32768 basis sums.
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
@@ -833,7 +832,8 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 const int j = g0 + jj;
                 p1[jj] = P1;
                 p2[jj] = P2;
-                wd[jj] = u16x2{filt[P1.x], filt[P1.y]};
+                const u16x2 X = P1 ^ P2;  // the word index of both windows
+                wd[jj] = u16x2{filt[X.x], filt[X.y]};
                 const u16x2 uo = pair_bytes(Ox[j >> 2], Ox[(j >> 2) + OW / 2], j & 3);
                 const u16x2 ui = pair_bytes(Sx[j >> 2], Sx[(j >> 2) + OW / 2], j & 3);
                 P1 = P1 + ui - uo;
@@ -880,33 +880,38 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
 // roll_packed_kernel's arithmetic and filter with lane-private parking: the
 // offset loop has no ballot and no scalar bookkeeping.  A pair step with a
 // filter hit stores the lane's (P1, P2) in its next LDS slot (c += hit, an
-// exec-masked store); the hit bits go to a per-lane mask
-// (bit j: stream a at step j, bit 16 + j: stream b).  A lane keeps up to
-// kLaneSlots entries per tile; a wave in which some lane parked more (its
-// writes ran into its neighbours' slots, never past the wave's padded region)
-// rolls the tile again with synchronous exact probes (rare: about 1.6 % of
-// wave-tiles at the 1 % filter rate; every tile on repetitive data).  The
-// exact probes of tile t run during tile t + 1: its first item's bucket loads
-// are issued before the offset loop and compared after it, further items
-// probed in place.
+// exec-masked store); the hit bits go to a per-lane mask (bit j: stream a at
+// step j, bit 16 + j: stream b).  Nothing on the roll's path waits for an
+// exact probe:
+//  * at the start of tile t + 1 each lane's first item of tile t (its lowest
+//    hit bit) gets its bucket loads, compared after the tile's sums and scan;
+//  * its further items, and the hits of a lane whose kLaneSlots slots are
+//    taken (spilled from the offset loop itself, a rarely taken branch), go
+//    -- (offset from the workgroup's first tile, sum) -- to the wave's region
+//    of a global list at a position from an LDS counter per wave, and
+//    roll_spill_probe_kernel probes them after the roll.  A full region
+//    sends its overflow straight to the candidates (the confirmation
+//    re-checks them exactly, as roll_kernel's full queue does).
 constexpr uint32_t kLaneSlots = 3;
-constexpr uint32_t kLanePad = 16;  // a lane advances at most once per pair step
 
-template <bool DIAG>  // DIAG: timing only, no redo and no in-place probes (results incomplete)
+template <bool DIAG>  // DIAG: timing only, no redo and no spills (results incomplete)
 __global__ __launch_bounds__(kRollThreads) void roll_lane_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t tile_lo, uint32_t tile_hi,
     const uint16_t *__restrict__ filter_g, const uint64_t *__restrict__ table, uint32_t bmask,
-    uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count) {
+    uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count, uint2 *__restrict__ spill,
+    uint32_t spill_cap, uint32_t *__restrict__ spill_n) {
     constexpr uint32_t kWaves = kRollThreads / 64;
     constexpr uint32_t P = kRollPerThread;
     constexpr int OW = (int)P / 4;
     constexpr int NV = (int)P / 16;
     constexpr int H = (int)P / 2;
-    static_assert(P == 32 && kWaves <= 16 && H <= kLanePad, "two streams of 16 offsets per lane");
-    __shared__ uint16_t filt[1u << 16];                                 // 128 KiB
-    __shared__ uint2 slots[kWaves][64 * kLaneSlots + kLanePad];         // 26 KiB
+    static_assert(P == 32 && kWaves <= 16, "two streams of 16 offsets per lane");
+    __shared__ uint16_t filt[1u << 16];                   // 128 KiB
+    __shared__ uint2 slots[kWaves][64 * kLaneSlots];      // 24 KiB
     __shared__ uint2 wsum[2][kWaves];
     __shared__ uint2 carry[2];
+    __shared__ uint32_t wspill[kWaves];                   // spilled items per wave
+    if (threadIdx.x < kWaves) wspill[threadIdx.x] = 0;
     {
         const uint4 *fg = reinterpret_cast<const uint4 *>(filter_g);
         uint4 *fl = reinterpret_cast<uint4 *>(filt);
@@ -925,7 +930,8 @@ __global__ __launch_bounds__(kRollThreads) void roll_lane_kernel(
         if (at < cap) cand[at] = q;
     };
     // item = lowest set bit of a hit mask m (bit j: stream a, step j; bit
-    // 16 + j: stream b), its entry = the number of steps below j with a hit
+    // 16 + j: stream b), its entry = the number of steps below j with a hit;
+    // false for an entry past the slots (spilled from the loop already)
     auto item = [&](uint32_t m, uint32_t mall, uint2 e0, uint2 e1, uint2 e2, uint32_t &off, uint32_t &sum) {
         const uint32_t b = __builtin_ctz(m);
         const uint32_t j = b & 15u;
@@ -936,10 +942,19 @@ __global__ __launch_bounds__(kRollThreads) void roll_lane_kernel(
                                      : __builtin_amdgcn_perm(e.y, e.x, 0x05040100u);
         off = b >= 16 ? j + (uint32_t)H : j;
         sum = unraw(raw);
+        return k < kLaneSlots;
     };
     const uint32_t per = (tile_hi - tile_lo + gridDim.x - 1) / gridDim.x;
     const uint32_t t_begin = tile_lo + blockIdx.x * per;
     const uint32_t t_end = min(tile_hi, t_begin + per);
+    const uint64_t q_wg = (uint64_t)t_begin * kScanTile;  // spilled offsets are relative to it
+    uint2 *const region = spill + (uint64_t)(blockIdx.x * kWaves + wave) * spill_cap;
+    // Spill (q, sum) of the calling lane (any exec mask).
+    auto spill_item = [&](uint64_t q, uint32_t sum) {
+        const uint32_t at = atomicAdd(&wspill[wave], 1u);
+        if (at < spill_cap) region[at] = make_uint2((uint32_t)(q - q_wg), sum);
+        else emit(q);  // region full: an unprobed candidate
+    };
     const uint32_t lo = threadIdx.x * P;
     const uint32_t sh = B & 3u;
     uint32_t D1 = 0, DM = 0;
@@ -993,9 +1008,8 @@ __global__ __launch_bounds__(kRollThreads) void roll_lane_kernel(
     };
     if (t_begin < t_end) fetch_plain(t_begin, O, A);
     const u16x2 negB = as_u16x2(((0x10000u - (B & 0xffffu)) & 0xffffu) * 0x10001u);
-    // the previous tile's hit mask (its entries are still in the lane's slots)
-    uint32_t pmall = 0;
-    uint64_t pq = 0;  // q0 + lo of the previous tile
+    uint32_t pmall = 0;  // the previous tile's hit mask (its entries are still in the lane's slots)
+    uint64_t pq = 0;     // q0 + lo of the previous tile
     for (uint32_t t = t_begin; t < t_end; t++) {
         const uint64_t q0 = (uint64_t)t * kScanTile;
         const uint64_t qt = q0 + lo;
@@ -1005,20 +1019,27 @@ __global__ __launch_bounds__(kRollThreads) void roll_lane_kernel(
         const bool next = t + 1 < t_end;
         if (next) fetch_plain(t + 1, On, A);
         // The previous tile's items, before this tile's offset loop reuses the
-        // slots: the first item's bucket loads now (they land during the sums
-        // and the scan below), the rest after the scan, in place.
-        const uint2 pe0 = myslot[0], pe1 = myslot[1], pe2 = myslot[2];
+        // slots: the first item's bucket loads now (compared after the sums
+        // and the scan below), the rest spilled.
         uint32_t pm = pmall;
         uint32_t poff = 0, psum = 0;
         uint64_t pb[2 * kBucketWays];
         const bool pv = pm != 0;
+        const uint2 pe0 = myslot[0], pe1 = myslot[1], pe2 = myslot[2];
+        bool pk = false;  // the prefetched item is in a slot
         if (pv) {
-            item(pm, pmall, pe0, pe1, pe2, poff, psum);
+            pk = item(pm, pmall, pe0, pe1, pe2, poff, psum);
             pm &= pm - 1u;
             const uint64_t *b1 = table + (uint64_t)(bucket_hash1(psum) & bmask) * kBucketWays;
             const uint64_t *b2 = table + (uint64_t)(bucket_hash2(psum) & bmask) * kBucketWays;
 #pragma unroll
             for (uint32_t i = 0; i < kBucketWays; i++) { pb[i] = b1[i]; pb[kBucketWays + i] = b2[i]; }
+        }
+        while (!DIAG && pm != 0) {
+            uint32_t off, sum;
+            const bool in_slot = item(pm, pmall, pe0, pe1, pe2, off, sum);
+            pm &= pm - 1u;
+            if (in_slot) spill_item(pq + off, sum);
         }
         int32_t o1, o2, s1, s2, v1, v2;
         vec_sums(O, o1, o2);
@@ -1053,18 +1074,12 @@ __global__ __launch_bounds__(kRollThreads) void roll_lane_kernel(
             DM = __builtin_amdgcn_readfirstlane(c.y);
         }
         parity ^= 1u;
-        if (pv) {
+        if (pk) {
             uint32_t fl = 0;
 #pragma unroll
             for (uint32_t i = 0; i < 2 * kBucketWays; i++)
                 if ((uint32_t)(pb[i] >> 32) == psum && (uint32_t)pb[i] != 0) fl |= (uint32_t)pb[i];
             if (fl & 2u) emit(pq + poff);
-        }
-        while (!DIAG && pm != 0) {
-            uint32_t off, sum;
-            item(pm, pmall, pe0, pe1, pe2, off, sum);
-            pm &= pm - 1u;
-            if (table_flags(table, bmask, sum) & 2u) emit(pq + off);
         }
         const uint32_t W1 = D1 + exA;
         const uint32_t W2 = (uint32_t)(qt + B) * W1 - (DM + exB);
@@ -1092,7 +1107,8 @@ __global__ __launch_bounds__(kRollThreads) void roll_lane_kernel(
                     const int j = g0 + jj;
                     p1[jj] = P1;
                     p2[jj] = P2;
-                    wd[jj] = u16x2{filt[P1.x], filt[P1.y]};
+                    const u16x2 X = P1 ^ P2;  // the word index of both windows
+                    wd[jj] = u16x2{filt[X.x], filt[X.y]};
                     const u16x2 uo = pair_bytes(Ox[j >> 2], Ox[(j >> 2) + OW / 2], j & 3);
                     const u16x2 ui = pair_bytes(Sx[j >> 2], Sx[(j >> 2) + OW / 2], j & 3);
                     P1 = P1 + ui - uo;
@@ -1111,35 +1127,23 @@ __global__ __launch_bounds__(kRollThreads) void roll_lane_kernel(
         };
         uint32_t m = 0, c = 0;
         const uint2 fin = steps(std::integral_constant<int, 4>{}, [&](int j, uint32_t r1, uint32_t r2, uint32_t z) {
-            // a hit takes the lane's next slot (an exec-masked store: a lane
-            // with all its slots taken never writes past them on a miss)
-            if (z != 0) myslot[c] = make_uint2(r1, r2);
+            // a hit takes the lane's next slot (an exec-masked store); with
+            // the slots taken, its items are spilled right here
+            if (z != 0) {
+                if (c < kLaneSlots) {
+                    myslot[c] = make_uint2(r1, r2);
+                } else if (!DIAG) {
+                    if (z & 1u) spill_item(qt + (uint32_t)j, unraw(__builtin_amdgcn_perm(r2, r1, 0x05040100u)));
+                    if (z >> 16) spill_item(qt + (uint32_t)(H + j), unraw(__builtin_amdgcn_perm(r2, r1, 0x07060302u)));
+                }
+            }
             m |= z << j;
             c += z != 0 ? 1u : 0u;
         });
-        if (!DIAG && __ballot(c > kLaneSlots)) {
-            // Some lane of this wave parked more than its slots hold: roll the
-            // tile again, probing every hit in place (the slots are dropped).
-            // (one pair step per group: its probes are not hoisted together)
-            (void)steps(std::integral_constant<int, 1>{}, [&](int j, uint32_t r1, uint32_t r2, uint32_t z) {
-                if (__ballot(z != 0)) {
-                    if (z & 1u) {
-                        if (table_flags(table, bmask, unraw(__builtin_amdgcn_perm(r2, r1, 0x05040100u))) & 2u)
-                            emit(qt + (uint32_t)j);
-                    }
-                    if (z >> 16) {
-                        if (table_flags(table, bmask, unraw(__builtin_amdgcn_perm(r2, r1, 0x07060302u))) & 2u)
-                            emit(qt + (uint32_t)(H + j));
-                    }
-                }
-            });
-            m = 0;
-        }
         if (threadIdx.x == kRollThreads - 1) {
             const uint32_t w1 = ((fin.x >> 16) - C128) & 0xffffu, w2 = fin.y >> 16;
             carry[parity] = make_uint2(w1, (uint32_t)(q0 + kScanTile + B) * w1 - w2);
         }
-        // this tile's entries become the next tile's items
         pmall = m;
         pq = qt;
         if (next) {
@@ -1147,12 +1151,36 @@ __global__ __launch_bounds__(kRollThreads) void roll_lane_kernel(
             for (int k = 0; k < OW; k++) O[k] = On[k];
         }
     }
-    const uint2 pe0 = myslot[0], pe1 = myslot[1], pe2 = myslot[2];
-    for (uint32_t pm = pmall; pm != 0;) {  // the last tile's items
-        uint32_t off, sum;
-        item(pm, pmall, pe0, pe1, pe2, off, sum);
-        pm &= pm - 1u;
-        if (table_flags(table, bmask, sum) & 2u) emit(pq + off);
+    if (!DIAG) {  // the last tile's items
+        const uint2 pe0 = myslot[0], pe1 = myslot[1], pe2 = myslot[2];
+        for (uint32_t pm = pmall; pm != 0;) {
+            uint32_t off, sum;
+            const bool in_slot = item(pm, pmall, pe0, pe1, pe2, off, sum);
+            pm &= pm - 1u;
+            if (in_slot) spill_item(pq + off, sum);
+        }
+    }
+    __syncthreads();  // every wave's spills counted
+    if (lane == 0) spill_n[blockIdx.x * kWaves + wave] = min(wspill[wave], spill_cap);
+}
+
+// Exact probes of roll_lane_kernel's spilled items: one workgroup per roll
+// wave region (same grid arithmetic as the roll).
+__global__ __launch_bounds__(64) void roll_spill_probe_kernel(const uint2 *__restrict__ spill, uint32_t spill_cap,
+                                                              const uint32_t *__restrict__ spill_n, uint32_t tile_lo,
+                                                              uint32_t per, const uint64_t *__restrict__ table,
+                                                              uint32_t bmask, uint64_t *__restrict__ cand,
+                                                              uint32_t cap, uint32_t *__restrict__ count) {
+    const uint32_t wid = blockIdx.x;
+    const uint32_t n = spill_n[wid];
+    const uint64_t q_wg = (uint64_t)(tile_lo + (wid / (kRollThreads / 64)) * per) * kScanTile;
+    const uint2 *region = spill + (uint64_t)wid * spill_cap;
+    for (uint32_t i = threadIdx.x; i < n; i += 64) {
+        const uint2 e = region[i];
+        if (table_flags(table, bmask, e.y) & 2u) {
+            const uint32_t at = atomicAdd(count, 1u);
+            if (at < cap) cand[at] = q_wg + e.x;
+        }
     }
 }
 
@@ -1238,7 +1266,7 @@ int roll_packed() {
     // (default) = the packed roll with ballot parking, 2 = with lane slots
     static const int v = [] {
         const char *e = getenv("RSG_ROLL_PACKED");
-        return e ? std::max(0, std::min(3, atoi(e))) : 1;  // 3: lane slots without slow paths (timing only)
+        return e ? std::max(0, std::min(3, atoi(e))) : 1;  // 3: lane slots without spills (timing only)
     }();
     return v;
 }
@@ -1254,8 +1282,8 @@ bool roll_filter_sel() {
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
                        const uint32_t *bitmap, const uint16_t *filter16, const uint64_t *table, uint32_t bmask,
-                       uint64_t *cand, uint32_t cap, uint32_t *count, uint32_t grid, bool fused,
-                       hipStream_t stream) {
+                       uint64_t *cand, uint32_t cap, uint32_t *count, uint32_t grid, bool fused, uint2 *spill,
+                       uint32_t *spill_n, hipStream_t stream) {
     if (tile_hi <= tile_lo) return hipSuccess;
     if (fused && filter16) {
         // Interior tiles [tile_lo, t_int) take the packed kernel: every offset
@@ -1266,10 +1294,17 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
         const uint32_t t_int = (uint32_t)std::max<uint64_t>(tile_lo, std::min<uint64_t>(tile_hi, lim / kScanTile));
         if (t_int > tile_lo) {
             const uint32_t g = min(grid, t_int - tile_lo);
-            auto kern = roll_packed() == 1 ? roll_packed_kernel
-                        : roll_packed() == 3 ? roll_lane_kernel<true> : roll_lane_kernel<false>;
-            hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, tile_lo, t_int, filter16,
-                               table, bmask, cand, cap, count);
+            if (roll_packed() == 1 || !spill) {
+                hipLaunchKernelGGL(roll_packed_kernel, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, tile_lo,
+                                   t_int, filter16, table, bmask, cand, cap, count);
+            } else {
+                auto kern = roll_packed() == 3 ? roll_lane_kernel<true> : roll_lane_kernel<false>;
+                hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, tile_lo, t_int,
+                                   filter16, table, bmask, cand, cap, count, spill, kRollSpillCap, spill_n);
+                const uint32_t per = (t_int - tile_lo + g - 1) / g;
+                hipLaunchKernelGGL(roll_spill_probe_kernel, dim3(g * (kRollThreads / 64)), dim3(64), 0, stream, spill,
+                                   kRollSpillCap, spill_n, tile_lo, per, table, bmask, cand, cap, count);
+            }
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
