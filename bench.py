@@ -63,8 +63,20 @@ def parse():
     return ap.parse_args()
 
 
+def keep_stdout_for_the_line():
+    """The bench line is the only thing on stdout: native libraries that print
+    there (RCCL's version banner at communicator init) write to stderr
+    instead.  fd 1 becomes a copy of fd 2; Python's sys.stdout keeps the
+    original stdout."""
+    sys.stdout.flush()
+    real = os.dup(1)
+    os.dup2(2, 1)
+    sys.stdout = os.fdopen(real, "w", buffering=1)
+
+
 def main():
     args = parse()
+    keep_stdout_for_the_line()
     import torch
     import torch.distributed as dist
 
