@@ -264,6 +264,39 @@ def test_file_sums_past_4gib(eng, unaligned):
             assert got[i].tobytes() == want, (i, off, n, mode)
 
 
+def test_sender_search_past_4gib(eng):
+    """The sender's rolling match (match.go:93-210) over a 5 GiB source: the
+    reference's offsets are int64, so the packed roll's tiles past 2^32
+    bytes, its carried start windows and the hand-off to roll_kernel's edge
+    tiles must give the reference's walk.  The source is the basis with
+    blocks overwritten on both sides of 4 GiB and at the remainder block:
+    every other block matches at its own offset, in order (a modified block
+    leaves the walk stepping byte by byte to the next block boundary)."""
+    B = 131072
+    size = 5 * GIB + 12345
+    basis = eng.alloc(size)
+    src = eng.alloc(size)
+    try:
+        eng.fill_splitmix64(basis, size, 77)
+        eng.fill_splitmix64(src, size, 77)
+        recs, total = eng.block_sums_device(basis, [(0, size, B)], cases.SEED)
+        s1, s2 = orc.parse_records(recs.download(total * 20).tobytes())
+        recs.free()
+        head = orc.sum_head(size, B)
+        assert head[0] == total == size // B + 1 and head[3] == 12345
+        four = 4 * GIB // B
+        bad = {four - 1, four, four + 1, total - 1}
+        bad |= {int(x) for x in np.random.default_rng(5).integers(0, total - 1, 12)}
+        for b in sorted(bad):
+            eng.fill_splitmix64(src, 64, 1000 + b, offset=b * B + 100)
+        eng.synchronize()
+        got = eng.hash_search_device(src, size, head, s1, s2, orc.stable_targets(s1), cases.SEED)
+        assert got == [(i * B, i) for i in range(total) if i not in bad]
+    finally:
+        src.free()
+        basis.free()
+
+
 def test_release_arenas(eng):
     """Frees the module's 5 GiB arenas (runs last in this file)."""
     for a, _, _ in _ARENAS.values():
