@@ -6,6 +6,7 @@
 
 #include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/rsg.h"
@@ -25,7 +26,20 @@ struct PinBuf {
 
 // Sender scratch of one search in flight; a batch rotates three of them so
 // later files' tables and kernels overlap file i's walk (rsg_match.cpp).
+// Host temporaries of a search's table build (rsg_match.cpp tables()), owned
+// by the slot and reused job after job: the ~2.5 MB they span stays faulted
+// in (fresh vectors per job page-faulted on the first roll's critical path).
+struct TableScratch {
+    std::vector<std::pair<uint32_t, int32_t>> pairs, groups;  // (sum1, block), then grouped by sum1
+    std::vector<uint32_t> cnt, hi16, bitmap;
+    std::vector<std::pair<uint32_t, uint32_t>> keys;  // distinct sum1 -> flags
+    std::vector<uint16_t> filter16;
+    std::vector<uint64_t> table;
+    std::vector<uint8_t> fill;
+};
+
 struct SearchSlot {
+    TableScratch hs;                   // host scratch of the table build
     DevBuf agg, prefix, counts, list;  // tile sums, tile prefixes, candidate count and list
     DevBuf spill, spill_n;             // packed roll's spilled filter hits (per wave) and their counts
     DevBuf blob;                       // basis tables, one upload: groups | hi16 | sum2 | filter | table

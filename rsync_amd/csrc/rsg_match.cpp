@@ -92,10 +92,6 @@ struct Search {
     rsg_sum_head head;
     int32_t seed;
     int64_t end;  // visited offsets are q < end (end >= 1: offset 0 is always visited)
-    // (sum1, block) in targets order, stably sorted by sum1: each sum's blocks
-    // are one run, in targets order (match.go:108 walks targets in that order)
-    std::vector<std::pair<uint32_t, int32_t>> groups;
-    std::vector<uint32_t> hi16;  // groups index of the first sum with a given high half (65537 entries)
     std::vector<rsg_match> out;
     hipStream_t side = nullptr;  // prefix pass (beside the previous file's roll)
     hipStream_t copy = nullptr;  // candidate read-back
@@ -369,6 +365,7 @@ rsg_status confirm_all_tail(Search &S, const std::vector<uint64_t> &key, uint64_
 rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets) {
     rsg_ctx *ctx = S.ctx;
     SearchSlot &sl = *S.sl;
+    TableScratch &T = sl.hs;
     const int64_t B = S.head.block_len;
     const int32_t count = S.head.count;
     const int64_t last_len = (S.head.rem != 0) ? S.head.rem : B;
@@ -376,35 +373,42 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
     const uint64_t ntiles64 = (S.size + kScanTile - 1) / kScanTile;
     if (ntiles64 >= 0xFFFFFFF0ull) return fail(ctx, RSG_ERR_INVALID, "source too large");
     S.ntiles = (uint32_t)ntiles64;
+    // (sum1, block) in targets order, stably sorted by sum1: each sum's blocks
+    // are one run, in targets order (match.go:108 walks targets in that
+    // order); hi16[h] = index of the first sum with high half h.
+    auto &groups = T.groups;
+    auto &hi16 = T.hi16;
     {
-        // Stable LSD radix sort (two 16-bit passes) of the targets-ordered
-        // (sum1, block) list: equal sums keep their targets order.
-        std::vector<std::pair<uint32_t, int32_t>> tmp((size_t)count);
-        S.groups.resize((size_t)count);
+        // Stable LSD radix sort (two 16-bit passes) of the targets-ordered list.
+        auto &tmp = T.pairs;
+        tmp.resize((size_t)count);
+        groups.resize((size_t)count);
         for (int32_t k = 0; k < count; k++) tmp[(size_t)k] = {sum1[targets[k]], targets[k]};
-        std::vector<uint32_t> cnt(65537);
+        T.cnt.resize(65537);
         for (int pass = 0; pass < 2; pass++) {
-            auto &from = pass == 0 ? tmp : S.groups;
-            auto &to = pass == 0 ? S.groups : tmp;
+            auto &from = pass == 0 ? tmp : groups;
+            auto &to = pass == 0 ? groups : tmp;
             const int shift = 16 * pass;
-            std::fill(cnt.begin(), cnt.end(), 0u);
-            for (auto &e : from) cnt[((e.first >> shift) & 0xffffu) + 1]++;
-            for (size_t h = 1; h < cnt.size(); h++) cnt[h] += cnt[h - 1];
-            for (auto &e : from) to[cnt[(e.first >> shift) & 0xffffu]++] = e;
+            std::fill(T.cnt.begin(), T.cnt.end(), 0u);
+            for (auto &e : from) T.cnt[((e.first >> shift) & 0xffffu) + 1]++;
+            for (size_t h = 1; h < T.cnt.size(); h++) T.cnt[h] += T.cnt[h - 1];
+            for (auto &e : from) to[T.cnt[(e.first >> shift) & 0xffffu]++] = e;
         }
-        S.groups.swap(tmp);
-        S.hi16.assign(65537, 0);
-        for (auto &e : S.groups) S.hi16[(e.first >> 16) + 1]++;
-        for (size_t h = 1; h < S.hi16.size(); h++) S.hi16[h] += S.hi16[h - 1];
+        groups.swap(tmp);
+        hi16.assign(65537, 0);
+        for (auto &e : groups) hi16[(e.first >> 16) + 1]++;
+        for (size_t h = 1; h < hi16.size(); h++) hi16[h] += hi16[h - 1];
     }
     S.pt.mark("groups");
-    std::vector<std::pair<uint32_t, uint32_t>> keys;  // distinct sum1 -> flags
-    for (size_t i = 0; i < S.groups.size(); i++) {
-        const uint32_t f = 1u | ((S.len_of(S.groups[i].second) == B) ? 2u : 4u);
-        if (!keys.empty() && keys.back().first == S.groups[i].first) keys.back().second |= f;
-        else keys.push_back({S.groups[i].first, f});
+    auto &keys = T.keys;
+    keys.clear();
+    for (size_t i = 0; i < groups.size(); i++) {
+        const uint32_t f = 1u | ((S.len_of(groups[i].second) == B) ? 2u : 4u);
+        if (!keys.empty() && keys.back().first == groups[i].first) keys.back().second |= f;
+        else keys.push_back({groups[i].first, f});
     }
-    std::vector<uint32_t> bitmap(rsg::kFilterBits / 32, 0);
+    auto &bitmap = T.bitmap;
+    bitmap.assign(rsg::kFilterBits / 32, 0);
     const bool sel = rsg::roll_filter_sel();
     for (auto &kv : keys) {
         if (sel) {
@@ -415,15 +419,16 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
         }
     }
     // the packed roll's filter (interior tiles of the fused mode)
-    std::vector<uint16_t> filter16;
+    auto &filter16 = T.filter16;
+    filter16.clear();
     if ((uint32_t)B <= rsg::kFusedMaxB && rsg::roll_packed()) {
         filter16.assign(rsg::kFilter16Words, 0);
         for (auto &kv : keys) filter16[rsg::f16_word(kv.first, (uint32_t)B)] |= (uint16_t)rsg::f16_mask(kv.first);
     }
     uint32_t nb = 16;
     while (nb < keys.size() / 2) nb <<= 1;
-    std::vector<uint64_t> table;
-    std::vector<uint8_t> fill;
+    auto &table = T.table;
+    auto &fill = T.fill;
     for (;;) {
         table.assign((size_t)nb * rsg::kBucketWays, 0);
         fill.assign(nb, 0);
@@ -439,9 +444,9 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
     }
     S.bmask = nb - 1;
     // blob layout, 256-byte aligned parts
-    static_assert(sizeof(S.groups[0]) == 8, "(sum1, block) pair must be 8 bytes");
+    static_assert(sizeof(groups[0]) == 8, "(sum1, block) pair must be 8 bytes");
     auto up = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
-    const uint64_t n_groups = S.groups.size() * 8, n_hi16 = S.hi16.size() * 4, n_sum2 = (uint64_t)count * 16;
+    const uint64_t n_groups = groups.size() * 8, n_hi16 = hi16.size() * 4, n_sum2 = (uint64_t)count * 16;
     const uint64_t n_filter = bitmap.size() * 4, n_table = table.size() * 8, n_filter16 = filter16.size() * 2;
     S.off_hi16 = up(n_groups);
     S.off_sum2 = S.off_hi16 + up(n_hi16);
@@ -452,8 +457,8 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
     rsg_status s;
     if ((s = ensure_pin(ctx, sl.stage, S.blob_bytes)) != RSG_OK) return s;
     uint8_t *st = (uint8_t *)sl.stage.p;
-    if (n_groups) memcpy(st, S.groups.data(), n_groups);
-    memcpy(st + S.off_hi16, S.hi16.data(), n_hi16);
+    if (n_groups) memcpy(st, groups.data(), n_groups);
+    memcpy(st + S.off_hi16, hi16.data(), n_hi16);
     if (n_sum2) memcpy(st + S.off_sum2, sum2, n_sum2);
     memcpy(st + S.off_filter, bitmap.data(), n_filter);
     if (n_filter16) memcpy(st + S.off_filter16, filter16.data(), n_filter16);
