@@ -101,17 +101,19 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
 constexpr uint32_t kRollSpillCap = 1024;
 inline uint64_t roll_spill_bytes(uint32_t grid) { return (uint64_t)grid * (kRollThreads / 64) * kRollSpillCap * 8; }
 // The packed roll's filter (roll_packed_kernel, fused mode, interior tiles):
-// 2^16 16-bit words, word ((s1 + 128 B) xor s2) mod 2^16, bits s2[0..3] and
-// s2[4..7].  s1 of a long window of random bytes is a sum of B terms (near-
-// Gaussian mod 2^16): a word indexed by s1 alone passed 1.9 % of real window
-// sums, the xor with s2 ~1.0 %.
+// 2^16 16-bit words, word ((s1 + 128 B) xor s2) mod 2^16, bits s2[0..3],
+// s2[4..7] and (by default) s2[8..11].  s1 of a long window of random bytes is
+// a sum of B terms (near-Gaussian mod 2^16): a word indexed by s1 alone passed
+// 1.9 % of real window sums with two bits, the xor with s2 ~1.0 %.
 constexpr uint32_t kFilter16Words = 1u << 16;
 __host__ __device__ inline uint32_t f16_word(uint32_t sum, uint32_t B) {
     return ((sum + 128u * B) ^ (sum >> 16)) & 0xffffu;
 }
-__host__ __device__ inline uint32_t f16_mask(uint32_t sum) {
-    return (1u << ((sum >> 16) & 15u)) | (1u << ((sum >> 20) & 15u));
+__host__ __device__ inline uint32_t f16_mask(uint32_t sum, int nbits = 2) {
+    const uint32_t m = (1u << ((sum >> 16) & 15u)) | (1u << ((sum >> 20) & 15u));
+    return nbits == 3 ? m | (1u << ((sum >> 24) & 15u)) : m;
 }
+int roll_filter_bits();  // RSG_ROLL_BITS (read once): bits per sum in the packed roll's filter, 2 or 3
 int roll_packed();  // RSG_ROLL_PACKED (read once): 0 roll_kernel only, 1 packed + ballots, 2 packed + lane slots
 // Block lengths up to which roll derives its window sums itself (no tile_agg
 // / tile_scan passes): each workgroup reads B extra bytes once.

@@ -423,7 +423,9 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
     filter16.clear();
     if ((uint32_t)B <= rsg::kFusedMaxB && rsg::roll_packed()) {
         filter16.assign(rsg::kFilter16Words, 0);
-        for (auto &kv : keys) filter16[rsg::f16_word(kv.first, (uint32_t)B)] |= (uint16_t)rsg::f16_mask(kv.first);
+        const int nbits = rsg::roll_filter_bits();
+        for (auto &kv : keys)
+            filter16[rsg::f16_word(kv.first, (uint32_t)B)] |= (uint16_t)rsg::f16_mask(kv.first, nbits);
     }
     uint32_t nb = 16;
     while (nb < keys.size() / 2) nb <<= 1;

@@ -610,9 +610,10 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
 //   W1 += x_in - x_out;  W2 += W1 - B x_out, the 128B in P1 absorbs the -128s)
 // one v_perm per operand pair and four v_pk_* per two offsets.  The filter is
 // 2^16 16-bit words indexed by P1 ^ P2 (word ((W1 + 128B) ^ W2) mod 2^16, the
-// host builds it shifted; one v_xor for both windows), bits W2[0..3] and
-// W2[4..7]: a 16-bit shift of both halves at once (v_pk_lshrrev_b16) per bit.
-// About 1 % of non-matching window sums pass with 32768 basis sums.
+// host builds it shifted; one v_xor for both windows), bits W2[0..3],
+// W2[4..7] and W2[8..11]: a 16-bit shift of both halves at once
+// (v_pk_lshrrev_b16) per bit.  About 0.6 % of non-matching window sums pass
+// with 32768 basis sums (1.0 % with the first two bits only).
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
@@ -633,6 +634,7 @@ __device__ __forceinline__ u16x2 pair_bytes(uint32_t wa, uint32_t wb, int p) {
     return as_u16x2(__builtin_amdgcn_perm(wb, wa, sel));
 }
 
+template <int NBITS>  // filter bits per sum: S2[0..3], S2[4..7] (and S2[8..11])
 __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t tile_lo, uint32_t tile_hi,
     const uint16_t *__restrict__ filter_g, const uint64_t *__restrict__ table, uint32_t bmask,
@@ -844,7 +846,9 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 const int j = g0 + jj;
                 const u16x2 x = pk_shr(wd[jj], p2[jj]);
                 const u16x2 y = pk_shr(wd[jj], p2[jj] >> (uint16_t)4);
-                uint32_t z = as_u32(x & y) & 0x00010001u;
+                u16x2 xy = x & y;
+                if constexpr (NBITS == 3) xy &= pk_shr(wd[jj], p2[jj] >> (uint16_t)8);
+                uint32_t z = as_u32(xy) & 0x00010001u;
                 asm("" : "+v"(z));
                 const uint32_t r1 = as_u32(p1[jj]), r2 = as_u32(p2[jj]);
                 park((z & 0xffffu) != 0, (uint32_t)j, __builtin_amdgcn_perm(r2, r1, 0x05040100u));
@@ -1271,6 +1275,17 @@ int roll_packed() {
     return v;
 }
 
+int roll_filter_bits() {
+    static const int v = [] {
+        // A/B switch: 2 = bits S2[0..3], S2[4..7] only; default 3 adds S2[8..11]
+        // (0.6 % instead of 1.0 % false hits: fewer parks for 2-3 more VALU
+        // per two offsets; roll 0.83-0.85 vs 0.86-0.87 ms per GiB)
+        const char *e = getenv("RSG_ROLL_BITS");
+        return (e && e[0] == '2') ? 2 : 3;
+    }();
+    return v;
+}
+
 bool roll_filter_sel() {
     static const bool sel = [] {
         const char *e = getenv("RSG_FILTER_SEL");  // A/B switch: 0 = the rotate-xor hash layout
@@ -1295,8 +1310,9 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
         if (t_int > tile_lo) {
             const uint32_t g = min(grid, t_int - tile_lo);
             if (roll_packed() == 1 || !spill) {
-                hipLaunchKernelGGL(roll_packed_kernel, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, tile_lo,
-                                   t_int, filter16, table, bmask, cand, cap, count);
+                auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3> : roll_packed_kernel<2>;
+                hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, tile_lo, t_int,
+                                   filter16, table, bmask, cand, cap, count);
             } else {
                 auto kern = roll_packed() == 3 ? roll_lane_kernel<true> : roll_lane_kernel<false>;
                 hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, tile_lo, t_int,
