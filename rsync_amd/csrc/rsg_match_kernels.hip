@@ -634,11 +634,14 @@ __device__ __forceinline__ u16x2 pair_bytes(uint32_t wa, uint32_t wb, int p) {
     return as_u16x2(__builtin_amdgcn_perm(wb, wa, sel));
 }
 
-template <int NBITS>  // filter bits per sum: S2[0..3], S2[4..7] (and S2[8..11])
+// NBITS: filter bits per sum, S2[0..3], S2[4..7] (and S2[8..11]); EDGE: the
+// kernel rolls the range's edge tiles itself (else the host leaves them to
+// roll_kernel and passes t_int = tile_hi).
+template <int NBITS, bool EDGE>
 __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
-    const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t tile_lo, uint32_t tile_hi,
-    const uint16_t *__restrict__ filter_g, const uint64_t *__restrict__ table, uint32_t bmask,
-    uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count) {
+    const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
+    uint32_t t_int, uint32_t tile_hi, const uint16_t *__restrict__ filter_g, const uint64_t *__restrict__ table,
+    uint32_t bmask, uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count) {
     constexpr uint32_t kWaves = kRollThreads / 64;
     constexpr uint32_t P = kRollPerThread;  // offsets per lane (2 streams of P/2)
     constexpr int OW = (int)P / 4;
@@ -660,10 +663,14 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     const uint32_t C128 = (128u * B) & 0xffffu;  // the filter index offset of P1
     uint32_t parity = 0;
 
-    // Exact probes of a wave's parked hits, as roll_kernel (every window here
-    // has length B: a block of length B must carry the sum).
+    // Exact probes of a wave's parked hits, as roll_kernel: the window at q
+    // has length k = min(B, size - q), a block of that length must carry the
+    // sum (interior windows: k = B).
+    const uint32_t rem_flag = (rem != 0 && rem != B) ? 4u : 2u;
     auto probe = [&](uint64_t q, uint32_t fl) {
-        if (fl & 2u) {
+        const uint32_t k = (uint32_t)min<uint64_t>((uint64_t)B, size - q);
+        const uint32_t need = (k == B) ? 2u : ((k == rem) ? rem_flag : 0u);
+        if (fl & need) {
             const uint32_t at = atomicAdd(count, 1u);
             if (at < cap) cand[at] = q;
         }
@@ -732,15 +739,23 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
             a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
         }
     };
-    if (t_begin < t_end) fetch_plain(t_begin, O, A);
     const u16x2 negB = as_u16x2(((0x10000u - (B & 0xffffu)) & 0xffffu) * 0x10001u);
+    bool have = false;  // O, A already hold tile t's bytes (prefetched)
     for (uint32_t t = t_begin; t < t_end; t++) {
         const uint64_t q0 = (uint64_t)t * kScanTile;
+        if (q0 >= end) break;  // uniform
         const uint64_t qt = q0 + lo;
+        if (!have) {  // the run's first tile, or an edge tile: guarded loads
+#pragma unroll
+            for (int q = 0; q < NV; q++) load_vec(src, size, qt + 16 * q, O + 4 * q);
+#pragma unroll
+            for (int q = 0; q < NV + 1; q++) load_vec(src, size, qt + B - sh + 16 * q, A + 4 * q);
+        }
+        const bool edge = EDGE && t >= t_int;  // windows shorter than B or offsets past end: the scalar path
         uint32_t S[OW];
 #pragma unroll
         for (int k = 0; k < OW; k++) S[k] = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sh);
-        const bool next = t + 1 < t_end;
+        const bool next = t + 1 < t_end && t + 1 < t_int;
         if (next) fetch_plain(t + 1, On, A);
         uint2 pe = make_uint2(0, 0);
         uint64_t pb[2 * kBucketWays];
@@ -790,21 +805,6 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
             DM = __builtin_amdgcn_readfirstlane(c.y);
         }
         parity ^= 1u;
-        // window at the lane's first offset, then at its 17th (16 rolling
-        // steps in closed form: W1 + sum d, W2 + 16 W1 + sum (16 - j) d_j - B sum x_out)
-        const uint32_t W1 = D1 + exA;
-        const uint32_t W2 = (uint32_t)(qt + B) * W1 - (DM + exB);
-        const uint32_t da = (uint32_t)(s1a - o1a);
-        const uint32_t W1b = W1 + da;
-        const uint32_t W2b = W2 + 16u * W1 + 16u * da - (uint32_t)(s2a - o2a) - B * (uint32_t)o1a;
-        u16x2 P1 = as_u16x2(((W1 + C128) & 0xffffu) | ((W1b + C128) << 16));
-        u16x2 P2 = as_u16x2((W2 & 0xffffu) | (W2b << 16));
-        uint32_t Ox[OW], Sx[OW];
-#pragma unroll
-        for (int k = 0; k < OW; k++) {
-            Ox[k] = O[k] ^ 0x80808080u;
-            Sx[k] = S[k] ^ 0x80808080u;
-        }
         uint32_t lol = lo;
         asm volatile("" : "+v"(lol));
         uint32_t nq = 0;
@@ -825,6 +825,62 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 }
             }
         };
+        if constexpr (!EDGE) {
+        } else if (edge) {
+            // The source's last tiles (roll_kernel's edge path, with this
+            // kernel's filter): 32-bit offsets relative to q0, the window at
+            // qt of length k = min(B, size - qt), bytes past the end read 0.
+            uint32_t W1 = D1 + exA;
+            const uint32_t M = DM + exB;
+            uint32_t k = qt + B <= size ? B : (qt < size ? (uint32_t)(size - qt) : 0u);
+            uint32_t W2 = (uint32_t)(qt + k) * W1 - M;
+            const uint32_t end_rel = (uint32_t)min<uint64_t>(end - q0, 0xFFFFFFFFull);
+            const uint32_t size_rel = (uint32_t)min<uint64_t>(size > q0 ? size - q0 : 0, 0xFFFFFFFFull);
+            constexpr int GE = 8;
+#pragma unroll
+            for (int g0 = 0; g0 < (int)P; g0 += GE) {
+                uint32_t raw[GE], word[GE];
+#pragma unroll
+                for (int jj = 0; jj < GE; jj++) {
+                    const int j = g0 + jj;
+                    const uint32_t qr = lol + j;
+                    raw[jj] = ((W1 + C128) & 0xffffu) | (W2 << 16);           // unraw() gives the sum
+                    word[jj] = filt[((W1 + C128) ^ W2) & 0xffffu];           // f16_word
+                    const int32_t xo = sx8(O[j >> 2], j & 3);                // match.go:171-196
+                    const bool more = qr + k < size_rel;
+                    const int32_t xi = more ? sx8(S[j >> 2], j & 3) : 0;
+                    W1 = W1 - (uint32_t)xo + (uint32_t)xi;
+                    W2 = W2 - k * (uint32_t)xo + (more ? W1 : 0u);
+                    if (!more) k--;
+                }
+#pragma unroll
+                for (int jj = 0; jj < GE; jj++) {
+                    const uint32_t s2 = raw[jj] >> 16;
+                    uint32_t bits = (word[jj] >> (s2 & 15u)) & (word[jj] >> ((s2 >> 4) & 15u));
+                    if constexpr (NBITS == 3) bits &= word[jj] >> ((s2 >> 8) & 15u);
+                    park((bits & 1u) && (lol + g0 + jj < end_rel), (uint32_t)(g0 + jj), raw[jj]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (threadIdx.x == kRollThreads - 1)
+                carry[parity] = make_uint2(W1, (uint32_t)(q0 + kScanTile + k) * W1 - W2);
+        }
+        if (!edge) {
+        // window at the lane's first offset, then at its 17th (16 rolling
+        // steps in closed form: W1 + sum d, W2 + 16 W1 + sum (16 - j) d_j - B sum x_out)
+        const uint32_t W1 = D1 + exA;
+        const uint32_t W2 = (uint32_t)(qt + B) * W1 - (DM + exB);
+        const uint32_t da = (uint32_t)(s1a - o1a);
+        const uint32_t W1b = W1 + da;
+        const uint32_t W2b = W2 + 16u * W1 + 16u * da - (uint32_t)(s2a - o2a) - B * (uint32_t)o1a;
+        u16x2 P1 = as_u16x2(((W1 + C128) & 0xffffu) | ((W1b + C128) << 16));
+        u16x2 P2 = as_u16x2((W2 & 0xffffu) | (W2b << 16));
+        uint32_t Ox[OW], Sx[OW];
+#pragma unroll
+        for (int k = 0; k < OW; k++) {
+            Ox[k] = O[k] ^ 0x80808080u;
+            Sx[k] = S[k] ^ 0x80808080u;
+        }
         constexpr int G = 4;  // pair steps per group: 8 filter reads in flight
 #pragma unroll
         for (int g0 = 0; g0 < H; g0 += G) {
@@ -861,6 +917,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
             const uint32_t w1 = ((as_u32(P1) >> 16) - C128) & 0xffffu, w2 = as_u32(P2) >> 16;
             carry[parity] = make_uint2(w1, (uint32_t)(q0 + kScanTile + B) * w1 - w2);
         }
+        }  // interior tile
         if (pv) {
             uint32_t fl = 0;
 #pragma unroll
@@ -876,6 +933,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
 #pragma unroll
             for (int k = 0; k < OW; k++) O[k] = On[k];
         }
+        have = next;
     }
     drain_rest(qh ^ 1, prev_q0, 0, prev_n);
 }
@@ -1275,6 +1333,14 @@ int roll_packed() {
     return v;
 }
 
+static bool roll_edge_inside() {
+    static const bool v = [] {
+        const char *e = getenv("RSG_ROLL_EDGE");  // A/B switch: 0 = edge tiles in a separate roll_kernel launch
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 int roll_filter_bits() {
     static const int v = [] {
         // A/B switch: 2 = bits S2[0..3], S2[4..7] only; default 3 adds S2[8..11]
@@ -1301,18 +1367,27 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                        uint32_t *spill_n, hipStream_t stream) {
     if (tile_hi <= tile_lo) return hipSuccess;
     if (fused && filter16) {
-        // Interior tiles [tile_lo, t_int) take the packed kernel: every offset
-        // of tile t visited ((t+1) T <= end) and its window and shifted-byte
-        // loads inside the source ((t+1) T + B + 48 <= size); the rest (the
-        // source's last B bytes or so) roll_kernel's edge path.
+        // Interior tiles [tile_lo, t_int): every offset of tile t visited
+        // ((t+1) T <= end) and its window and shifted-byte loads inside the
+        // source ((t+1) T + B + 48 <= size).  The packed kernel (default) takes
+        // the whole range and rolls the rest -- the source's last B bytes or
+        // so -- with its scalar edge path; the lane-slot variant leaves them
+        // to roll_kernel.  A range with no interior tile is roll_kernel's.
         const uint64_t lim = std::min<uint64_t>(end, size >= (uint64_t)B + 48 ? size - B - 48 : 0);
         const uint32_t t_int = (uint32_t)std::max<uint64_t>(tile_lo, std::min<uint64_t>(tile_hi, lim / kScanTile));
         if (t_int > tile_lo) {
             const uint32_t g = min(grid, t_int - tile_lo);
-            if (roll_packed() == 1 || !spill) {
-                auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3> : roll_packed_kernel<2>;
-                hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, tile_lo, t_int,
-                                   filter16, table, bmask, cand, cap, count);
+            if ((roll_packed() == 1 || !spill) && roll_edge_inside()) {
+                // the whole range: the packed kernel rolls its edge tiles itself
+                const uint32_t ga = min(grid, tile_hi - tile_lo);
+                auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, true> : roll_packed_kernel<2, true>;
+                hipLaunchKernelGGL(kern, dim3(ga), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
+                                   t_int, tile_hi, filter16, table, bmask, cand, cap, count);
+                return hipGetLastError();
+            } else if (roll_packed() == 1 || !spill) {
+                auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, false> : roll_packed_kernel<2, false>;
+                hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
+                                   t_int, t_int, filter16, table, bmask, cand, cap, count);
             } else {
                 auto kern = roll_packed() == 3 ? roll_lane_kernel<true> : roll_lane_kernel<false>;
                 hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, tile_lo, t_int,
