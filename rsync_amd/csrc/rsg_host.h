@@ -35,6 +35,7 @@ struct TableScratch {
     std::vector<std::pair<uint32_t, uint32_t>> keys;  // distinct sum1 -> flags
     std::vector<uint16_t> filter16;
     std::vector<uint64_t> table;
+    std::vector<uint32_t> table_keys;  // the table's keys only (empty slots: an existing key)
     std::vector<uint8_t> fill;
 };
 

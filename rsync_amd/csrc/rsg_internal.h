@@ -93,9 +93,9 @@ hipError_t launch_resolve(const uint8_t *records, const DevFile *files, uint64_t
                           int32_t s2len, int32_t *res, hipStream_t stream);
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
-                       const uint32_t *bitmap, const uint16_t *filter16, const uint64_t *table, uint32_t bmask,
-                       uint64_t *cand, uint32_t cap, uint32_t *count, uint32_t grid, bool fused, uint2 *spill,
-                       uint32_t *spill_n, hipStream_t stream);
+                       const uint32_t *bitmap, const uint16_t *filter16, const uint64_t *table,
+                       const uint32_t *table_keys, uint32_t bmask, uint64_t *cand, uint32_t cap, uint32_t *count,
+                       uint32_t grid, bool fused, uint2 *spill, uint32_t *spill_n, hipStream_t stream);
 // Spill regions of the lane-slot packed roll: kRollSpillCap (offset, sum)
 // items per roll wave (grid x 16 waves), and one count per wave.
 constexpr uint32_t kRollSpillCap = 1024;

@@ -102,12 +102,13 @@ struct Search {
     std::function<bool()> hook_ready;        // hook() would not wait
     std::function<rsg_status()> tail;        // set by finish(): the rest of the job (wait + walk), any thread
     // device tables inside the slot's blob
-    uint64_t off_hi16 = 0, off_sum2 = 0, off_filter = 0, off_filter16 = 0, off_table = 0, blob_bytes = 0;
+    uint64_t off_hi16 = 0, off_sum2 = 0, off_filter = 0, off_filter16 = 0, off_table = 0, off_keys = 0, blob_bytes = 0;
     const uint2 *d_groups = nullptr;
     const uint32_t *d_hi16 = nullptr, *d_filter = nullptr;
     const uint16_t *d_filter16 = nullptr;  // packed roll (nullptr: not built)
     const uint8_t *d_sum2 = nullptr;
     const uint64_t *d_table = nullptr;
+    const uint32_t *d_table_keys = nullptr;
     uint32_t ntiles = 0, tile_end = 0, bmask = 0, cus = 256;
     uint32_t roll_grid = 0;    // roll workgroups (0 = one per CU)
     uint32_t confirm_lds = 0;  // dynamic LDS of the confirmation kernel's workgroups
@@ -445,6 +446,10 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
         nb <<= 1;
     }
     S.bmask = nb - 1;
+    auto &tkeys = T.table_keys;  // the packed roll's key-only copy
+    tkeys.resize(table.size());
+    for (size_t i = 0; i < table.size(); i++)
+        tkeys[i] = (uint32_t)table[i] != 0 ? (uint32_t)(table[i] >> 32) : (keys.empty() ? 0u : keys[0].first);
     // blob layout, 256-byte aligned parts
     static_assert(sizeof(groups[0]) == 8, "(sum1, block) pair must be 8 bytes");
     auto up = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
@@ -455,7 +460,8 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
     S.off_filter = S.off_sum2 + up(n_sum2);
     S.off_filter16 = S.off_filter + up(n_filter);
     S.off_table = S.off_filter16 + up(n_filter16);
-    S.blob_bytes = S.off_table + up(n_table);
+    S.off_keys = S.off_table + up(n_table);
+    S.blob_bytes = S.off_keys + up(tkeys.size() * 4);
     rsg_status s;
     if ((s = ensure_pin(ctx, sl.stage, S.blob_bytes)) != RSG_OK) return s;
     uint8_t *st = (uint8_t *)sl.stage.p;
@@ -465,6 +471,7 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
     memcpy(st + S.off_filter, bitmap.data(), n_filter);
     if (n_filter16) memcpy(st + S.off_filter16, filter16.data(), n_filter16);
     memcpy(st + S.off_table, table.data(), n_table);
+    memcpy(st + S.off_keys, tkeys.data(), tkeys.size() * 4);
     S.pt.mark("tables");
     return RSG_OK;
 }
@@ -511,6 +518,7 @@ rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
     S.d_filter = (const uint32_t *)(blob + S.off_filter);
     S.d_filter16 = S.off_table > S.off_filter16 ? (const uint16_t *)(blob + S.off_filter16) : nullptr;
     S.d_table = (const uint64_t *)(blob + S.off_table);
+    S.d_table_keys = (const uint32_t *)(blob + S.off_keys);
     RSG_HIP(ctx, hipStreamWaitEvent(S.st, sl.scanned, 0));
 
     int dev_cus = 256;
@@ -536,7 +544,7 @@ rsg_status launch_range(Search &S, uint32_t lo, uint32_t hi) {
     hipEvent_t t0 = timed_begin(ctx, S.st);
     RSG_HIP(ctx, rsg::launch_roll(S.d_src, S.size, (uint32_t)S.head.block_len, (uint32_t)S.head.rem, (uint64_t)S.end,
                                   lo, hi, (const TileAgg *)sl.agg.p, (const TilePrefix *)sl.prefix.p, S.ntiles,
-                                  S.d_filter, S.d_filter16, S.d_table, S.bmask, (uint64_t *)sl.list.p, kCandCap,
+                                  S.d_filter, S.d_filter16, S.d_table, S.d_table_keys, S.bmask, (uint64_t *)sl.list.p, kCandCap,
                                   (uint32_t *)sl.counts.p, S.cus, S.fused, (uint2 *)sl.spill.p,
                                   (uint32_t *)sl.spill_n.p, S.st));
     timed_end(ctx, t0, S.st, 0);

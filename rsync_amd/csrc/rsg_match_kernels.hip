@@ -230,6 +230,20 @@ __device__ __forceinline__ uint32_t table_flags(const uint64_t *__restrict__ tab
     return fl;
 }
 
+// Whether sum is a basis Sum1, from the key-only copy of the bucket table
+// (same buckets; empty slots hold an existing key): two 16-byte loads, eight
+// compares.  The block length is not checked here: the confirmation resolves
+// a window only to blocks of its own length (match.go:118).
+__device__ __forceinline__ bool table_has(uint4 a, uint4 b, uint32_t sum) {
+    return (a.x == sum) | (a.y == sum) | (a.z == sum) | (a.w == sum) | (b.x == sum) | (b.y == sum) | (b.z == sum) |
+           (b.w == sum);
+}
+__device__ __forceinline__ void table_buckets(const uint32_t *__restrict__ keys, uint32_t bmask, uint32_t sum,
+                                              uint4 &a, uint4 &b) {
+    a = *reinterpret_cast<const uint4 *>(keys + (uint64_t)(bucket_hash1(sum) & bmask) * kBucketWays);
+    b = *reinterpret_cast<const uint4 *>(keys + (uint64_t)(bucket_hash2(sum) & bmask) * kBucketWays);
+}
+
 // The filter word of sum s, and whether both of s's bits are set in it.
 template <bool SEL>
 __device__ __forceinline__ uint32_t filt_index(uint32_t s) {
@@ -640,7 +654,7 @@ __device__ __forceinline__ u16x2 pair_bytes(uint32_t wa, uint32_t wb, int p) {
 template <int NBITS, bool EDGE>
 __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
-    uint32_t t_int, uint32_t tile_hi, const uint16_t *__restrict__ filter_g, const uint64_t *__restrict__ table,
+    uint32_t t_int, uint32_t tile_hi, const uint16_t *__restrict__ filter_g, const uint32_t *__restrict__ keys,
     uint32_t bmask, uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count) {
     constexpr uint32_t kWaves = kRollThreads / 64;
     constexpr uint32_t P = kRollPerThread;  // offsets per lane (2 streams of P/2)
@@ -663,14 +677,12 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     const uint32_t C128 = (128u * B) & 0xffffu;  // the filter index offset of P1
     uint32_t parity = 0;
 
-    // Exact probes of a wave's parked hits, as roll_kernel: the window at q
-    // has length k = min(B, size - q), a block of that length must carry the
-    // sum (interior windows: k = B).
-    const uint32_t rem_flag = (rem != 0 && rem != B) ? 4u : 2u;
-    auto probe = [&](uint64_t q, uint32_t fl) {
+    // Exact probes of a wave's parked hits: the window at q (length k =
+    // min(B, size - q); interior windows k = B) is a candidate when its sum
+    // is a basis Sum1 and some block has length k.
+    auto probe = [&](uint64_t q, bool present) {
         const uint32_t k = (uint32_t)min<uint64_t>((uint64_t)B, size - q);
-        const uint32_t need = (k == B) ? 2u : ((k == rem) ? rem_flag : 0u);
-        if (fl & need) {
+        if (present && (k == B || k == rem)) {
             const uint32_t at = atomicAdd(count, 1u);
             if (at < cap) cand[at] = q;
         }
@@ -679,7 +691,10 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     auto drain_rest = [&](uint32_t qh, uint64_t q0, uint32_t from, uint32_t n) {
         for (uint32_t i = from + lane; i < n; i += 64) {
             const uint2 e = queue[wave][qh][i];
-            probe(q0 + e.x, table_flags(table, bmask, unraw(e.y)));
+            const uint32_t sum = unraw(e.y);
+            uint4 ba, bb;
+            table_buckets(keys, bmask, sum, ba, bb);
+            probe(q0 + e.x, table_has(ba, bb, sum));
         }
     };
     uint32_t prev_n = 0, qh = 0;
@@ -758,15 +773,12 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         const bool next = t + 1 < t_end && t + 1 < t_int;
         if (next) fetch_plain(t + 1, On, A);
         uint2 pe = make_uint2(0, 0);
-        uint64_t pb[2 * kBucketWays];
+        uint4 pba, pbb;
         const bool pv = lane < prev_n;
         if (pv) {
             pe = queue[wave][qh ^ 1][lane];
             pe.y = unraw(pe.y);
-            const uint64_t *b1 = table + (uint64_t)(bucket_hash1(pe.y) & bmask) * kBucketWays;
-            const uint64_t *b2 = table + (uint64_t)(bucket_hash2(pe.y) & bmask) * kBucketWays;
-#pragma unroll
-            for (uint32_t i = 0; i < kBucketWays; i++) { pb[i] = b1[i]; pb[kBucketWays + i] = b2[i]; }
+            table_buckets(keys, bmask, pe.y, pba, pbb);
         }
         // lane totals, and the first 16 bytes' own (stream a's range) for
         // stream b's start window
@@ -918,13 +930,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
             carry[parity] = make_uint2(w1, (uint32_t)(q0 + kScanTile + B) * w1 - w2);
         }
         }  // interior tile
-        if (pv) {
-            uint32_t fl = 0;
-#pragma unroll
-            for (uint32_t i = 0; i < 2 * kBucketWays; i++)
-                if ((uint32_t)(pb[i] >> 32) == pe.y && (uint32_t)pb[i] != 0) fl |= (uint32_t)pb[i];
-            probe(prev_q0 + pe.x, fl);
-        }
+        if (pv) probe(prev_q0 + pe.x, table_has(pba, pbb, pe.y));
         if (prev_n > 64) drain_rest(qh ^ 1, prev_q0, 64, prev_n);
         prev_n = nq;
         prev_q0 = q0;
@@ -1362,9 +1368,9 @@ bool roll_filter_sel() {
 
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
-                       const uint32_t *bitmap, const uint16_t *filter16, const uint64_t *table, uint32_t bmask,
-                       uint64_t *cand, uint32_t cap, uint32_t *count, uint32_t grid, bool fused, uint2 *spill,
-                       uint32_t *spill_n, hipStream_t stream) {
+                       const uint32_t *bitmap, const uint16_t *filter16, const uint64_t *table,
+                       const uint32_t *table_keys, uint32_t bmask, uint64_t *cand, uint32_t cap, uint32_t *count,
+                       uint32_t grid, bool fused, uint2 *spill, uint32_t *spill_n, hipStream_t stream) {
     if (tile_hi <= tile_lo) return hipSuccess;
     if (fused && filter16) {
         // Interior tiles [tile_lo, t_int): every offset of tile t visited
@@ -1382,12 +1388,12 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                 const uint32_t ga = min(grid, tile_hi - tile_lo);
                 auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, true> : roll_packed_kernel<2, true>;
                 hipLaunchKernelGGL(kern, dim3(ga), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
-                                   t_int, tile_hi, filter16, table, bmask, cand, cap, count);
+                                   t_int, tile_hi, filter16, table_keys, bmask, cand, cap, count);
                 return hipGetLastError();
             } else if (roll_packed() == 1 || !spill) {
                 auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, false> : roll_packed_kernel<2, false>;
                 hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
-                                   t_int, t_int, filter16, table, bmask, cand, cap, count);
+                                   t_int, t_int, filter16, table_keys, bmask, cand, cap, count);
             } else {
                 auto kern = roll_packed() == 3 ? roll_lane_kernel<true> : roll_lane_kernel<false>;
                 hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, tile_lo, t_int,
