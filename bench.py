@@ -581,7 +581,7 @@ def bench_sender(args, rank, world, local):
                                      "call": "rsg_hash_search_batch_device, one call per pass"},
                           "ms_per_file": round(dt * 1e3 / (steps * len(metas)), 3),
                           "single_file_calls_gib_s": single_gib_s,
-                          "roofline": {"bound": "hbm", "kernel": "roll_packed_kernel (+ roll_kernel on the edge tiles)",
+                          "roofline": {"bound": "hbm", "kernel": "roll_packed_kernel (edge tiles included)",
                                        "note": "the roll is VALU-issue-bound (integer ops at 4 cycles per wave64, "
                                                "DESIGN.md section 4.2); frac is its HBM fraction, as the metric's unit",
                                        "achieved": round(src_bytes / (roll_ms * 1e-3) / 1e9, 1),
