@@ -42,7 +42,6 @@ struct TableScratch {
 struct SearchSlot {
     TableScratch hs;                   // host scratch of the table build
     DevBuf agg, prefix, counts, list;  // tile sums, tile prefixes, candidate count and list
-    DevBuf spill, spill_n;             // packed roll's spilled filter hits (per wave) and their counts
     DevBuf blob;                       // basis tables, one upload: groups | hi16 | sum2 | filter | table
     DevBuf src;                        // realigned or uploaded source
     PinBuf stage;                      // pinned staging of the blob

@@ -95,11 +95,7 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
                        const uint32_t *bitmap, const uint16_t *filter16, const uint64_t *table,
                        const uint32_t *table_keys, uint32_t bmask, uint64_t *cand, uint32_t cap, uint32_t *count,
-                       uint32_t grid, bool fused, uint2 *spill, uint32_t *spill_n, hipStream_t stream);
-// Spill regions of the lane-slot packed roll: kRollSpillCap (offset, sum)
-// items per roll wave (grid x 16 waves), and one count per wave.
-constexpr uint32_t kRollSpillCap = 1024;
-inline uint64_t roll_spill_bytes(uint32_t grid) { return (uint64_t)grid * (kRollThreads / 64) * kRollSpillCap * 8; }
+                       uint32_t grid, bool fused, hipStream_t stream);
 // The packed roll's filter (roll_packed_kernel, fused mode, interior tiles):
 // 2^16 16-bit words, word ((s1 + 128 B) xor s2) mod 2^16, bits s2[0..3],
 // s2[4..7] and (by default) s2[8..11].  s1 of a long window of random bytes is
@@ -114,7 +110,7 @@ __host__ __device__ inline uint32_t f16_mask(uint32_t sum, int nbits = 2) {
     return nbits == 3 ? m | (1u << ((sum >> 24) & 15u)) : m;
 }
 int roll_filter_bits();  // RSG_ROLL_BITS (read once): bits per sum in the packed roll's filter, 2 or 3
-int roll_packed();  // RSG_ROLL_PACKED (read once): 0 roll_kernel only, 1 packed + ballots, 2 packed + lane slots
+int roll_packed();  // RSG_ROLL_PACKED (read once): 0 roll_kernel only, else the packed roll (default)
 // Block lengths up to which roll derives its window sums itself (no tile_agg
 // / tile_scan passes): each workgroup reads B extra bytes once.
 constexpr uint32_t kFusedMaxB = 4 * kScanTile;

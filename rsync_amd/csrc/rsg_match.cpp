@@ -526,10 +526,6 @@ rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
     S.cus = S.roll_grid ? std::min<uint32_t>(S.roll_grid, (uint32_t)dev_cus) : (uint32_t)dev_cus;
     const uint64_t scan_end = std::min<uint64_t>((uint64_t)S.end, S.size);
     S.tile_end = (uint32_t)((scan_end + kScanTile - 1) / kScanTile);
-    if (S.d_filter16) {  // the packed roll's spill regions (one per roll wave)
-        if ((s = ensure_dev(ctx, sl.spill, rsg::roll_spill_bytes(S.cus))) != RSG_OK) return s;
-        if ((s = ensure_dev(ctx, sl.spill_n, (uint64_t)S.cus * (rsg::kRollThreads / 64) * 4)) != RSG_OK) return s;
-    }
     if ((s = launch_range(S, 0, S.tile_end)) != RSG_OK) return s;
     S.pending = true;
     return RSG_OK;
@@ -545,22 +541,8 @@ rsg_status launch_range(Search &S, uint32_t lo, uint32_t hi) {
     RSG_HIP(ctx, rsg::launch_roll(S.d_src, S.size, (uint32_t)S.head.block_len, (uint32_t)S.head.rem, (uint64_t)S.end,
                                   lo, hi, (const TileAgg *)sl.agg.p, (const TilePrefix *)sl.prefix.p, S.ntiles,
                                   S.d_filter, S.d_filter16, S.d_table, S.d_table_keys, S.bmask, (uint64_t *)sl.list.p, kCandCap,
-                                  (uint32_t *)sl.counts.p, S.cus, S.fused, (uint2 *)sl.spill.p,
-                                  (uint32_t *)sl.spill_n.p, S.st));
+                                  (uint32_t *)sl.counts.p, S.cus, S.fused, S.st));
     timed_end(ctx, t0, S.st, 0);
-    if (getenv("RSG_ROLL_DEBUG") && sl.spill_n.p) {  // diagnostic: spilled items per roll wave
-        const size_t nw = (size_t)S.cus * (rsg::kRollThreads / 64);
-        std::vector<uint32_t> sn(nw);
-        uint32_t cnt = 0;
-        RSG_HIP(ctx, hipStreamSynchronize(S.st));
-        RSG_HIP(ctx, hipMemcpy(sn.data(), sl.spill_n.p, nw * 4, hipMemcpyDeviceToHost));
-        RSG_HIP(ctx, hipMemcpy(&cnt, sl.counts.p, 4, hipMemcpyDeviceToHost));
-        uint64_t tot = 0;
-        uint32_t mx = 0;
-        for (uint32_t v : sn) { tot += v; mx = std::max(mx, v); }
-        fprintf(stderr, "[rsg] roll tiles [%u, %u): %u candidates, spilled %llu (max %u per wave)\n", lo, hi, cnt,
-                (unsigned long long)tot, mx);
-    }
     RSG_HIP(ctx, hipMemcpyAsync(sl.count.p, sl.counts.p, 4, hipMemcpyDeviceToHost, S.st));
     RSG_HIP(ctx, hipEventRecord(sl.rolled, S.st));
     return RSG_OK;

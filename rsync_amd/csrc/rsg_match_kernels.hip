@@ -24,7 +24,6 @@
 #include <stdlib.h>
 
 #include <algorithm>
-#include <type_traits>
 
 #include "rsg_internal.h"
 
@@ -944,314 +943,6 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     drain_rest(qh ^ 1, prev_q0, 0, prev_n);
 }
 
-// --------------------------------------------------------------- roll, packed, lane slots
-// roll_packed_kernel's arithmetic and filter with lane-private parking: the
-// offset loop has no ballot and no scalar bookkeeping.  A pair step with a
-// filter hit stores the lane's (P1, P2) in its next LDS slot (c += hit, an
-// exec-masked store); the hit bits go to a per-lane mask (bit j: stream a at
-// step j, bit 16 + j: stream b).  Nothing on the roll's path waits for an
-// exact probe:
-//  * at the start of tile t + 1 each lane's first item of tile t (its lowest
-//    hit bit) gets its bucket loads, compared after the tile's sums and scan;
-//  * its further items, and the hits of a lane whose kLaneSlots slots are
-//    taken (spilled from the offset loop itself, a rarely taken branch), go
-//    -- (offset from the workgroup's first tile, sum) -- to the wave's region
-//    of a global list at a position from an LDS counter per wave, and
-//    roll_spill_probe_kernel probes them after the roll.  A full region
-//    sends its overflow straight to the candidates (the confirmation
-//    re-checks them exactly, as roll_kernel's full queue does).
-constexpr uint32_t kLaneSlots = 3;
-
-template <bool DIAG>  // DIAG: timing only, no redo and no spills (results incomplete)
-__global__ __launch_bounds__(kRollThreads) void roll_lane_kernel(
-    const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t tile_lo, uint32_t tile_hi,
-    const uint16_t *__restrict__ filter_g, const uint64_t *__restrict__ table, uint32_t bmask,
-    uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count, uint2 *__restrict__ spill,
-    uint32_t spill_cap, uint32_t *__restrict__ spill_n) {
-    constexpr uint32_t kWaves = kRollThreads / 64;
-    constexpr uint32_t P = kRollPerThread;
-    constexpr int OW = (int)P / 4;
-    constexpr int NV = (int)P / 16;
-    constexpr int H = (int)P / 2;
-    static_assert(P == 32 && kWaves <= 16, "two streams of 16 offsets per lane");
-    __shared__ uint16_t filt[1u << 16];                   // 128 KiB
-    __shared__ uint2 slots[kWaves][64 * kLaneSlots];      // 24 KiB
-    __shared__ uint2 wsum[2][kWaves];
-    __shared__ uint2 carry[2];
-    __shared__ uint32_t wspill[kWaves];                   // spilled items per wave
-    if (threadIdx.x < kWaves) wspill[threadIdx.x] = 0;
-    {
-        const uint4 *fg = reinterpret_cast<const uint4 *>(filter_g);
-        uint4 *fl = reinterpret_cast<uint4 *>(filt);
-        for (uint32_t i = threadIdx.x; i < (1u << 16) / 8; i += kRollThreads) fl[i] = fg[i];
-    }
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t C128 = (128u * B) & 0xffffu;
-    uint2 *const myslot = &slots[wave][lane * kLaneSlots];
-    uint32_t parity = 0;
-
-    auto unraw = [&](uint32_t raw) { return (raw & 0xffff0000u) | ((raw - C128) & 0xffffu); };
-    auto emit = [&](uint64_t q) {
-        const uint32_t at = atomicAdd(count, 1u);
-        if (at < cap) cand[at] = q;
-    };
-    // item = lowest set bit of a hit mask m (bit j: stream a, step j; bit
-    // 16 + j: stream b), its entry = the number of steps below j with a hit;
-    // false for an entry past the slots (spilled from the loop already)
-    auto item = [&](uint32_t m, uint32_t mall, uint2 e0, uint2 e1, uint2 e2, uint32_t &off, uint32_t &sum) {
-        const uint32_t b = __builtin_ctz(m);
-        const uint32_t j = b & 15u;
-        const uint32_t any = (mall | (mall >> 16)) & ((1u << j) - 1u);
-        const uint32_t k = __builtin_popcount(any);
-        const uint2 e = k == 0 ? e0 : (k == 1 ? e1 : e2);
-        const uint32_t raw = b >= 16 ? __builtin_amdgcn_perm(e.y, e.x, 0x07060302u)
-                                     : __builtin_amdgcn_perm(e.y, e.x, 0x05040100u);
-        off = b >= 16 ? j + (uint32_t)H : j;
-        sum = unraw(raw);
-        return k < kLaneSlots;
-    };
-    const uint32_t per = (tile_hi - tile_lo + gridDim.x - 1) / gridDim.x;
-    const uint32_t t_begin = tile_lo + blockIdx.x * per;
-    const uint32_t t_end = min(tile_hi, t_begin + per);
-    const uint64_t q_wg = (uint64_t)t_begin * kScanTile;  // spilled offsets are relative to it
-    uint2 *const region = spill + (uint64_t)(blockIdx.x * kWaves + wave) * spill_cap;
-    // Spill (q, sum) of the calling lane (any exec mask).
-    auto spill_item = [&](uint64_t q, uint32_t sum) {
-        const uint32_t at = atomicAdd(&wspill[wave], 1u);
-        if (at < spill_cap) region[at] = make_uint2((uint32_t)(q - q_wg), sum);
-        else emit(q);  // region full: an unprobed candidate
-    };
-    const uint32_t lo = threadIdx.x * P;
-    const uint32_t sh = B & 3u;
-    uint32_t D1 = 0, DM = 0;
-    if (t_begin < t_end) {
-        const uint64_t qb = (uint64_t)t_begin * kScanTile;
-        uint32_t a1 = 0, a2 = 0;
-        for (uint32_t off = threadIdx.x * 16u; off < B; off += kRollThreads * 16u) {
-            uint32_t w[4];
-            load_vec(src, size, qb + off, w);
-            if (off + 16u > B) {
-                const uint32_t keep = B - off;
-#pragma unroll
-                for (uint32_t q = 0; q < 4; q++) {
-                    const uint32_t nb = keep > 4 * q ? min(keep - 4 * q, 4u) : 0u;
-                    w[q] &= nb >= 4 ? 0xffffffffu : ((1u << (8 * nb)) - 1u);
-                }
-            }
-            int32_t v1, v2;
-            vec_sums(w, v1, v2);
-            a1 += (uint32_t)v1;
-            a2 += (uint32_t)v2 + (uint32_t)(qb + off) * (uint32_t)v1;
-        }
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-            a1 += __shfl_xor(a1, m, 64);
-            a2 += __shfl_xor(a2, m, 64);
-        }
-        if (lane == 0) wsum[0][wave] = make_uint2(a1, a2);
-        __syncthreads();
-#pragma unroll
-        for (uint32_t w = 0; w < kWaves; w++) {
-            D1 += __builtin_amdgcn_readfirstlane(wsum[0][w].x);
-            DM += __builtin_amdgcn_readfirstlane(wsum[0][w].y);
-        }
-        __syncthreads();
-    }
-    uint32_t O[OW], A[OW + 4], On[OW];
-    auto fetch_plain = [&](uint32_t tt, uint32_t *o, uint32_t *a) {
-        const uint8_t *p = src + (uint64_t)tt * kScanTile + lo;
-#pragma unroll
-        for (int q = 0; q < NV; q++) {
-            const u32x4a4m v = *reinterpret_cast<const u32x4a4m *>(p + 16 * q);
-            o[4 * q] = v.x; o[4 * q + 1] = v.y; o[4 * q + 2] = v.z; o[4 * q + 3] = v.w;
-        }
-        const uint8_t *pa = p + B - sh;
-#pragma unroll
-        for (int q = 0; q < NV + 1; q++) {
-            const u32x4a4m v = *reinterpret_cast<const u32x4a4m *>(pa + 16 * q);
-            a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
-        }
-    };
-    if (t_begin < t_end) fetch_plain(t_begin, O, A);
-    const u16x2 negB = as_u16x2(((0x10000u - (B & 0xffffu)) & 0xffffu) * 0x10001u);
-    uint32_t pmall = 0;  // the previous tile's hit mask (its entries are still in the lane's slots)
-    uint64_t pq = 0;     // q0 + lo of the previous tile
-    for (uint32_t t = t_begin; t < t_end; t++) {
-        const uint64_t q0 = (uint64_t)t * kScanTile;
-        const uint64_t qt = q0 + lo;
-        uint32_t S[OW];
-#pragma unroll
-        for (int k = 0; k < OW; k++) S[k] = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sh);
-        const bool next = t + 1 < t_end;
-        if (next) fetch_plain(t + 1, On, A);
-        // The previous tile's items, before this tile's offset loop reuses the
-        // slots: the first item's bucket loads now (compared after the sums
-        // and the scan below), the rest spilled.
-        uint32_t pm = pmall;
-        uint32_t poff = 0, psum = 0;
-        uint64_t pb[2 * kBucketWays];
-        const bool pv = pm != 0;
-        const uint2 pe0 = myslot[0], pe1 = myslot[1], pe2 = myslot[2];
-        bool pk = false;  // the prefetched item is in a slot
-        if (pv) {
-            pk = item(pm, pmall, pe0, pe1, pe2, poff, psum);
-            pm &= pm - 1u;
-            const uint64_t *b1 = table + (uint64_t)(bucket_hash1(psum) & bmask) * kBucketWays;
-            const uint64_t *b2 = table + (uint64_t)(bucket_hash2(psum) & bmask) * kBucketWays;
-#pragma unroll
-            for (uint32_t i = 0; i < kBucketWays; i++) { pb[i] = b1[i]; pb[kBucketWays + i] = b2[i]; }
-        }
-        while (!DIAG && pm != 0) {
-            uint32_t off, sum;
-            const bool in_slot = item(pm, pmall, pe0, pe1, pe2, off, sum);
-            pm &= pm - 1u;
-            if (in_slot) spill_item(pq + off, sum);
-        }
-        int32_t o1, o2, s1, s2, v1, v2;
-        vec_sums(O, o1, o2);
-        vec_sums(S, s1, s2);
-        const int32_t o1a = o1, o2a = o2, s1a = s1, s2a = s2;
-#pragma unroll
-        for (int c = 1; c < NV; c++) {
-            vec_sums(O + 4 * c, v1, v2);
-            o2 += v2 + 16 * c * v1;
-            o1 += v1;
-            vec_sums(S + 4 * c, v1, v2);
-            s2 += v2 + 16 * c * v1;
-            s1 += v1;
-        }
-        uint32_t exA, exB;
-        {
-            const uint32_t so2 = (uint32_t)s2 + lo * (uint32_t)s1, oo2 = (uint32_t)o2 + lo * (uint32_t)o1;
-            const uint32_t a = (uint32_t)s1 - (uint32_t)o1;
-            const uint32_t b = (so2 + (uint32_t)(q0 + B) * (uint32_t)s1) - (oo2 + (uint32_t)q0 * (uint32_t)o1);
-            const uint32_t ia = wave_incl_scan(a), ib = wave_incl_scan(b);
-            if (lane == 63) wsum[parity][wave] = make_uint2(ia, ib);
-            __syncthreads();
-            const uint32_t w = lane & 15u;
-            uint2 p = wsum[parity][min(w, kWaves - 1)];
-            if (w >= wave) p = make_uint2(0, 0);
-            exA = ia - a + row16_sum(p.x);
-            exB = ib - b + row16_sum(p.y);
-        }
-        if (t != t_begin) {
-            const uint2 c = carry[parity];
-            D1 = __builtin_amdgcn_readfirstlane(c.x);
-            DM = __builtin_amdgcn_readfirstlane(c.y);
-        }
-        parity ^= 1u;
-        if (pk) {
-            uint32_t fl = 0;
-#pragma unroll
-            for (uint32_t i = 0; i < 2 * kBucketWays; i++)
-                if ((uint32_t)(pb[i] >> 32) == psum && (uint32_t)pb[i] != 0) fl |= (uint32_t)pb[i];
-            if (fl & 2u) emit(pq + poff);
-        }
-        const uint32_t W1 = D1 + exA;
-        const uint32_t W2 = (uint32_t)(qt + B) * W1 - (DM + exB);
-        const uint32_t da = (uint32_t)(s1a - o1a);
-        const uint32_t W1b = W1 + da;
-        const uint32_t W2b = W2 + 16u * W1 + 16u * da - (uint32_t)(s2a - o2a) - B * (uint32_t)o1a;
-        const u16x2 P10 = as_u16x2(((W1 + C128) & 0xffffu) | ((W1b + C128) << 16));
-        const u16x2 P20 = as_u16x2((W2 & 0xffffu) | (W2b << 16));
-        uint32_t Ox[OW], Sx[OW];
-#pragma unroll
-        for (int k = 0; k < OW; k++) {
-            Ox[k] = O[k] ^ 0x80808080u;
-            Sx[k] = S[k] ^ 0x80808080u;
-        }
-        // One pass over the lane's 16 pair steps; `sink(j, p1, p2, z)` gets
-        // each step's packed sums and its filter bits (bit 0: a, bit 16: b).
-        auto steps = [&](auto g_tag, auto &&sink) {
-            u16x2 P1 = P10, P2 = P20;
-            constexpr int G = decltype(g_tag)::value;
-#pragma unroll
-            for (int g0 = 0; g0 < H; g0 += G) {
-                u16x2 p1[G], p2[G], wd[G];
-#pragma unroll
-                for (int jj = 0; jj < G; jj++) {
-                    const int j = g0 + jj;
-                    p1[jj] = P1;
-                    p2[jj] = P2;
-                    const u16x2 X = P1 ^ P2;  // the word index of both windows
-                    wd[jj] = u16x2{filt[X.x], filt[X.y]};
-                    const u16x2 uo = pair_bytes(Ox[j >> 2], Ox[(j >> 2) + OW / 2], j & 3);
-                    const u16x2 ui = pair_bytes(Sx[j >> 2], Sx[(j >> 2) + OW / 2], j & 3);
-                    P1 = P1 + ui - uo;
-                    P2 = P2 + uo * negB + P1;
-                }
-#pragma unroll
-                for (int jj = 0; jj < G; jj++) {
-                    const u16x2 x = pk_shr(wd[jj], p2[jj]);
-                    const u16x2 y = pk_shr(wd[jj], p2[jj] >> (uint16_t)4);
-                    const uint32_t z = as_u32(x & y) & 0x00010001u;
-                    sink(g0 + jj, as_u32(p1[jj]), as_u32(p2[jj]), z);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            return make_uint2(as_u32(P1), as_u32(P2));
-        };
-        uint32_t m = 0, c = 0;
-        const uint2 fin = steps(std::integral_constant<int, 4>{}, [&](int j, uint32_t r1, uint32_t r2, uint32_t z) {
-            // a hit takes the lane's next slot (an exec-masked store); with
-            // the slots taken, its items are spilled right here
-            if (z != 0) {
-                if (c < kLaneSlots) {
-                    myslot[c] = make_uint2(r1, r2);
-                } else if (!DIAG) {
-                    if (z & 1u) spill_item(qt + (uint32_t)j, unraw(__builtin_amdgcn_perm(r2, r1, 0x05040100u)));
-                    if (z >> 16) spill_item(qt + (uint32_t)(H + j), unraw(__builtin_amdgcn_perm(r2, r1, 0x07060302u)));
-                }
-            }
-            m |= z << j;
-            c += z != 0 ? 1u : 0u;
-        });
-        if (threadIdx.x == kRollThreads - 1) {
-            const uint32_t w1 = ((fin.x >> 16) - C128) & 0xffffu, w2 = fin.y >> 16;
-            carry[parity] = make_uint2(w1, (uint32_t)(q0 + kScanTile + B) * w1 - w2);
-        }
-        pmall = m;
-        pq = qt;
-        if (next) {
-#pragma unroll
-            for (int k = 0; k < OW; k++) O[k] = On[k];
-        }
-    }
-    if (!DIAG) {  // the last tile's items
-        const uint2 pe0 = myslot[0], pe1 = myslot[1], pe2 = myslot[2];
-        for (uint32_t pm = pmall; pm != 0;) {
-            uint32_t off, sum;
-            const bool in_slot = item(pm, pmall, pe0, pe1, pe2, off, sum);
-            pm &= pm - 1u;
-            if (in_slot) spill_item(pq + off, sum);
-        }
-    }
-    __syncthreads();  // every wave's spills counted
-    if (lane == 0) spill_n[blockIdx.x * kWaves + wave] = min(wspill[wave], spill_cap);
-}
-
-// Exact probes of roll_lane_kernel's spilled items: one workgroup per roll
-// wave region (same grid arithmetic as the roll).
-__global__ __launch_bounds__(64) void roll_spill_probe_kernel(const uint2 *__restrict__ spill, uint32_t spill_cap,
-                                                              const uint32_t *__restrict__ spill_n, uint32_t tile_lo,
-                                                              uint32_t per, const uint64_t *__restrict__ table,
-                                                              uint32_t bmask, uint64_t *__restrict__ cand,
-                                                              uint32_t cap, uint32_t *__restrict__ count) {
-    const uint32_t wid = blockIdx.x;
-    const uint32_t n = spill_n[wid];
-    const uint64_t q_wg = (uint64_t)(tile_lo + (wid / (kRollThreads / 64)) * per) * kScanTile;
-    const uint2 *region = spill + (uint64_t)wid * spill_cap;
-    for (uint32_t i = threadIdx.x; i < n; i += 64) {
-        const uint2 e = region[i];
-        if (table_flags(table, bmask, e.y) & 2u) {
-            const uint32_t at = atomicAdd(count, 1u);
-            if (at < cap) cand[at] = q_wg + e.x;
-        }
-    }
-}
-
 // --------------------------------------------------------------- confirm plan
 // One DevFile per candidate window, in the roll's append order: window
 // [q, q + min(B, size - q)) is record i (match.go:114-117).  The confirmation
@@ -1331,10 +1022,10 @@ hipError_t launch_tile_scan(const TileAgg *agg, uint32_t ntiles, TilePrefix *pre
 
 int roll_packed() {
     // A/B switch RSG_ROLL_PACKED: 0 = roll_kernel for every tile, 1
-    // (default) = the packed roll with ballot parking, 2 = with lane slots
+    // (default) = the packed roll for the fused mode
     static const int v = [] {
         const char *e = getenv("RSG_ROLL_PACKED");
-        return e ? std::max(0, std::min(3, atoi(e))) : 1;  // 3: lane slots without spills (timing only)
+        return (e && e[0] == '0') ? 0 : 1;
     }();
     return v;
 }
@@ -1370,38 +1061,30 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
                        const uint32_t *bitmap, const uint16_t *filter16, const uint64_t *table,
                        const uint32_t *table_keys, uint32_t bmask, uint64_t *cand, uint32_t cap, uint32_t *count,
-                       uint32_t grid, bool fused, uint2 *spill, uint32_t *spill_n, hipStream_t stream) {
+                       uint32_t grid, bool fused, hipStream_t stream) {
     if (tile_hi <= tile_lo) return hipSuccess;
     if (fused && filter16) {
         // Interior tiles [tile_lo, t_int): every offset of tile t visited
         // ((t+1) T <= end) and its window and shifted-byte loads inside the
         // source ((t+1) T + B + 48 <= size).  The packed kernel (default) takes
         // the whole range and rolls the rest -- the source's last B bytes or
-        // so -- with its scalar edge path; the lane-slot variant leaves them
-        // to roll_kernel.  A range with no interior tile is roll_kernel's.
+        // so -- with its scalar edge path (RSG_ROLL_EDGE=0: a roll_kernel
+        // launch takes them).  A range with no interior tile is roll_kernel's.
         const uint64_t lim = std::min<uint64_t>(end, size >= (uint64_t)B + 48 ? size - B - 48 : 0);
         const uint32_t t_int = (uint32_t)std::max<uint64_t>(tile_lo, std::min<uint64_t>(tile_hi, lim / kScanTile));
         if (t_int > tile_lo) {
             const uint32_t g = min(grid, t_int - tile_lo);
-            if ((roll_packed() == 1 || !spill) && roll_edge_inside()) {
+            if (roll_edge_inside()) {
                 // the whole range: the packed kernel rolls its edge tiles itself
                 const uint32_t ga = min(grid, tile_hi - tile_lo);
                 auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, true> : roll_packed_kernel<2, true>;
                 hipLaunchKernelGGL(kern, dim3(ga), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
                                    t_int, tile_hi, filter16, table_keys, bmask, cand, cap, count);
                 return hipGetLastError();
-            } else if (roll_packed() == 1 || !spill) {
-                auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, false> : roll_packed_kernel<2, false>;
-                hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
-                                   t_int, t_int, filter16, table_keys, bmask, cand, cap, count);
-            } else {
-                auto kern = roll_packed() == 3 ? roll_lane_kernel<true> : roll_lane_kernel<false>;
-                hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, tile_lo, t_int,
-                                   filter16, table, bmask, cand, cap, count, spill, kRollSpillCap, spill_n);
-                const uint32_t per = (t_int - tile_lo + g - 1) / g;
-                hipLaunchKernelGGL(roll_spill_probe_kernel, dim3(g * (kRollThreads / 64)), dim3(64), 0, stream, spill,
-                                   kRollSpillCap, spill_n, tile_lo, per, table, bmask, cand, cap, count);
             }
+            auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, false> : roll_packed_kernel<2, false>;
+            hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, t_int,
+                               t_int, filter16, table_keys, bmask, cand, cap, count);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
