@@ -19,6 +19,10 @@
 //              candidates.  Candidates are confirmed on the host side of the
 //              C-ABI with the strong-sum kernel (rsg_blocksums.hip) in the
 //              greedy order of match.go (rsg_match.cpp).
+//   roll_packed  the default for B <= kFusedMaxB: the same roll with two
+//              windows per lane in the 16-bit halves of each register
+//              (v_pk_* updates), a 2^16 x 16-bit LDS filter and a key-only
+//              probe table; its range's last tiles on a scalar edge path.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
