@@ -587,7 +587,7 @@ def bench_sender(args, rank, world, local):
                                        "achieved": round(src_bytes / (roll_ms * 1e-3) / 1e9, 1),
                                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                        "frac": round(src_bytes / (roll_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                       "traffic": None, "kernel_ms": round(roll_ms, 4),
+                                       "traffic": cfg3_traffic(), "kernel_ms": round(roll_ms, 4),
                                        "launches": kt["roll_launches"],
                                        "algorithmic_bytes_per_launch": int(src_bytes),
                                        "confirm_ms_per_batch": round(confirm_ms, 4),
@@ -597,6 +597,16 @@ def bench_sender(args, rank, world, local):
                           "oracle_parity_file0": parity,
                           "cpu_baseline": cpu}), flush=True)
     eng.close()
+
+
+def cfg3_traffic():
+    """HBM bytes per roll launch from the committed PMC pass of the cfg3 bench
+    (FETCH_SIZE x 2, profiles/traffic.json; not measured in this run)."""
+    try:
+        t = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
+        return int(t["roll_packed_kernel_cfg3_bytes_per_launch"])
+    except Exception:
+        return None
 
 
 def cfg4_traffic(world, records):
