@@ -163,7 +163,8 @@ rsg_status rsg_set_block_sums_kernel(int32_t variant);
  * product kernel and the "records" it writes are meaningless.  1 = staged
  * memory only, 2 = staged hashing only, 3 = park memory only, 4 = park
  * hashing only, 5 = linear read of the arena (plain loads), 6 = linear read
- * (LDS DMA).  0 = off (default; environment RSG_BLOCKSUMS_DIAG).  Kept apart
+ * (LDS DMA), 7 = linear read (LDS DMA) 4 bytes off 16-byte alignment, 8 = park
+ * memory only with 16-byte aligned requests.  0 = off (default; environment RSG_BLOCKSUMS_DIAG).  Kept apart
  * from rsg_set_block_sums_kernel so the product knob can never select a
  * diagnostic. */
 rsg_status rsg_set_block_sums_diagnostic(int32_t diag);

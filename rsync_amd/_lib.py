@@ -155,6 +155,9 @@ _PROTOS = {
     "rsg_mux_deframe": (_st, [_vp, _u64, _vp, _u64, ctypes.POINTER(_u64)]),
     "rsg_put_int64": (_st, [ctypes.c_int64, _vp, ctypes.POINTER(_u64)]),
     "rsg_get_int64": (_st, [_vp, _u64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(_u64)]),
+    # include/rsg_testing.h (test hooks, not part of the drop-in boundary)
+    "rsg_testing_walk": (_st, [_vp, _u64, _vp, _u64, ctypes.POINTER(SumHead), ctypes.POINTER(Match), _u64,
+                               ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
 }
 
 for _name, (_res, _args) in _PROTOS.items():

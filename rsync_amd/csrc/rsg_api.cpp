@@ -432,7 +432,7 @@ rsg_status rsg_set_block_sums_kernel(int32_t variant) {
 }
 
 rsg_status rsg_set_block_sums_diagnostic(int32_t diag) {
-    if (diag < 0 || diag > 6) return fail(nullptr, RSG_ERR_INVALID, "diagnostic must be 0..6");
+    if (diag < 0 || diag > 8) return fail(nullptr, RSG_ERR_INVALID, "diagnostic must be 0..8");
     rsg::set_block_sums_diagnostic(diag);
     return RSG_OK;
 }

@@ -476,14 +476,16 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
 // hashing, i.e. the empirical HBM-read roofline of this box for DESIGN.md.
 // LDS = false: coalesced global_load_dwordx4, 4 in flight per lane;
 // LDS = true: the same bytes through buffer_load_dwordx4 ... lds.
-template <bool LDS>
+// MIS: every lane's 16-byte request shifted by 4 bytes (LDS only): the same
+// linear stream, misaligned as most quads of 700-byte blocks are.
+template <bool LDS, uint32_t MIS = 0>
 __global__ __launch_bounds__(256) void diag_linear_read(const uint8_t *__restrict__ arena, uint64_t bytes,
                                                         uint32_t *__restrict__ sink) {
     __shared__ __attribute__((aligned(16))) uint8_t buf[4 * 4096];
     const uint64_t per_iter = (uint64_t)gridDim.x * 256 * 64;  // 4 x 16 B per lane
     uint32_t acc = 0;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint64_t base = (uint64_t)blockIdx.x * 256 * 64; base + 256 * 64 <= bytes; base += per_iter) {
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 * 64; base + 256 * 64 + MIS <= bytes; base += per_iter) {
         if (LDS) {
             const uint64_t wb = base + wave * 4096;
             const __amdgpu_buffer_rsrc_t r =
@@ -492,7 +494,7 @@ __global__ __launch_bounds__(256) void diag_linear_read(const uint8_t *__restric
             for (int i = 0; i < 4; i++)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
                     r, (__attribute__((address_space(3))) void *)(buf + wave * 4096 + 1024 * i), 16,
-                    (threadIdx.x & 63) * 16, 1024 * i, 0, 0);
+                    (threadIdx.x & 63) * 16 + MIS, 1024 * i, 0, 0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             acc ^= *reinterpret_cast<const uint32_t *>(buf + wave * 4096 + (threadIdx.x & 63) * 4);
         } else {
@@ -650,11 +652,15 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
 // jj/uu: per-lane block index and byte offset (0x40000000 for the pad) of
 // each instruction, precomputed by the loader (UNROLL); otherwise computed on
 // the fly (a caller short of VGPRs).
-template <int AUX, bool UNROLL>
+template <int AUX, bool UNROLL, bool ALN = false>
 __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, const PkDesc &d, uint32_t lane,
                                          const uint32_t *jj = nullptr, const uint32_t *uu = nullptr) {
+    // ALN (timing diagnostic only): every quad request rounded down to a
+    // 16-byte boundary of the arena -- the same bytes per tile, naturally
+    // aligned, to price the misaligned quads of blocks at a 700-byte stride
+    const uint32_t amis = ALN ? (uint32_t)(d.base & 15u) : 0u;
     const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(arena + d.base), (short)0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)(arena + (d.base - amis)), (short)0, 0x7FFFFFFF, 0x00020000);
     const int rel = (int)(uint32_t)(d.off - d.base);
 #define RSG_PK_ONE(I_, REG)                                                                                     \
     do {                                                                                                        \
@@ -671,7 +677,7 @@ __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, con
         uint32_t vo_;                                                                                           \
         if (REG) {                                                                                              \
             const uint32_t nj_ = j_ == d.jl ? d.nl : d.B;                                                       \
-            vo_ = u16_ < nj_ ? d.B * j_ + u16_ : 0x80000000u;                                                   \
+            vo_ = u16_ < nj_ ? (ALN ? ((d.B * j_ + u16_ + amis) & ~15u) : d.B * j_ + u16_) : 0x80000000u;     \
         } else {                                                                                                \
             const uint32_t rj_ = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * j_), rel);                  \
             const uint32_t nj_ = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * j_), (int)d.n);             \
@@ -711,7 +717,7 @@ __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, con
 #pragma unroll
                 for (uint32_t k = 0; k < kBatch; k++) {
                     const uint32_t u16 = uu[i0 + k];
-                    const uint32_t vo = u16 < nj[k] ? rj[k] + u16 : 0x80000000u;
+                    const uint32_t vo = u16 < nj[k] ? (ALN ? ((rj[k] + u16 + amis) & ~15u) : rj[k] + u16) : 0x80000000u;
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(
                         rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * (i0 + k)), 16, vo, 0, 0, AUX);
                 }
@@ -758,7 +764,8 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
 }
 
 // MODE 0 = product; diagnostics: 1 = memory only (DMA + copy, no hashing),
-// 2 = hashing only (no DMA: the hashers hash whatever the slots hold).
+// 2 = hashing only (no DMA: the hashers hash whatever the slots hold),
+// 3 = memory only with every quad request 16-byte aligned (ALN above).
 // The tile DMA uses the nt cache policy (aux = 2): every byte is read once.
 // (A/B, profiles/r02f_ab_park_cache_policy*.json: the default policy, sc0 or
 // sc1 alone cost 6-9 %; nt combined with sc0 / sc1 equals nt.)
@@ -815,7 +822,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             sh.n[slot][lane] = cur.n;
             if (lane == 0) sh.kind[slot] = cur.staged ? 1u : 0u;
             const bool staged = cur.staged;
-            if (staged && MODE != 2) pk_issue<AUX, true>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
+            if (staged && MODE != 2) pk_issue<AUX, true, MODE == 3>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
             uint32_t kn = k + 1;
             while (!owned(kn)) kn++;
             const uint64_t tn = blockIdx.x + (uint64_t)kn * G;
@@ -875,7 +882,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);
             const uint32_t nfull = n >> 6;
-            if (MODE == 1) {
+            if (MODE == 1 || MODE == 3) {
 #pragma unroll
                 for (int q = 0; q < 16 * (int)kRegChunks; q++) h[q & 3] ^= R[q];
             } else {
@@ -912,7 +919,8 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
 // product knob can never select one; their "records" are meaningless):
 // 1 = staged memory only, 2 = staged hashing only, 3 = park memory only,
 // 4 = park hashing only, 5 = linear read with plain loads, 6 = linear read
-// with LDS DMA.
+// with LDS DMA, 7 = the same with every request 4 bytes off a 16-byte
+// boundary, 8 = park memory only with 16-byte aligned quad requests.
 constexpr int kParkLoaders = 3;  // 1 / 2 / 3 loaders measured
 static int g_variant = -2;  // -2 = not yet read from RSG_BLOCKSUMS_KERNEL
 static int g_diag = -2;     // -2 = not yet read from RSG_BLOCKSUMS_DIAG
@@ -968,6 +976,15 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             case 6:
                 hipLaunchKernelGGL(diag_linear_read<true>, dim3(2048), dim3(256), 0, stream, arena, arena_bytes,
                                    (uint32_t *)out);
+                break;
+            case 7:
+                hipLaunchKernelGGL((diag_linear_read<true, 4>), dim3(2048), dim3(256), 0, stream, arena, arena_bytes,
+                                   (uint32_t *)out);
+                break;
+            case 8:
+                if (max_blen <= kRegMaxBytes)
+                    hipLaunchKernelGGL((block_sums_park<3, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes,
+                                       files, wg_file, nwg, total_blocks, seed, out);
                 break;
         }
         return hipGetLastError();

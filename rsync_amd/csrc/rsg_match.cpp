@@ -27,6 +27,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "../../include/rsg_testing.h"
 #include "rsg_host.h"
 
 using namespace rsgh;
@@ -66,6 +67,7 @@ namespace {
 
 constexpr uint32_t kCandCap = 1u << 22;      // candidates per roll launch (32 MiB)
 constexpr uint64_t kSparseBatch = 1u << 16;  // windows per verification batch
+constexpr uint64_t kDenseBatch = 1u << 14;   // reach-set windows per dense round trip (Walker)
 
 // RSG_TIMING=1 prints the host-side phase times of each search to stderr.
 struct PhaseTimer {
@@ -232,58 +234,139 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
 }
 
 // Greedy walk over one range's sorted candidates (match.go:93-210 reduced to
-// the offsets where the weak sum can hit).
-rsg_status walk(Search &S, const std::vector<uint64_t> &C, uint64_t &pos, std::vector<int32_t> *known = nullptr) {
-    std::vector<int32_t> res = known ? std::move(*known) : std::vector<int32_t>(C.size(), -2);
-    size_t i = std::lower_bound(C.begin(), C.end(), pos) - C.begin();
-    std::vector<uint32_t> batch;
-    while (i < C.size()) {
-        const uint64_t c = C[i];
-        if ((int64_t)c >= S.end) break;
-        if (res[i] == -2) {
-            // Batch: every pending candidate ahead while they are sparse (the
-            // hashing they cost stays below twice the span they cover); in
-            // dense stretches (repetitive data) follow the chain of offsets the
-            // walk visits if each confirmation succeeds, plus the candidate
-            // after each one in case it fails.
-            batch.clear();
-            uint64_t hashed = 0;
-            size_t j = i;
-            for (; j < C.size() && batch.size() < kSparseBatch && (int64_t)C[j] < S.end; j++) {
-                if (res[j] == -2) {
-                    batch.push_back((uint32_t)j);
-                    hashed += S.window(C[j]);
-                }
-            }
-            const uint64_t span = (j > i ? C[j - 1] - c : 0) + (uint64_t)S.head.block_len;
-            if (hashed > 2 * span + (1u << 20)) {
+// the offsets where the weak sum can hit): visit offset C[i]; a match of
+// block b moves the walk to C[i] + Len_b (match.go:158 + the roll), a miss to
+// the next candidate.  Results come from `verify` (GPU confirmation) in
+// batches; res[i] = -2 until known.
+//
+// Batching (bounded GPU round trips):
+//  * sparse stretches (hashing every pending candidate costs at most twice
+//    the span they cover): the next kSparseBatch pending candidates at once;
+//  * dense stretches (repetitive data, where a match skips B candidates):
+//    (a) the chain of offsets the walk visits if every confirmation
+//    succeeds, plus one successor per step (exact on periodic data: 4096
+//    matches per round trip), and (b) the reach set: from the interval of
+//    positions the walk can be at, the candidates in it plus `width` more,
+//    step after step, up to kDenseBatch windows (robust when some of the
+//    chain's confirmations fail).  A round trip after which the walk
+//    visits no more than `width` candidates before needing another one
+//    means a run of failures longer than `width` (dense FALSE candidates:
+//    equal weak sums, different MD4): width grows x4 up to kSparseBatch, so
+//    such a stretch costs O(log) round trips to reach full batches instead
+//    of one round trip per ~2 candidates (round 3's d1 stall: ~240 000
+//    round trips of one 32 KiB MD4 chain each).
+//  * the sparse test scans up to kSparseBatch pending candidates; a dense
+//    verdict is remembered up to the last candidate it scanned, so a dense
+//    stretch does not rescan them every round trip.
+struct Walker {
+    int64_t end = 0;   // visited offsets are < end (match.go:70)
+    uint64_t size = 0;
+    rsg_sum_head head{};
+    std::function<rsg_status(const std::vector<uint32_t> &idx, std::vector<int32_t> &res)> verify;
+    std::vector<rsg_match> *out = nullptr;
+    uint64_t batches = 0, windows = 0;  // round trips, windows confirmed
+    uint64_t dense_until = 0;           // candidates below this offset were judged dense
+    uint32_t width = 2;                 // successors per chain step in a dense stretch
+
+    uint32_t window(uint64_t q) const { return (uint32_t)std::min<uint64_t>((uint64_t)head.block_len, size - q); }
+    int64_t len_of(int32_t i) const { return (i == head.count - 1 && head.rem != 0) ? head.rem : head.block_len; }
+
+    rsg_status run(const std::vector<uint64_t> &C, uint64_t &pos, std::vector<int32_t> *known) {
+        std::vector<int32_t> res = known ? std::move(*known) : std::vector<int32_t>(C.size(), -2);
+        size_t i = std::lower_bound(C.begin(), C.end(), pos) - C.begin();
+        std::vector<uint32_t> batch;
+        uint64_t consumed = 0;     // candidates visited since the last dense round trip
+        bool last_dense = false;   // the last round trip was a dense chain
+        while (i < C.size()) {
+            const uint64_t c = C[i];
+            if ((int64_t)c >= end) break;
+            if (res[i] == -2) {
                 batch.clear();
-                uint64_t x = c;
-                for (int n = 0; n < 4096; n++) {
-                    size_t a = std::lower_bound(C.begin() + i, C.end(), x) - C.begin();
-                    if (a >= C.size() || (int64_t)C[a] >= S.end) break;
-                    if (res[a] == -2) batch.push_back((uint32_t)a);
-                    if (a + 1 < C.size() && (int64_t)C[a + 1] < S.end && res[a + 1] == -2)
-                        batch.push_back((uint32_t)(a + 1));
-                    x = C[a] + S.window(C[a]);
+                bool dense = c < dense_until;
+                if (!dense) {
+                    uint64_t hashed = 0;
+                    size_t j = i;
+                    for (; j < C.size() && batch.size() < kSparseBatch && (int64_t)C[j] < end; j++) {
+                        if (res[j] == -2) {
+                            batch.push_back((uint32_t)j);
+                            hashed += window(C[j]);
+                        }
+                    }
+                    const uint64_t span = (j > i ? C[j - 1] - c : 0) + (uint64_t)head.block_len;
+                    if (hashed > 2 * span + (1u << 20)) {
+                        dense = true;
+                        dense_until = C[j - 1];
+                    } else {
+                        width = 2;  // a sparse stretch: the next dense one starts narrow again
+                    }
                 }
-                std::sort(batch.begin(), batch.end());
-                batch.erase(std::unique(batch.begin(), batch.end()), batch.end());
+                if (dense) {
+                    // a pure failure run longer than the successors pushed
+                    if (last_dense && consumed <= width)
+                        width = (uint32_t)std::min<uint64_t>(4ull * width, kSparseBatch);
+                    batch.clear();
+                    // (a) the chain of offsets visited if every confirmation
+                    // succeeds, plus one successor per step
+                    uint64_t x = c;
+                    for (int n = 0; n < 4096; n++) {
+                        size_t a = std::lower_bound(C.begin() + i, C.end(), x) - C.begin();
+                        if (a >= C.size() || (int64_t)C[a] >= end) break;
+                        if (res[a] == -2) batch.push_back((uint32_t)a);
+                        if (a + 1 < C.size() && (int64_t)C[a + 1] < end && res[a + 1] == -2)
+                            batch.push_back((uint32_t)(a + 1));
+                        x = C[a] + window(C[a]);
+                    }
+                    // (b) every offset the walk can reach: from the interval
+                    // of possible positions [lo, hi], the candidates in it plus
+                    // `width` after it; a success at any of them lands in the
+                    // next interval [C[a] + len, C[e - 1] + len]
+                    const size_t cap_b = batch.size() + std::max<uint64_t>(kDenseBatch, width);
+                    uint64_t lo = c, hi = c;
+                    for (int n = 0; n < 4096 && batch.size() < cap_b; n++) {
+                        const size_t a = std::lower_bound(C.begin() + i, C.end(), lo) - C.begin();
+                        if (a >= C.size() || (int64_t)C[a] >= end) break;
+                        size_t e = std::upper_bound(C.begin() + a, C.end(), hi) - C.begin();
+                        e = std::min<size_t>(std::max(e, a + 1) + (width - 1), C.size());
+                        e = std::min<size_t>(e, a + (cap_b - batch.size()));
+                        while (e > a + 1 && (int64_t)C[e - 1] >= end) e--;
+                        for (size_t b = a; b < e; b++)
+                            if (res[b] == -2) batch.push_back((uint32_t)b);
+                        lo = C[a] + window(C[a]);
+                        hi = C[e - 1] + window(C[e - 1]);
+                    }
+                    std::sort(batch.begin(), batch.end());
+                    batch.erase(std::unique(batch.begin(), batch.end()), batch.end());
+                }
+                last_dense = dense;
+                consumed = 0;
+                batches++;
+                windows += batch.size();
+                rsg_status s = verify(batch, res);
+                if (s != RSG_OK) return s;
             }
-            rsg_status s = verify(S, C, res, batch);
-            if (s != RSG_OK) return s;
+            consumed++;
+            const int32_t b = res[i];
+            if (b >= 0) {
+                out->push_back(rsg_match{(int64_t)c, b, 0});
+                pos = c + (uint64_t)len_of(b);  // match.go:158 + the roll
+                while (i < C.size() && C[i] < pos) i++;  // each candidate is stepped over once
+            } else {
+                pos = c + 1;
+                i++;
+            }
         }
-        const int32_t b = res[i];
-        if (b >= 0) {
-            S.out.push_back(rsg_match{(int64_t)c, b, 0});
-            pos = c + (uint64_t)S.len_of(b);  // match.go:158 + the roll
-            while (i < C.size() && C[i] < pos) i++;  // each candidate is stepped over once
-        } else {
-            pos = c + 1;
-            i++;
-        }
+        return RSG_OK;
     }
-    return RSG_OK;
+};
+
+rsg_status walk(Search &S, const std::vector<uint64_t> &C, uint64_t &pos, std::vector<int32_t> *known = nullptr) {
+    Walker w;
+    w.end = S.end;
+    w.size = S.size;
+    w.head = S.head;
+    w.out = &S.out;
+    w.verify = [&S, &C](const std::vector<uint32_t> &idx, std::vector<int32_t> &res) { return verify(S, C, res, idx); };
+    return w.run(C, pos, known);
 }
 
 rsg_status launch_range(Search &S, uint32_t lo, uint32_t hi);
@@ -927,6 +1010,38 @@ static rsg_status search_one(rsg_ctx *ctx, const void *src, uint64_t src_len, co
     const rsg_status s = search_batch(ctx, &j, 1, seed, host_src);
     *n_matches = j.n_matches;
     return s;
+}
+
+// Test hook (include/rsg_testing.h): the sender's greedy walk with the GPU
+// confirmation replaced by a table of answers, so its batching can be
+// checked on a machine without a GPU.
+rsg_status rsg_testing_walk(const uint64_t *cand, uint64_t n, const int32_t *truth, uint64_t size,
+                            const rsg_sum_head *head, rsg_match *out, uint64_t cap, uint64_t *n_out,
+                            uint64_t stats[2]) {
+    if (!head || !n_out || !stats || (n && (!cand || !truth))) return fail(nullptr, RSG_ERR_INVALID, "NULL argument");
+    std::vector<uint64_t> C(cand, cand + n);
+    for (uint64_t k = 1; k < n; k++)
+        if (C[k] <= C[k - 1]) return fail(nullptr, RSG_ERR_INVALID, "candidates must be strictly increasing");
+    std::vector<rsg_match> found;
+    Walker w;
+    const int64_t last_len = head->rem != 0 ? head->rem : head->block_len;
+    w.end = std::max<int64_t>((int64_t)size + 1 - last_len, 1);
+    w.size = size;
+    w.head = *head;
+    w.out = &found;
+    w.verify = [truth](const std::vector<uint32_t> &idx, std::vector<int32_t> &res) {
+        for (uint32_t k : idx) res[k] = truth[k];
+        return RSG_OK;
+    };
+    uint64_t pos = 0;
+    const rsg_status s = w.run(C, pos, nullptr);
+    if (s != RSG_OK) return s;
+    *n_out = found.size();
+    stats[0] = w.batches;
+    stats[1] = w.windows;
+    if (found.size() > cap) return fail(nullptr, RSG_ERR_TRUNCATED, "%llu matches", (unsigned long long)found.size());
+    if (!found.empty()) memcpy(out, found.data(), found.size() * sizeof(rsg_match));
+    return RSG_OK;
 }
 
 rsg_status rsg_hash_search_device(rsg_ctx *ctx, const void *d_src, uint64_t src_len, const rsg_sum_head *head,

@@ -1,5 +1,5 @@
 """CPU-side checks of the C-ABI library: it loads, exports every symbol
-include/rsg.h declares, and its host-only arithmetic (sizing, token encoding)
+include/*.h declare, and its host-only arithmetic (sizing, token encoding)
 matches the oracle.  No kernel is launched here."""
 import ctypes
 import os
@@ -15,9 +15,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _header_symbols():
-    txt = open(os.path.join(ROOT, "include", "rsg.h")).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(rsg_[a-z0-9_]+)\s*\(", txt)))
+    syms = set()
+    for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        if h.endswith(".h"):
+            txt = open(os.path.join(ROOT, "include", h)).read()
+            txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+            syms |= set(re.findall(r"\b(rsg_[a-z0-9_]+)\s*\(", txt))
+    return sorted(syms)
 
 
 def test_library_exports_every_header_symbol():
