@@ -67,3 +67,40 @@ func SumsStream(idx []int32, heads []rsync.SumHead, rec []byte, mux bool) ([]byt
 func (e *Engine) GenerateFiles(files []*os.File, idx []int32, sizes []int64, seed int32, w io.Writer, mux bool) error {
 	return ErrUnavailable
 }
+
+type RecvJob struct {
+	Stream []byte
+	Head   rsync.SumHead
+	Basis  []byte
+	Size   int64
+}
+
+func (e *Engine) ReceiveDataBatch(jobs []RecvJob, seed int32) ([][]byte, []error, error) {
+	return nil, nil, ErrUnavailable
+}
+
+type Piece struct {
+	File, B0, B1, Offset, Length, Record uint64
+	BlockLen                             int32
+	Rank, Batch                          int32
+}
+
+func ShardPlan(lengths []int64, blockLens []int32, world, nbatch int) ([]Piece, [][]uint64, error) {
+	return nil, nil, ErrUnavailable
+}
+
+type Node struct{ Engines []*Engine }
+
+func NewNode(devices []int) (*Node, error) { return nil, ErrUnavailable }
+
+func (nd *Node) Close() {}
+
+func (nd *Node) CommInit() error { return ErrUnavailable }
+
+func (nd *Node) BlockSums(files [][]byte, blockLen int32, seed int32) ([]rsync.SumHead, []byte, []uint64, error) {
+	return nil, nil, nil, ErrUnavailable
+}
+
+func (nd *Node) GenerateFiles(files []*os.File, idx []int32, sizes []int64, seed int32, w io.Writer, mux bool) error {
+	return ErrUnavailable
+}

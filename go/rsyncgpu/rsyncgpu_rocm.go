@@ -14,6 +14,9 @@
 //	HashSearch       hashSearch's byte loop, internal/sender/match.go:21-230
 //	HashSearchBatch  SendFiles' per-file hashSearch calls, internal/sender/sender.go:19-115
 //	ReceiveData      receiveData's token loop and whole-file check, internal/receiver/receiver.go:98-188
+//	ReceiveDataBatch RecvFiles' per-file receiveData calls, receiver.go:18-188 (the call to use for many files)
+//	ShardPlan        the block-range plan of a file list over a node's GPUs (SURVEY §8(e))
+//	Node             one process driving several GPUs: BlockSums / GenerateFiles sharded over them
 //	FileSums         rsyncchecksum.ReaderChecksum (rsyncchecksum.go:60-66), many files per call
 //	SumsStream       the per-block Conn writes of a batch, generator.go:317,341-346 (+ mux, wire.go:28-36)
 //
@@ -388,4 +391,227 @@ func (e *Engine) GenerateFiles(files []*os.File, idx []int32, sizes []int64, see
 		C.rsg_write_fn(C.rsgGoWrite), unsafe.Pointer(user), nil, &written)
 	runtime.KeepAlive(files)
 	return e.err(st)
+}
+
+// RecvJob is one file of RecvFiles' loop (receiver.go:18-188): the bytes
+// after its SumHead (tokens, int32 0, the 16-byte file sum) and its basis.
+type RecvJob struct {
+	Stream []byte
+	Head   rsync.SumHead
+	Basis  []byte // nil: no local file
+	Size   int64  // rebuilt size (the file list's length)
+}
+
+// ReceiveDataBatch replaces receiveData (receiver.go:98-188) for many files
+// at once (rsg_receive_data_batch): tokens applied on host threads, the
+// seeded whole-file MD4s of a whole batch hashed together on the GPU (one
+// lane per file) while the next batch's tokens are applied.  This is the call
+// to use for a transfer with many files; per-file errors (ErrCorrupt for a
+// sum mismatch) come back in errs.
+func (e *Engine) ReceiveDataBatch(jobs []RecvJob, seed int32) ([][]byte, []error, error) {
+	n := len(jobs)
+	if n == 0 {
+		return nil, nil, nil
+	}
+	cj := unsafe.Slice((*C.rsg_recv_job)(C.calloc(C.size_t(n), C.sizeof_rsg_recv_job)), n)
+	defer C.free(unsafe.Pointer(&cj[0]))
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	outs := make([][]byte, n)
+	for i, j := range jobs {
+		outs[i] = make([]byte, int(j.Size)+1)
+		pin.Pin(&outs[i][0])
+		cj[i].out, cj[i].out_cap = (*C.uint8_t)(unsafe.Pointer(&outs[i][0])), C.uint64_t(j.Size)
+		if len(j.Stream) > 0 {
+			pin.Pin(&j.Stream[0])
+			cj[i].tokens = (*C.uint8_t)(unsafe.Pointer(&j.Stream[0]))
+		}
+		cj[i].tokens_len = C.uint64_t(len(j.Stream))
+		if len(j.Basis) > 0 {
+			pin.Pin(&j.Basis[0])
+			cj[i].basis = (*C.uint8_t)(unsafe.Pointer(&j.Basis[0]))
+		}
+		cj[i].basis_len = C.uint64_t(len(j.Basis))
+		cj[i].head = cHead(j.Head)
+	}
+	st := C.rsg_receive_data_batch(e.ctx, &cj[0], C.uint64_t(n), C.int32_t(seed))
+	errs := make([]error, n)
+	for i := range cj {
+		switch cj[i].status {
+		case C.RSG_OK:
+			outs[i] = outs[i][:cj[i].out_len]
+		case C.RSG_ERR_CORRUPT:
+			errs[i], outs[i] = ErrCorrupt, nil
+		default:
+			errs[i], outs[i] = fmt.Errorf("rsg status %d", int(cj[i].status)), nil
+		}
+	}
+	if st != C.RSG_OK && st != C.RSG_ERR_INVALID && st != C.RSG_ERR_TRUNCATED && st != C.RSG_ERR_CORRUPT {
+		return outs, errs, e.err(st)
+	}
+	return outs, errs, nil
+}
+
+// Piece is one entry of a shard plan (rsg_shard_plan): blocks [B0, B1) of
+// file File, bytes [Offset, Offset+Length) of it, hashed by device Rank in
+// its batch Batch; Record = global record index of block B0.
+type Piece struct {
+	File, B0, B1, Offset, Length, Record uint64
+	BlockLen                             int32
+	Rank, Batch                          int32
+}
+
+// ShardPlan cuts a file list's global block sequence into world contiguous,
+// byte-balanced ranges and each into nbatch batches (block boundaries only).
+// blockLens nil: SumSizesSqroot for every file.  records[q][b] = records of
+// rank q's batch b.
+func ShardPlan(lengths []int64, blockLens []int32, world, nbatch int) ([]Piece, [][]uint64, error) {
+	n := len(lengths)
+	ln := make([]C.uint64_t, n+1)
+	for i, l := range lengths {
+		ln[i] = C.uint64_t(l)
+	}
+	var bl *C.int32_t
+	if blockLens != nil {
+		bl = (*C.int32_t)(unsafe.Pointer(&blockLens[0]))
+	}
+	recs := make([]uint64, world*nbatch+1)
+	var np C.uint64_t
+	st := C.rsg_shard_plan(&ln[0], bl, C.uint64_t(n), 0, C.int32_t(world), C.int32_t(nbatch), nil, 0, &np,
+		(*C.uint64_t)(unsafe.Pointer(&recs[0])))
+	if st != C.RSG_OK && st != C.RSG_ERR_TRUNCATED {
+		return nil, nil, hostErr(st)
+	}
+	ps := make([]C.rsg_piece, int(np)+1)
+	if st := C.rsg_shard_plan(&ln[0], bl, C.uint64_t(n), 0, C.int32_t(world), C.int32_t(nbatch), &ps[0], np, &np,
+		(*C.uint64_t)(unsafe.Pointer(&recs[0]))); st != C.RSG_OK {
+		return nil, nil, hostErr(st)
+	}
+	out := make([]Piece, int(np))
+	for i := range out {
+		p := ps[i]
+		out[i] = Piece{File: uint64(p.file), B0: uint64(p.b0), B1: uint64(p.b1), Offset: uint64(p.offset),
+			Length: uint64(p.length), Record: uint64(p.record), BlockLen: int32(p.block_len), Rank: int32(p.rank),
+			Batch: int32(p.batch)}
+	}
+	perRank := make([][]uint64, world)
+	for q := range perRank {
+		perRank[q] = recs[q*nbatch : (q+1)*nbatch]
+	}
+	return out, perRank, nil
+}
+
+// Node is one process driving several GPUs, the shape of gokr-rsync's
+// receiver (one generator goroutine, receiver/do.go:96-98): one Engine per
+// device, called from the goroutine that owns the Node.  The file list's
+// global block sequence is sharded over the devices; outputs are the
+// single-device bytes.
+type Node struct {
+	Engines []*Engine
+	ctxs    **C.rsg_ctx // C array of the engines' contexts
+}
+
+// NewNode opens one engine per device ordinal.
+func NewNode(devices []int) (*Node, error) {
+	nd := &Node{}
+	for _, d := range devices {
+		e, err := New(d)
+		if err != nil {
+			nd.Close()
+			return nil, err
+		}
+		nd.Engines = append(nd.Engines, e)
+	}
+	arr := unsafe.Slice((**C.rsg_ctx)(C.calloc(C.size_t(len(devices)+1), C.size_t(unsafe.Sizeof(uintptr(0))))),
+		len(devices)+1)
+	for i, e := range nd.Engines {
+		arr[i] = e.ctx
+	}
+	nd.ctxs = &arr[0]
+	return nd, nil
+}
+
+func (nd *Node) Close() {
+	for _, e := range nd.Engines {
+		e.Close()
+	}
+	if nd.ctxs != nil {
+		C.free(unsafe.Pointer(nd.ctxs))
+		nd.ctxs = nil
+	}
+	nd.Engines = nil
+}
+
+func (nd *Node) err(st C.rsg_status) error { return nd.Engines[0].err(st) }
+
+// CommInit builds the RCCL communicator over the node's devices
+// (ncclCommInitAll; engine q = rank q) for the device-resident gather.
+func (nd *Node) CommInit() error {
+	return nd.err(C.rsg_comm_init_all(nd.ctxs, C.int32_t(len(nd.Engines))))
+}
+
+// BlockSums is Engine.BlockSums with the file list sharded over the node's
+// devices (rsg_block_sums_host_multi): same heads, records and first indices.
+func (nd *Node) BlockSums(files [][]byte, blockLen int32, seed int32) ([]rsync.SumHead, []byte, []uint64, error) {
+	n := len(files)
+	if n == 0 {
+		return nil, nil, nil, nil
+	}
+	desc := unsafe.Slice((*C.rsg_file)(C.calloc(C.size_t(n), C.sizeof_rsg_file)), n)
+	defer C.free(unsafe.Pointer(&desc[0]))
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	for i, f := range files {
+		desc[i].len = C.uint64_t(len(f))
+		desc[i].block_len = C.int32_t(blockLen)
+		if len(f) > 0 {
+			pin.Pin(&f[0])
+			desc[i].data = (*C.uint8_t)(unsafe.Pointer(&f[0]))
+		}
+	}
+	heads := make([]C.rsg_sum_head, n)
+	first := make([]uint64, n)
+	var total C.uint64_t
+	if st := C.rsg_plan_block_sums(&desc[0], C.uint64_t(n), &heads[0],
+		(*C.uint64_t)(unsafe.Pointer(&first[0])), &total); st != C.RSG_OK {
+		return nil, nil, nil, hostErr(st)
+	}
+	rec := make([]byte, int(total)*C.RSG_RECORD_BYTES+1)
+	if st := C.rsg_block_sums_host_multi(nd.ctxs, C.int32_t(len(nd.Engines)), &desc[0], C.uint64_t(n),
+		C.int32_t(seed), bytePtr(rec), total); st != C.RSG_OK {
+		return nil, nil, nil, nd.err(st)
+	}
+	out := make([]rsync.SumHead, n)
+	for i, h := range heads {
+		out[i] = goHead(h)
+	}
+	return out, rec[:int(total)*C.RSG_RECORD_BYTES], first, nil
+}
+
+// GenerateFiles is Engine.GenerateFiles with every device reading and
+// hashing its byte-balanced range of the file list
+// (rsg_generate_files_fd_multi); w receives the same stream, written from
+// this goroutine's thread in file-list order (generator.go:20-52).
+func (nd *Node) GenerateFiles(files []*os.File, idx []int32, sizes []int64, seed int32, w io.Writer, mux bool) error {
+	if len(files) == 0 {
+		return nil
+	}
+	desc := make([]C.rsg_fd_file, len(files))
+	for i, f := range files {
+		desc[i] = C.rsg_fd_file{fd: C.int32_t(f.Fd()), idx: C.int32_t(idx[i]), len: C.uint64_t(sizes[i])}
+	}
+	flags := C.int32_t(C.RSG_GEN_IDX | C.RSG_GEN_TERMINATE)
+	if mux {
+		flags |= C.RSG_GEN_MUX
+	}
+	h := cgo.NewHandle(w)
+	defer h.Delete()
+	user := (*cgo.Handle)(C.malloc(C.size_t(unsafe.Sizeof(h))))
+	defer C.free(unsafe.Pointer(user))
+	*user = h
+	var written C.uint64_t
+	st := C.rsg_generate_files_fd_multi(nd.ctxs, C.int32_t(len(nd.Engines)), &desc[0], C.uint64_t(len(desc)),
+		C.int32_t(seed), flags, C.rsg_write_fn(C.rsgGoWrite), unsafe.Pointer(user), nil, &written)
+	runtime.KeepAlive(files)
+	return nd.err(st)
 }

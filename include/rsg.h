@@ -406,6 +406,85 @@ rsg_status rsg_block_sums_gather(rsg_ctx *ctx, const rsg_shard_batch *batches, u
 rsg_status rsg_block_sums_d2h(rsg_ctx *ctx, const rsg_shard_batch *batches, uint64_t nbatch,
                               const void *d_arena, int32_t seed, void *d_records, uint8_t *h_records);
 
+/* ------------------------------------------ one process, many GPUs
+ * gokr-rsync is ONE process whose generator is one goroutine
+ * (internal/receiver/do.go:96-98, generator.go:20-52): the drop-in for a node
+ * of N GPUs is that process driving N contexts (one per device) from the
+ * calling thread.  The file list's global block sequence is cut into N
+ * contiguous, byte-balanced ranges on block boundaries (rank q takes range
+ * q), each range again into nbatch batches; records of rank q land at
+ * rank_offset[q] of the global record stream, so their concatenation is the
+ * single-GPU (and the reference's) record order.  The same plan is what the
+ * multi-process bench uses (rsync_amd/dist.py restates it for the tests).
+ * Multi-context calls report failures in rsg_last_error(ctxs[0]). */
+
+/* One piece of a shard plan: blocks [b0, b1) of file `file` (bytes
+ * [offset, offset + length) of it; the last block may be the file's
+ * remainder), in rank `rank`'s batch `batch`; `record` = global record index
+ * of block b0. */
+typedef struct rsg_piece {
+    uint64_t file;
+    uint64_t b0, b1;
+    uint64_t offset, length;
+    uint64_t record;
+    int32_t block_len;
+    int32_t rank;
+    int32_t batch;
+    int32_t reserved;
+} rsg_piece;
+/* Host arithmetic.  lengths[nfiles]; block_lens[nfiles] (NULL: every file
+ * block_len; 0 = SumSizesSqroot).  Pieces in global order (= rank, batch
+ * order); pieces == NULL or cap too small: RSG_ERR_TRUNCATED with *n_pieces
+ * set.  records (may be NULL): world * nbatch counts, records[q * nbatch + b]
+ * = records of rank q's batch b. */
+rsg_status rsg_shard_plan(const uint64_t *lengths, const int32_t *block_lens, uint64_t nfiles, int32_t block_len,
+                          int32_t world, int32_t nbatch, rsg_piece *pieces, uint64_t cap, uint64_t *n_pieces,
+                          uint64_t *records);
+
+/* RCCL communicator over the devices of n contexts in this process
+ * (ncclCommInitAll): ctxs[q] becomes rank q.  Distinct devices only. */
+rsg_status rsg_comm_init_all(rsg_ctx *const *ctxs, int32_t n);
+
+/* Device-resident sharded step over n contexts from one thread: rank q's
+ * batches (ranks[q].batches, plans of ctxs[q] over ranks[q].d_arena, records
+ * into ranks[q].d_records at each batch's record_offset), batch b's kernels on
+ * every device, then its records delivered while batch b+1 hashes:
+ *   rsg_block_sums_gather_multi: to ranks[root]'s device at d_recv over RCCL
+ *     (rsg_comm_init_all first), landing at the batches' recv_offsets;
+ *   rsg_block_sums_d2h_multi: every device's records to h_records + 20 *
+ *     (rank_record_offset + record_offset) over its own PCIe link.
+ * Every rank has the same nbatch.  Synchronous. */
+typedef struct rsg_shard_rank {
+    rsg_ctx *ctx;
+    const void *d_arena;
+    void *d_records;
+    const rsg_shard_batch *batches;
+    uint64_t nbatch;
+    uint64_t rank_record_offset;  /* d2h: first global record of this rank */
+} rsg_shard_rank;
+rsg_status rsg_block_sums_gather_multi(const rsg_shard_rank *ranks, int32_t n, int32_t seed, void *d_recv,
+                                       int32_t root);
+rsg_status rsg_block_sums_d2h_multi(const rsg_shard_rank *ranks, int32_t n, int32_t seed, uint8_t *h_records);
+
+/* Host buffers in, host records out, over n contexts: rsg_block_sums_host's
+ * contract for the whole file list, the global block sequence sharded over
+ * the contexts' devices (rsg_shard_plan, one batch per rank), every rank's
+ * share staged and hashed on its own device concurrently and its records
+ * written straight into `records` at its global offset. */
+rsg_status rsg_block_sums_host_multi(rsg_ctx *const *ctxs, int32_t n, const rsg_file *files, uint64_t nfiles,
+                                     int32_t seed, uint8_t *records, uint64_t records_cap);
+
+/* rsg_generate_files_fd over n contexts: the same stream (idx, SumHead,
+ * records, phase markers; MsgData framing with RSG_GEN_MUX) in file-list
+ * order, written on the calling thread, while every rank reads and hashes
+ * its contiguous byte-balanced range of the global block sequence (files may
+ * be split between ranks on block boundaries) on its own device.  The
+ * demuxed bytes equal the single-context call's.  Rank q's records are
+ * buffered in host memory until ranks < q have been written. */
+rsg_status rsg_generate_files_fd_multi(rsg_ctx *const *ctxs, int32_t n, const rsg_fd_file *files, uint64_t nfiles,
+                                       int32_t seed, int32_t flags, rsg_write_fn write, void *user,
+                                       rsg_sum_head *heads_out, uint64_t *bytes_written);
+
 /* ------------------------------------------ wire formats
  * Host byte formatting around the checksum path, so the engine's records
  * leave wire-ready.  No GPU work; re-entrant.  Outputs follow the

@@ -88,6 +88,21 @@ class ShardBatch(ctypes.Structure):
                 ("send_bytes", ctypes.POINTER(ctypes.c_uint64)), ("recv_offsets", ctypes.POINTER(ctypes.c_uint64))]
 
 
+class Piece(ctypes.Structure):
+    """rsg_piece: blocks [b0, b1) of a file in rank `rank`'s batch `batch` (rsg_shard_plan)."""
+    _fields_ = [("file", ctypes.c_uint64), ("b0", ctypes.c_uint64), ("b1", ctypes.c_uint64),
+                ("offset", ctypes.c_uint64), ("length", ctypes.c_uint64), ("record", ctypes.c_uint64),
+                ("block_len", ctypes.c_int32), ("rank", ctypes.c_int32), ("batch", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+class ShardRank(ctypes.Structure):
+    """rsg_shard_rank: one context's side of rsg_block_sums_{gather,d2h}_multi."""
+    _fields_ = [("ctx", ctypes.c_void_p), ("d_arena", ctypes.c_void_p), ("d_records", ctypes.c_void_p),
+                ("batches", ctypes.POINTER(ShardBatch)), ("nbatch", ctypes.c_uint64),
+                ("rank_record_offset", ctypes.c_uint64)]
+
+
 # rsg_write_fn: int32 (*)(void *user, const uint8_t *data, uint64_t len)
 WRITE_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
 
@@ -148,6 +163,14 @@ _PROTOS = {
     "rsg_gatherv_bytes": (_st, [_vp, _vp, ctypes.POINTER(_u64), _vp, ctypes.POINTER(_u64), _i32, _vp]),
     "rsg_block_sums_gather": (_st, [_vp, ctypes.POINTER(ShardBatch), _u64, _vp, _i32, _vp, _vp, _i32]),
     "rsg_block_sums_d2h": (_st, [_vp, ctypes.POINTER(ShardBatch), _u64, _vp, _i32, _vp, _vp]),
+    "rsg_shard_plan": (_st, [_vp, _vp, _u64, _i32, _i32, _i32, ctypes.POINTER(Piece), _u64, ctypes.POINTER(_u64),
+                             _vp]),
+    "rsg_comm_init_all": (_st, [ctypes.POINTER(_vp), _i32]),
+    "rsg_block_sums_gather_multi": (_st, [ctypes.POINTER(ShardRank), _i32, _i32, _vp, _i32]),
+    "rsg_block_sums_d2h_multi": (_st, [ctypes.POINTER(ShardRank), _i32, _i32, _vp]),
+    "rsg_block_sums_host_multi": (_st, [ctypes.POINTER(_vp), _i32, ctypes.POINTER(File), _u64, _i32, _vp, _u64]),
+    "rsg_generate_files_fd_multi": (_st, [ctypes.POINTER(_vp), _i32, ctypes.POINTER(FdFile), _u64, _i32, _i32,
+                                          WRITE_FN, _vp, ctypes.POINTER(SumHead), ctypes.POINTER(_u64)]),
     "rsg_check_sum_head": (_st, [ctypes.POINTER(SumHead)]),
     "rsg_encode_sums": (_st, [_vp, ctypes.POINTER(SumHead), _u64, _vp, _i32, _vp, _u64, ctypes.POINTER(_u64)]),
     "rsg_decode_sums": (_st, [_vp, _u64, ctypes.POINTER(SumHead), _vp, _vp, _u64, ctypes.POINTER(_u64)]),

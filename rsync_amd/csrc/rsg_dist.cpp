@@ -19,7 +19,7 @@
 
 using namespace rsgh;
 
-namespace {
+namespace rsgh {
 
 // Root receives send_bytes[q] bytes from every rank q at recv_off[q] (or the
 // exclusive prefix of send_bytes when recv_off is NULL); grouped
@@ -52,6 +52,10 @@ rsg_status gatherv(rsg_ctx *ctx, const void *d_send, const uint64_t *send_bytes,
         return fail(ctx, RSG_ERR_HIP, "rccl gather: %s", ncclGetErrorString(r != ncclSuccess ? r : r2));
     return RSG_OK;
 }
+
+}  // namespace rsgh
+
+namespace {
 
 struct Events {  // one per batch, destroyed on every exit
     std::vector<hipEvent_t> ev;

@@ -160,11 +160,15 @@ struct Emitter {
 
 }  // namespace
 
-extern "C" {
+namespace rsgh {
 
-rsg_status rsg_generate_files_fd(rsg_ctx *ctx, const rsg_fd_file *files, uint64_t nfiles, int32_t seed,
-                                 int32_t flags, rsg_write_fn write, void *user, rsg_sum_head *heads_out,
-                                 uint64_t *bytes_written) {
+// records_only: the stream carries only the 20-byte records of the files'
+// blocks (no idx, SumHead, phase markers or framing): the per-rank part of
+// rsg_generate_files_fd_multi (rsg_shard.cpp), whose caller thread puts the
+// heads between the ranks' records.
+rsg_status generate_files_fd_impl(rsg_ctx *ctx, const rsg_fd_file *files, uint64_t nfiles, int32_t seed,
+                                  int32_t flags, rsg_write_fn write, void *user, rsg_sum_head *heads_out,
+                                  uint64_t *bytes_written, bool records_only) {
     if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
     std::lock_guard<std::recursive_mutex> lock(ctx->mu);
     RSG_HIP(ctx, hipSetDevice(ctx->device));
@@ -181,6 +185,7 @@ rsg_status rsg_generate_files_fd(rsg_ctx *ctx, const rsg_fd_file *files, uint64_
     if (!write || (nfiles && !files)) return fail(ctx, RSG_ERR_INVALID, "NULL argument");
     if (flags & ~(RSG_GEN_IDX | RSG_GEN_TERMINATE | RSG_GEN_MUX))
         return fail(ctx, RSG_ERR_INVALID, "unknown flags 0x%x", flags);
+    if (records_only) flags = 0;
     std::vector<rsg_sum_head> heads(nfiles);
     for (uint64_t i = 0; i < nfiles; i++) {
         if (files[i].len > (uint64_t)INT64_MAX || files[i].offset < 0)
@@ -238,6 +243,7 @@ rsg_status rsg_generate_files_fd(rsg_ctx *ctx, const rsg_fd_file *files, uint64_
     Emitter em{write, user, (flags & RSG_GEN_MUX) != 0};
     uint64_t next_head = 0;  // first file whose idx + SumHead are not out yet
     auto emit_heads_through = [&](uint64_t f) {
+        if (records_only) return;
         for (; next_head <= f && next_head < nfiles; next_head++) {
             const rsg_sum_head &h = heads[next_head];
             if (flags & RSG_GEN_IDX) em.i32(files[next_head].idx);  // generator.go:317
@@ -323,6 +329,16 @@ rsg_status rsg_generate_files_fd(rsg_ctx *ctx, const rsg_fd_file *files, uint64_
     if ((s = em.flush(ctx)) != RSG_OK) return s;
     if (bytes_written) *bytes_written = em.written;
     return RSG_OK;
+}
+
+}  // namespace rsgh
+
+extern "C" {
+
+rsg_status rsg_generate_files_fd(rsg_ctx *ctx, const rsg_fd_file *files, uint64_t nfiles, int32_t seed,
+                                 int32_t flags, rsg_write_fn write, void *user, rsg_sum_head *heads_out,
+                                 uint64_t *bytes_written) {
+    return generate_files_fd_impl(ctx, files, nfiles, seed, flags, write, user, heads_out, bytes_written, false);
 }
 
 }  // extern "C"

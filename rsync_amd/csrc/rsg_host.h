@@ -138,6 +138,18 @@ rsg_status launch_file_sums_async(rsg_ctx *ctx, const void *d_arena, uint64_t ar
                                   const std::vector<rsg::FileSpan> &spans, int32_t mode, int32_t seed, void *d_out,
                                   int slot, hipStream_t stream);
 
+// The generator's host loop (rsg_generate.cpp); records_only = only the
+// 20-byte records in the stream (the per-rank part of the multi-GPU call).
+rsg_status generate_files_fd_impl(rsg_ctx *ctx, const rsg_fd_file *files, uint64_t nfiles, int32_t seed,
+                                  int32_t flags, rsg_write_fn write, void *user, rsg_sum_head *heads_out,
+                                  uint64_t *bytes_written, bool records_only);
+
+// Ragged RCCL gather of one rank's bytes to the root (rsg_dist.cpp): root
+// receives send_bytes[q] from rank q at recv_off[q] (NULL: exclusive prefix).
+// Grouped sends/receives; may be nested inside the caller's ncclGroupStart.
+rsg_status gatherv(rsg_ctx *ctx, const void *d_send, const uint64_t *send_bytes, void *d_recv,
+                   const uint64_t *recv_off, int32_t root, hipStream_t st);
+
 // Kernel timing helpers (no-ops unless ctx->timing): begin records an event
 // on `stream` and returns it; end records the closing event.
 hipEvent_t timed_begin(rsg_ctx *ctx, hipStream_t stream);

@@ -88,6 +88,26 @@ PIN(rsg_recv_job, consumed, 72);
 PIN(rsg_recv_job, status, 80);
 PIN(rsg_recv_job, reserved, 84);
 
+SIZE(rsg_piece, 64);
+PIN(rsg_piece, file, 0);
+PIN(rsg_piece, b0, 8);
+PIN(rsg_piece, b1, 16);
+PIN(rsg_piece, offset, 24);
+PIN(rsg_piece, length, 32);
+PIN(rsg_piece, record, 40);
+PIN(rsg_piece, block_len, 48);
+PIN(rsg_piece, rank, 52);
+PIN(rsg_piece, batch, 56);
+PIN(rsg_piece, reserved, 60);
+
+SIZE(rsg_shard_rank, 48);
+PIN(rsg_shard_rank, ctx, 0);
+PIN(rsg_shard_rank, d_arena, 8);
+PIN(rsg_shard_rank, d_records, 16);
+PIN(rsg_shard_rank, batches, 24);
+PIN(rsg_shard_rank, nbatch, 32);
+PIN(rsg_shard_rank, rank_record_offset, 40);
+
 #define F(T, M) printf("\"%s\": [%zu, %zu]", #M, offsetof(T, M), sizeof(((T *)0)->M))
 
 static void layout(void) {
@@ -121,6 +141,17 @@ static void layout(void) {
     F(rsg_recv_job, out); printf(", "); F(rsg_recv_job, out_cap); printf(", "); F(rsg_recv_job, out_len);
     printf(", "); F(rsg_recv_job, consumed); printf(", "); F(rsg_recv_job, status); printf(", ");
     F(rsg_recv_job, reserved);
+    printf("},\n");
+    printf(" \"rsg_piece\": {\"size\": %zu, ", sizeof(rsg_piece));
+    F(rsg_piece, file); printf(", "); F(rsg_piece, b0); printf(", "); F(rsg_piece, b1); printf(", ");
+    F(rsg_piece, offset); printf(", "); F(rsg_piece, length); printf(", "); F(rsg_piece, record); printf(", ");
+    F(rsg_piece, block_len); printf(", "); F(rsg_piece, rank); printf(", "); F(rsg_piece, batch); printf(", ");
+    F(rsg_piece, reserved);
+    printf("},\n");
+    printf(" \"rsg_shard_rank\": {\"size\": %zu, ", sizeof(rsg_shard_rank));
+    F(rsg_shard_rank, ctx); printf(", "); F(rsg_shard_rank, d_arena); printf(", "); F(rsg_shard_rank, d_records);
+    printf(", "); F(rsg_shard_rank, batches); printf(", "); F(rsg_shard_rank, nbatch); printf(", ");
+    F(rsg_shard_rank, rank_record_offset);
     printf("}}\n");
 }
 
