@@ -247,6 +247,23 @@ rsg_status rsg_hash_search_device(rsg_ctx *ctx, const void *d_src, uint64_t src_
                                   const uint8_t *sum2, const int32_t *targets, int32_t seed,
                                   rsg_match *matches, uint64_t match_cap, uint64_t *n_matches);
 
+/* Same, with the source read from a file by the engine (row a13: the
+ * sender's mapFile / ptr window, internal/sender/fileio.go:31-112): bytes
+ * [offset, offset + src_len) of fd (src_len = the stat'ed size, as
+ * sendFile's fi.Size()) are read with pread in windows of
+ * RSG_SEARCH_WINDOW_KB (default 256 MiB; at least 2 B), each uploaded with a
+ * B-1 byte halo and searched while the next window is read, so host and HBM
+ * use stay bounded by two windows whatever the file size.  A file shorter
+ * than src_len (or a read error) is RSG_ERR_IO "file has changed
+ * mid-transfer" (fileio.go:99-104).  file_sum != NULL also receives the
+ * transfer's whole-file sum MD4(int32_LE(seed) || source) (match.go:52-53,
+ * 220-226), computed on a host thread over the same staged bytes (one
+ * serial chain per file).  head->count == 0 (sendFile, sender.go:86-88) or
+ * an empty source searches nothing and only reads the file for file_sum. */
+rsg_status rsg_hash_search_fd(rsg_ctx *ctx, int32_t fd, int64_t offset, uint64_t src_len, const rsg_sum_head *head,
+                              const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets, int32_t seed,
+                              rsg_match *matches, uint64_t match_cap, uint64_t *n_matches, uint8_t file_sum[16]);
+
 /* Batched search over the files of a transfer: replaces SendFiles' per-file
  * loop (sender.go:19-115) once their sums have been read, i.e. one
  * hashSearch (sender.go:90) per job, in job order.  Jobs are pipelined: job

@@ -22,6 +22,15 @@ rsg_status rsg_testing_walk(const uint64_t *cand, uint64_t n, const int32_t *tru
                             const rsg_sum_head *head, rsg_match *out, uint64_t cap, uint64_t *n_out,
                             uint64_t stats[2]);
 
+/* The product's host MD4 (RFC 1320; rsync_amd/csrc/rsg_md4_host.cpp), used
+ * for whole-file sums whose bytes stream through host memory: the sender's
+ * MD4(int32_LE(seed) || source) in rsg_hash_search_fd and receiveData's
+ * check of large files.  seeded != 0 prefixes int32_LE(seed) (match.go:52-53).
+ * The data is hashed in `piece`-byte updates (0 = one update) to exercise
+ * the streaming path. */
+rsg_status rsg_testing_md4(const uint8_t *data, uint64_t n, int32_t seeded, int32_t seed, uint64_t piece,
+                           uint8_t out[16]);
+
 #ifdef __cplusplus
 }
 #endif

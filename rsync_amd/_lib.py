@@ -144,6 +144,8 @@ _PROTOS = {
                                    ctypes.POINTER(Match), _u64, ctypes.POINTER(_u64)]),
     "rsg_hash_search_device": (_st, [_vp, _vp, _u64, ctypes.POINTER(SumHead), _vp, _vp, _vp, _i32,
                                      ctypes.POINTER(Match), _u64, ctypes.POINTER(_u64)]),
+    "rsg_hash_search_fd": (_st, [_vp, _i32, ctypes.c_int64, _u64, ctypes.POINTER(SumHead), _vp, _vp, _vp, _i32,
+                                 ctypes.POINTER(Match), _u64, ctypes.POINTER(_u64), _vp]),
     "rsg_hash_search_batch_device": (_st, [_vp, ctypes.POINTER(SearchJob), _u64, _i32]),
     "rsg_hash_search_batch_host": (_st, [_vp, ctypes.POINTER(SearchJob), _u64, _i32]),
     "rsg_set_kernel_timing": (_st, [_vp, _i32]),
@@ -181,6 +183,7 @@ _PROTOS = {
     # include/rsg_testing.h (test hooks, not part of the drop-in boundary)
     "rsg_testing_walk": (_st, [_vp, _u64, _vp, _u64, ctypes.POINTER(SumHead), ctypes.POINTER(Match), _u64,
                                ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
+    "rsg_testing_md4": (_st, [_vp, _u64, _i32, _i32, _u64, _vp]),
 }
 
 for _name, (_res, _args) in _PROTOS.items():

@@ -150,6 +150,19 @@ rsg_status generate_files_fd_impl(rsg_ctx *ctx, const rsg_fd_file *files, uint64
 rsg_status gatherv(rsg_ctx *ctx, const void *d_send, const uint64_t *send_bytes, void *d_recv,
                    const uint64_t *recv_off, int32_t root, hipStream_t st);
 
+// MD4 on the host (rsg_md4_host.cpp): whole-file sums whose serial chain
+// streams through host memory (the sender's h, match.go:52-53; receiveData's
+// check of large files).  Not used for block checksums.
+struct Md4 {
+    uint32_t st[4];
+    uint64_t total;
+    uint8_t buf[64];
+    uint32_t nbuf;
+    void init();
+    void update(const uint8_t *p, uint64_t n);
+    void final(uint8_t out[16]);
+};
+
 // Kernel timing helpers (no-ops unless ctx->timing): begin records an event
 // on `stream` and returns it; end records the closing event.
 hipEvent_t timed_begin(rsg_ctx *ctx, hipStream_t stream);

@@ -13,17 +13,21 @@
 // Sum1_i == weak(q), Len_i == min(B, size - q) and MD4(window || seed)[:s2len]
 // == Sum2_i[:s2len] (match.go:108-136); after a match the next visited offset
 // is q + Len_i (match.go:158), otherwise q + 1.
+#include <errno.h>
 #include <stdio.h>
+#include <unistd.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <climits>
 #include <functional>
 #include <future>
 #include <memory>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -116,6 +120,8 @@ struct Search {
     uint32_t confirm_lds = 0;  // dynamic LDS of the confirmation kernel's workgroups
     bool fused = false;  // roll derives its window sums itself (B <= kFusedMaxB)
     bool pending = false;  // prepare() launched the roll of [0, tile_end) and its count read-back
+    uint64_t pos0 = 0;     // the walk's first position (a window of rsg_hash_search_fd: carried over)
+    uint64_t pos_end = 0;  // its position when finish() (or the tail) is done
 
     int64_t len_of(int32_t i) const {
         return (i == head.count - 1 && head.rem != 0) ? head.rem : head.block_len;  // sender.go:135-139
@@ -638,12 +644,16 @@ rsg_status finish(Search &S) {
     rsg_ctx *ctx = S.ctx;
     SearchSlot &sl = *S.sl;
     uint32_t lo = 0, span = S.tile_end;
-    uint64_t pos = 0;
+    uint64_t pos = S.pos0;
     std::vector<uint64_t> C;
     rsg_status s;
     while (lo < S.tile_end) {
         const uint32_t hi = std::min(S.tile_end, lo + span);
         if ((uint64_t)hi * kScanTile <= pos) {  // the walk already jumped past this range
+            if (S.pending) {  // its roll was launched: nothing may outlive the search
+                RSG_HIP(ctx, hipEventSynchronize(sl.rolled));
+                S.pending = false;
+            }
             lo = hi;
             continue;
         }
@@ -676,7 +686,9 @@ rsg_status finish(Search &S) {
                 const uint64_t p0 = pos;
                 S.tail = [Sp, key, p0]() {
                     uint64_t p = p0;
-                    return confirm_all_tail(*Sp, *key, p);
+                    const rsg_status st = confirm_all_tail(*Sp, *key, p);
+                    Sp->pos_end = p;
+                    return st;
                 };
                 break;
             }
@@ -695,6 +707,7 @@ rsg_status finish(Search &S) {
         S.pt.mark("walk");
         lo = hi;
     }
+    S.pos_end = pos;
     if ((s = run_hook(S, true)) != RSG_OK) return s;
     return RSG_OK;
 }
@@ -938,6 +951,179 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
     return first;
 }
 
+// ---------------------------------------------------------------- streaming sender (§8 a13)
+// io.ReadFull-style pread of [off, off + n) on a few threads; -1 = EOF
+// before n bytes, else 0 or an errno.
+int pread_full(int fd, int64_t off, uint8_t *dst, uint64_t n) {
+    const uint64_t piece = 4ull << 20;
+    const uint64_t npieces = (n + piece - 1) / piece;
+    const int nt = (int)std::min<uint64_t>(8, std::max<uint64_t>(1, npieces));
+    std::atomic<uint64_t> next{0};
+    std::atomic<int> bad{0};
+    auto worker = [&] {
+        for (uint64_t k; (k = next.fetch_add(1)) < npieces && bad.load() == 0;) {
+            uint64_t o = k * piece, m = std::min(piece, n - o);
+            while (m) {
+                const ssize_t r = pread(fd, dst + o, (size_t)m, (off_t)(off + (int64_t)o));
+                if (r < 0 && errno == EINTR) continue;
+                if (r <= 0) {
+                    int expected = 0;
+                    bad.compare_exchange_strong(expected, r < 0 ? errno : -1);
+                    return;
+                }
+                o += (uint64_t)r;
+                m -= (uint64_t)r;
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; t++) pool.emplace_back(worker);
+    worker();
+    for (auto &t : pool) t.join();
+    return bad.load();
+}
+
+// Window of the streamed source: RSG_SEARCH_WINDOW_KB (default 256 MiB),
+// whole scan tiles, at least 2 B.
+uint64_t search_window_bytes(uint32_t B) {
+    const char *e = getenv("RSG_SEARCH_WINDOW_KB");
+    uint64_t w = (e ? (uint64_t)std::max(1L, atol(e)) : 256ull * 1024) << 10;
+    w = std::max<uint64_t>(w, 2ull * B);
+    return (w + kScanTile - 1) / kScanTile * kScanTile;
+}
+
+// hashSearch over a file read in windows (fileio.go:31-112 mapFile/ptr; the
+// reference's window is max(3B, 256 KiB), match.go:34-35): window k holds
+// bytes [kW, (k+1)W + B - 1) of the source in HBM and yields the walk over
+// the offsets [kW, (k+1)W); the walk's position carries from window to
+// window.  Two pinned staging slots and two device windows: window k+1 is
+// read while window k is uploaded and searched.  With file_sum, h =
+// MD4(int32_LE(seed) || source) (match.go:52-53) is computed on a host
+// thread over the same staging bytes, in order.
+rsg_status search_fd(rsg_ctx *ctx, int32_t fd, int64_t off0, uint64_t size, const rsg_sum_head *head,
+                     const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets, int32_t seed,
+                     std::vector<rsg_match> &out, uint8_t *file_sum) {
+    rsg_status s;
+    const bool search = head->count > 0 && size > 0;  // count == 0: sendFile (sender.go:86-88)
+    const uint32_t B = search ? (uint32_t)head->block_len : 0;
+    const uint64_t W = search_window_bytes(B);
+    const uint64_t halo = B ? B - 1 : 0;
+    const uint64_t cap = W + halo + 64;
+    if (size && fd < 0) return fail(ctx, RSG_ERR_INVALID, "bad descriptor");
+    const uint64_t nwin = (size + W - 1) / W;
+    for (int k = 0; k < 2 && nwin; k++) {
+        if ((s = ensure_pin(ctx, ctx->h_in[k], cap)) != RSG_OK) return s;
+        if (search && (s = ensure_dev(ctx, ctx->d_in[k], cap)) != RSG_OK) return s;
+    }
+    struct Drain {
+        rsg_ctx *c;
+        ~Drain() {
+            for (int k = 0; k < 2; k++) (void)hipStreamSynchronize(c->side[k]);
+            (void)hipStreamSynchronize(c->stream);
+        }
+    } drain_guard{ctx};
+    Md4 h;
+    h.init();
+    if (file_sum) {
+        const uint8_t sb[4] = {(uint8_t)seed, (uint8_t)(seed >> 8), (uint8_t)(seed >> 16), (uint8_t)(seed >> 24)};
+        h.update(sb, 4);  // binary.Write(h, LittleEndian, st.Seed), match.go:52-53
+    }
+    std::future<void> md4_prev;  // the previous window's MD4 (windows hash in order)
+    auto read_win = [&](uint64_t k) -> int {
+        const uint64_t a = k * W, n = std::min(W + halo, size - a);
+        return pread_full(fd, off0 + (int64_t)a, (uint8_t *)ctx->h_in[k & 1].p, n);
+    };
+    auto read_err = [&](int code) {
+        if (code == -1) return fail(ctx, RSG_ERR_IO, "file has changed mid-transfer");  // fileio.go:99-104
+        return fail(ctx, RSG_ERR_IO, "file has changed mid-transfer: %s", strerror(code));
+    };
+    // the basis tables, once (slot 0's pinned stage keeps them for every window)
+    std::unique_ptr<Search> T;
+    SearchSlot &sl = ctx->search[0];
+    if (search) {
+        T.reset(new Search());
+        T->ctx = ctx;
+        T->sl = &sl;
+        T->size = size;
+        T->head = *head;
+        if ((s = tables(*T, sum1, sum2, targets)) != RSG_OK) return s;
+    }
+    const int64_t end_global = search ? T->end : 0;
+    hipEvent_t up[2] = {nullptr, nullptr};
+    struct Ev {
+        hipEvent_t *e;
+        ~Ev() {
+            for (int k = 0; k < 2; k++)
+                if (e[k]) hipEventDestroy(e[k]);
+        }
+    } ev_guard{up};
+    for (int k = 0; k < 2; k++) RSG_HIP(ctx, hipEventCreateWithFlags(&up[k], hipEventDisableTiming));
+    int code = nwin ? read_win(0) : 0;
+    if (code) return read_err(code);
+    uint64_t pos = 0;
+    for (uint64_t k = 0; k < nwin; k++) {
+        const int slot = (int)(k & 1);
+        const uint64_t a = k * W, nnew = std::min(W, size - a), nread = std::min(W + halo, size - a);
+        const uint8_t *hp = (const uint8_t *)ctx->h_in[slot].p;
+        const bool visit = search && (int64_t)a < end_global && pos < a + W;
+        if (visit)
+            RSG_HIP(ctx, hipMemcpyAsync(ctx->d_in[slot].p, hp, nread, hipMemcpyHostToDevice, ctx->side[1]));
+        RSG_HIP(ctx, hipEventRecord(up[slot], ctx->side[1]));
+        if (file_sum) {
+            std::future<void> prev = std::move(md4_prev);
+            md4_prev = std::async(std::launch::async, [&h, hp, nnew, p = std::move(prev)]() mutable {
+                if (p.valid()) p.wait();
+                h.update(hp, nnew);
+            });
+        }
+        // window k+1 into the other slot once window k-1's upload and MD4 left it
+        std::future<int> next;
+        if (k + 1 < nwin) {
+            RSG_HIP(ctx, hipEventSynchronize(up[slot ^ 1]));
+            next = std::async(std::launch::async, [&, k, slot]() {
+                (void)slot;
+                return read_win(k + 1);
+            });
+        }
+        if (visit) {
+            Search S;
+            S.ctx = ctx;
+            S.sl = &sl;
+            S.st = S.cst = ctx->side[0];
+            S.side = ctx->side[1];
+            S.copy = ctx->stream;
+            S.head = *head;
+            S.seed = seed;
+            S.size = nread;
+            S.ntiles = (uint32_t)((nread + kScanTile - 1) / kScanTile);
+            S.end = std::min<int64_t>((int64_t)W, end_global - (int64_t)a);
+            S.off_hi16 = T->off_hi16;
+            S.off_sum2 = T->off_sum2;
+            S.off_filter = T->off_filter;
+            S.off_filter16 = T->off_filter16;
+            S.off_table = T->off_table;
+            S.off_keys = T->off_keys;
+            S.blob_bytes = T->blob_bytes;
+            S.bmask = T->bmask;
+            S.pos0 = pos > a ? pos - a : 0;
+            if ((s = enqueue_scan(S, (const uint8_t *)ctx->d_in[slot].p, false)) != RSG_OK) return s;
+            if ((s = finish(S)) != RSG_OK) return s;
+            if (S.tail && (s = S.tail()) != RSG_OK) return s == RSG_ERR_HIP ? fail(ctx, s, "confirmation wait failed") : s;
+            for (const rsg_match &m : S.out) out.push_back(rsg_match{m.offset + (int64_t)a, m.index, 0});
+            pos = a + S.pos_end;
+        }
+        if (next.valid() && (code = next.get()) != 0) {
+            if (md4_prev.valid()) md4_prev.wait();
+            return read_err(code);
+        }
+        // window k+2 reuses this slot: its MD4 must be done before that read
+        if (file_sum && k + 1 < nwin) md4_prev.wait();
+    }
+    if (md4_prev.valid()) md4_prev.wait();
+    if (file_sum) h.final(file_sum);
+    return RSG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1010,6 +1196,26 @@ static rsg_status search_one(rsg_ctx *ctx, const void *src, uint64_t src_len, co
     const rsg_status s = search_batch(ctx, &j, 1, seed, host_src);
     *n_matches = j.n_matches;
     return s;
+}
+
+rsg_status rsg_hash_search_fd(rsg_ctx *ctx, int32_t fd, int64_t offset, uint64_t src_len, const rsg_sum_head *head,
+                              const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets, int32_t seed,
+                              rsg_match *matches, uint64_t match_cap, uint64_t *n_matches, uint8_t file_sum[16]) {
+    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    RSG_HIP(ctx, hipSetDevice(ctx->device));
+    rsg_status s = check_args(ctx, head, sum1, sum2, targets, matches, match_cap, n_matches);
+    if (s != RSG_OK) return s;
+    *n_matches = 0;
+    if (offset < 0 || src_len > (uint64_t)INT64_MAX) return fail(ctx, RSG_ERR_INVALID, "bad offset / length");
+    std::vector<rsg_match> out;
+    if ((s = search_fd(ctx, fd, offset, src_len, head, sum1, sum2, targets, seed, out, file_sum)) != RSG_OK) return s;
+    *n_matches = out.size();
+    if (out.size() > match_cap)
+        return fail(ctx, RSG_ERR_TRUNCATED, "%llu matches, capacity %llu", (unsigned long long)out.size(),
+                    (unsigned long long)match_cap);
+    if (!out.empty()) memcpy(matches, out.data(), out.size() * sizeof(rsg_match));
+    return RSG_OK;
 }
 
 // Test hook (include/rsg_testing.h): the sender's greedy walk with the GPU

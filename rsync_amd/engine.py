@@ -429,6 +429,25 @@ class Engine:
                                          _ptr(s2), _ptr(tg), _i32(seed), out, cap, ctypes.byref(nm)), self.ctx)
         return _matches_list(out, nm.value)
 
+    def hash_search_fd(self, fd: int, src_len: int, head, sum1, sum2, targets, seed: int, offset: int = 0,
+                       file_sum: bool = False):
+        """hashSearch over a source the engine reads from `fd` in windows
+        (rsg_hash_search_fd; sendFile's mapFile/ptr, fileio.go:31-112).
+        -> matches, or (matches, MD4(int32_LE(seed) || source)) with file_sum."""
+        h = head if isinstance(head, SumHead) else SumHead(*head)
+        s1 = np.ascontiguousarray(sum1, dtype=np.uint32)
+        s2 = np.ascontiguousarray(sum2, dtype=np.uint8).reshape(-1)
+        tg = np.ascontiguousarray(targets, dtype=np.int32)
+        cap = src_len // max(h.block_len, 1) + 2
+        out = (Match * cap)()
+        nm = ctypes.c_uint64()
+        dig = np.zeros(16, np.uint8)
+        check(lib.rsg_hash_search_fd(self.ctx, fd, offset, src_len, ctypes.byref(h), _ptr(s1), _ptr(s2), _ptr(tg),
+                                     _i32(seed), out, cap, ctypes.byref(nm),
+                                     _ptr(dig) if file_sum else None), self.ctx)
+        m = _matches_list(out, nm.value)
+        return (m, dig.tobytes()) if file_sum else m
+
     def hash_search_batch(self, jobs, seed: int, device: bool = True, raise_on_error: bool = True,
                           as_arrays: bool = False):
         """SendFiles' per-file hashSearch loop (sender.go:19-115) in one
