@@ -921,13 +921,15 @@ def bench_filesums(args, rank, world, local):
 
 def bench_receive(args, rank, world, local):
     """receiveData (receiver.go:98-188) latency and batch
-    rate: token application on the host, the seeded whole-file MD4
-    (receiver.go:117-120) on the GPU.  MD4 is one serial chain per file, so a
-    single file runs on ONE GPU lane: its latency is measured for a 1 MiB and
-    a 1 GiB file next to the one-core host MD4 rate (the C restatement); the
-    batched call (rsg_receive_data_batch) hashes many files in parallel.
-    Streams: every block of an identical basis matched (all tokens are
-    matches), i.e. the whole file is rebuilt from the basis."""
+    rate: token application on the host plus the seeded whole-file MD4 check
+    (receiver.go:117-120).  MD4 is one serial chain per file: a single file
+    (rsg_receive_data) is hashed on the host as its tokens are applied (on the
+    GPU it would get one lane, ~10x slower than a core: measured here too with
+    RSG_RECV_MD4=gpu on the 1 MiB file); the batched call
+    (rsg_receive_data_batch) hashes many files at once on the GPU, one lane
+    per file, and sends a batch's few large files to host threads when that
+    is faster (its cost split).  Streams: every block of an identical basis
+    matched, i.e. the whole file is rebuilt from the basis."""
     import rsync_amd
     import cases
     from oracle import oracle as orc
@@ -944,39 +946,62 @@ def bench_receive(args, rank, world, local):
         t_cpu = time.perf_counter() - c0
         return rsync_amd.encode_tokens(data, head, matches) + fsum, head, t_cpu
 
+    def timed(fn, reps=1):
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            r = fn()
+            dt = time.perf_counter() - t0
+            best = dt if best is None or dt < best else best
+        return r, best
+
     for name, size in (("1MiB", 1 << 20), ("1GiB", 1 << 30)):
         data = cases.splitmix64_bytes(77, size)
         stream, head, t_cpu = stream_for(data)
+        eng.receive_data(stream, head, data, seed)  # warm-up
+        (out, used), dt = timed(lambda: eng.receive_data(stream, head, data, seed), 5 if size <= (1 << 20) else 2)
+        r = {"s": round(dt, 4), "gib_s": round(size / dt / GIB, 4),
+             "equal": out == data.tobytes() and used == len(stream),
+             "md4_on": "host (fused with token application)",
+             "cpu_md4_1core_s": round(t_cpu, 4), "cpu_md4_1core_gib_s": round(size / t_cpu / GIB, 4)}
         if size <= (1 << 20):
-            eng.receive_data(stream, head, data, seed)  # warm-up
-        t0 = time.perf_counter()
-        out, used = eng.receive_data(stream, head, data, seed)
-        dt = time.perf_counter() - t0
-        res[f"single_{name}"] = {"s": round(dt, 4), "gib_s": round(size / dt / GIB, 4),
-                                 "equal": out == data.tobytes() and used == len(stream),
-                                 "cpu_md4_1core_s": round(t_cpu, 4),
-                                 "cpu_md4_1core_gib_s": round(size / t_cpu / GIB, 4)}
+            os.environ["RSG_RECV_MD4"] = "gpu"
+            try:
+                (out, used), dg = timed(lambda: eng.receive_data(stream, head, data, seed), 5)
+            finally:
+                del os.environ["RSG_RECV_MD4"]
+            r["gpu_one_lane_s"] = round(dg, 4)
+        res[f"single_{name}"] = r
         del data, stream, out
-    # batch: 1024 files of 1 MiB (one lane each)
-    n, size = 1024, 1 << 20
-    files = [cases.splitmix64_bytes(1000 + f, size) for f in range(n)]
-    jobs, t_cpu = [], 0.0
-    for d in files:
-        st, head, tc = stream_for(d)
-        jobs.append((st, head, d))
-        t_cpu += tc
-    eng.receive_data_batch(jobs[:16], seed)
-    t0 = time.perf_counter()
-    got = eng.receive_data_batch(jobs, seed)
-    dt = time.perf_counter() - t0
-    res["batch_1024x1MiB"] = {"s": round(dt, 4), "gib_s": round(n * size / dt / GIB, 3),
-                              "equal": all(g[0] == d.tobytes() for g, d in zip(got, files)),
-                              "cpu_md4_1core_gib_s": round(n * size / t_cpu / GIB, 4)}
+
+    def batch(tag, n, size):
+        files = [cases.splitmix64_bytes(1000 + f, size) for f in range(n)]
+        jobs, t_cpu = [], 0.0
+        for d in files:
+            st, head, tc = stream_for(d)
+            jobs.append((st, head, d))
+            t_cpu += tc
+        eng.receive_data_batch(jobs[:4], seed)
+        got, dt = timed(lambda: eng.receive_data_batch(jobs, seed), 2)
+        res[tag] = {"s": round(dt, 4), "gib_s": round(n * size / dt / GIB, 3),
+                    "equal": all(g[0] == d.tobytes() for g, d in zip(got, files)),
+                    "cpu_md4_1core_gib_s": round(n * size / t_cpu / GIB, 4)}
+        if n >= 64:
+            os.environ["RSG_RECV_MD4"] = "host"
+            try:
+                _, dh = timed(lambda: eng.receive_data_batch(jobs, seed), 2)
+            finally:
+                del os.environ["RSG_RECV_MD4"]
+            res[tag]["all_host_threads_gib_s"] = round(n * size / dh / GIB, 3)
+
+    batch("batch_1024x1MiB", 1024, 1 << 20)
+    batch("batch_4x256MiB", 4, 256 << 20)
     print(json.dumps({"metric": "receiveData (token application + seeded whole-file MD4 check)",
                       "value": res["batch_1024x1MiB"]["gib_s"], "unit": "GiB/s", "n_gpus": 1,
                       "higher_is_better": True, "dtype": "u32",
                       "data": "synthetic (splitmix64 files, identical basis: every block a match token)",
-                      "config": {"workload": "receive: single 1 MiB / 1 GiB files (latency), 1024 x 1 MiB batch"},
+                      "config": {"workload": "receive: single 1 MiB / 1 GiB files (latency), 1024 x 1 MiB and "
+                                             "4 x 256 MiB batches"},
                       "results": res}), flush=True)
     eng.close()
 

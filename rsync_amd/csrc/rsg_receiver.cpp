@@ -7,8 +7,14 @@
 // bytes at i*BlockLength, RemainderLength for the last block), the int32 0
 // terminator, then the sender's 16-byte whole-file sum MD4(int32_LE(seed) ||
 // file).  Rebuilding is byte copying (the reference does one ReadAt per
-// matched block); the whole-file sum check runs on the GPU through the
-// seeded file-sum kernel (rsg_filesums.hip).
+// matched block).  The whole-file sum h = MD4(int32_LE(seed) || file)
+// (receiver.go:117-120,166) is one serial chain per file: the GPU's seeded
+// file-sum kernel (rsg_filesums.hip) hashes many files at once, one lane per
+// file, but a lane is ~10x slower than a host core, so a
+// single file (rsg_receive_data) is hashed on the host while its tokens are
+// applied, as the reference writes h as it goes (receiver.go:159-164), and
+// a batch (rsg_receive_data_batch) sends its largest files to host threads
+// when that shortens the batch (pick_host below) and the rest to the GPU.
 #include <string.h>
 
 #include <algorithm>
@@ -28,9 +34,11 @@ int32_t rd_i32(const uint8_t *p) {
 
 // Walks the stream; copies into out while it fits.  Sets *out_len (the
 // rebuilt length) and *sum_at (offset of the 16-byte whole-file sum).
+// With h, the rebuilt bytes are also fed to h as they are written (the
+// reference's h.Write of every token's data, receiver.go:159-164).
 rsg_status apply(rsg_ctx *ctx, const uint8_t *tokens, uint64_t tokens_len, const rsg_sum_head *head,
                  const uint8_t *basis, uint64_t basis_len, uint8_t *out, uint64_t out_cap, uint64_t *out_len,
-                 uint64_t *sum_at) {
+                 uint64_t *sum_at, Md4 *h = nullptr) {
     if (!head || !out_len || (tokens_len && !tokens))
         return fail(ctx, RSG_ERR_INVALID, "NULL argument");
     uint64_t pos = 0, off = 0;
@@ -60,8 +68,12 @@ rsg_status apply(rsg_ctx *ctx, const uint8_t *tokens, uint64_t tokens_len, const
                             (unsigned long long)basis_len);
             data = basis + off2;
         }
-        if (out && off + n <= out_cap) memcpy(out + off, data, n);
-        else if (out) fits = false;
+        if (out && off + n <= out_cap) {
+            memcpy(out + off, data, n);
+            if (h) h->update(out + off, n);
+        } else if (out) {
+            fits = false;
+        }
         off += n;
     }
     *out_len = off;
@@ -70,15 +82,67 @@ rsg_status apply(rsg_ctx *ctx, const uint8_t *tokens, uint64_t tokens_len, const
     return RSG_OK;
 }
 
+// The whole-file sum's seed prefix, binary.Write(h, LittleEndian, seed)
+// (receiver.go:117-120).
+void md4_seeded(Md4 &h, int32_t seed) {
+    h.init();
+    const uint8_t sb[4] = {(uint8_t)seed, (uint8_t)(seed >> 8), (uint8_t)(seed >> 16), (uint8_t)(seed >> 24)};
+    h.update(sb, 4);
+}
+
+// Which jobs of a batch hash on the host.  The GPU batch takes about
+// (largest GPU file) / lane rate + (GPU bytes) / staging rate (the host
+// copies into pinned memory and the PCIe upload); host threads take about
+// max(largest host file / core rate, host bytes / (threads x core rate)),
+// the two running side by side.  The k largest files go to the host for the
+// k that minimises the longer of the two.  RSG_RECV_MD4 = gpu / host forces
+// one side (tests, A/B).  Rates (GiB/s): one GPU lane 0.09 and one host core
+// 0.9 (profiles/r03f_receive_line.json), staging 3.
+std::vector<uint8_t> pick_host(const rsg_recv_job *jobs, uint64_t i0, uint64_t i1, int threads) {
+    const uint64_t n = i1 - i0;
+    std::vector<uint8_t> host(n, 0);
+    const char *e = getenv("RSG_RECV_MD4");
+    if (e && !strcmp(e, "gpu")) return host;
+    if (e && !strcmp(e, "host")) {
+        std::fill(host.begin(), host.end(), 1);
+        return host;
+    }
+    constexpr double kLane = 0.09, kCore = 0.9, kStage = 3.0, kGiB = 1073741824.0;
+    std::vector<uint64_t> ord(n);
+    for (uint64_t k = 0; k < n; k++) ord[k] = k;
+    std::sort(ord.begin(), ord.end(), [&](uint64_t a, uint64_t b) { return jobs[i0 + a].out_cap > jobs[i0 + b].out_cap; });
+    double total = 0;
+    for (uint64_t k = 0; k < n; k++) total += (double)jobs[i0 + k].out_cap;
+    double best = 1e300, pre = 0;
+    uint64_t best_k = 0;
+    for (uint64_t k = 0; k <= n; k++) {  // the k largest on the host
+        const double gpu = k < n ? ((double)jobs[i0 + ord[k]].out_cap / kLane + (total - pre) / kStage) / kGiB : 0;
+        const double hst = k ? std::max((double)jobs[i0 + ord[0]].out_cap / kCore, pre / (threads * kCore)) / kGiB : 0;
+        const double t = std::max(gpu, hst);
+        if (t < best) {
+            best = t;
+            best_k = k;
+        }
+        if (k < n) pre += (double)jobs[i0 + ord[k]].out_cap;
+    }
+    for (uint64_t k = 0; k < best_k; k++) host[ord[k]] = 1;
+    return host;
+}
+
+int copy_threads() {
+    const char *e = getenv("RSG_COPY_THREADS");
+    const int t = e ? atoi(e) : 8;
+    return std::max(1, std::min(t, 64));
+}
+
 // Token application of many jobs on a few host threads (byte copying; each
 // job writes only its own output).  Sets every job's out_len / consumed /
 // status; returns nothing (failures are per job).
-void apply_jobs(rsg_recv_job *jobs, uint64_t i0, uint64_t i1, std::vector<uint64_t> &sum_at) {
-    static const int threads = [] {
-        const char *e = getenv("RSG_COPY_THREADS");
-        const int t = e ? atoi(e) : 8;
-        return std::max(1, std::min(t, 64));
-    }();
+// host[k - i0]: job k's whole-file sum is checked on this thread while its
+// tokens are applied (status RSG_ERR_CORRUPT on a mismatch, consumed set).
+void apply_jobs(rsg_recv_job *jobs, uint64_t i0, uint64_t i1, std::vector<uint64_t> &sum_at,
+                const std::vector<uint8_t> &host, int32_t seed) {
+    const int threads = copy_threads();
     std::atomic<uint64_t> next{i0};
     auto worker = [&] {
         for (uint64_t k; (k = next.fetch_add(1)) < i1;) {
@@ -86,16 +150,25 @@ void apply_jobs(rsg_recv_job *jobs, uint64_t i0, uint64_t i1, std::vector<uint64
             j.out_len = 0;
             j.consumed = 0;
             uint64_t at = 0;
+            Md4 h;
+            const bool on_host = host[k - i0] != 0;
+            if (on_host) md4_seeded(h, seed);
             rsg_status st = apply(nullptr, j.tokens, j.tokens_len, &j.head, j.basis, j.basis_len, j.out, j.out_cap,
-                                  &j.out_len, &at);
+                                  &j.out_len, &at, on_host ? &h : nullptr);
             if (st == RSG_OK && at + 16 > j.tokens_len) st = RSG_ERR_INVALID;  // receiver.go:167-170
             if (st == RSG_OK && j.out_len && !j.out) st = RSG_ERR_INVALID;
             sum_at[k - i0] = at;
+            if (st == RSG_OK && on_host) {
+                uint8_t local[16];
+                h.final(local);
+                j.consumed = at + 16;
+                if (memcmp(local, j.tokens + at, 16) != 0) st = RSG_ERR_CORRUPT;  // receiver.go:171-173
+            }
             j.status = st;
         }
     };
     uint64_t bytes = 0;
-    for (uint64_t k = i0; k < i1; k++) bytes += jobs[k].tokens_len;
+    for (uint64_t k = i0; k < i1; k++) bytes += jobs[k].tokens_len + (host[k - i0] ? (16ull << 20) : 0);
     const int nt = (int)std::min<uint64_t>((uint64_t)threads, std::min<uint64_t>(i1 - i0, 1 + bytes / (1ull << 20)));
     std::vector<std::thread> pool;
     for (int t = 1; t < nt; t++) pool.emplace_back(worker);
@@ -120,19 +193,32 @@ rsg_status rsg_receive_data(rsg_ctx *ctx, const uint8_t *tokens, uint64_t tokens
                             const uint8_t *basis, uint64_t basis_len, int32_t seed, uint8_t *out, uint64_t out_cap,
                             uint64_t *out_len, uint64_t *consumed) {
     if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    // One file: h = MD4(seed_LE || rebuilt file) (receiver.go:117-120,166) is
+    // one serial chain, hashed here as the tokens are applied -- on a GPU it
+    // would get one lane, ~10x slower than this core.
+    // RSG_RECV_MD4=gpu checks it with the GPU's seeded file-sum kernel instead.
+    const char *e = getenv("RSG_RECV_MD4");
+    const bool gpu = e && !strcmp(e, "gpu");
+    Md4 h;
+    md4_seeded(h, seed);
     uint64_t sum_at = 0;
-    rsg_status s = apply(ctx, tokens, tokens_len, head, basis, basis_len, out, out_cap, out_len, &sum_at);
+    rsg_status s = apply(ctx, tokens, tokens_len, head, basis, basis_len, out, out_cap, out_len, &sum_at,
+                         gpu ? nullptr : &h);
     if (s != RSG_OK) return s;
     if (sum_at + 16 > tokens_len)  // io.ReadFull(remoteSum), receiver.go:167-170
         return fail(ctx, RSG_ERR_INVALID, "token stream ends before the whole-file sum");
     if (*out_len && !out) return fail(ctx, RSG_ERR_INVALID, "NULL output");
-    // h = MD4(seed_LE || rebuilt file), receiver.go:117-120,166
-    rsg_file f;
-    memset(&f, 0, sizeof f);
-    f.data = out;
-    f.len = *out_len;
     uint8_t local[16];
-    if ((s = rsg_file_sums_host(ctx, &f, 1, RSG_FILESUM_SEEDED, seed, local)) != RSG_OK) return s;
+    if (gpu) {
+        rsg_file f;
+        memset(&f, 0, sizeof f);
+        f.data = out;
+        f.len = *out_len;
+        if ((s = rsg_file_sums_host(ctx, &f, 1, RSG_FILESUM_SEEDED, seed, local)) != RSG_OK) return s;
+    } else {
+        h.final(local);
+    }
     if (consumed) *consumed = sum_at + 16;
     if (memcmp(local, tokens + sum_at, 16) != 0)  // receiver.go:171-173
         return fail(ctx, RSG_ERR_CORRUPT, "file corruption: whole-file sum mismatch");
@@ -191,13 +277,14 @@ rsg_status rsg_receive_data_batch(rsg_ctx *ctx, rsg_recv_job *jobs, uint64_t njo
         sl.i0 = i;
         sl.i1 = i1;
         sl.sum_at.assign(i1 - i, 0);
-        apply_jobs(jobs, i, i1, sl.sum_at);
+        const std::vector<uint8_t> host = pick_host(jobs, i, i1, copy_threads());
+        apply_jobs(jobs, i, i1, sl.sum_at, host, seed);
         sl.lane.clear();
         std::vector<rsg::FileSpan> spans;
         std::vector<CopyJob> copies;
         uint64_t off = 0;
         for (uint64_t q = i; q < i1; q++) {
-            if (jobs[q].status != RSG_OK) continue;
+            if (jobs[q].status != RSG_OK || host[q - i]) continue;  // failed, or checked on the host already
             sl.lane.push_back(q);
             spans.push_back({off, jobs[q].out_len});
             if (jobs[q].out_len) copies.push_back({nullptr, jobs[q].out, jobs[q].out_len});

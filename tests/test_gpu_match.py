@@ -132,13 +132,18 @@ def test_identical_large_property(eng):
 
 
 @pytest.mark.parametrize("seed_case", range(4))
-def test_delta_round_trip_on_gpu(eng, seed_case):
-    """The whole delta path through the C-ABI, every checksum on the GPU:
-    receiver block sums of the basis (generator.go:325-350) -> sender search
-    (match.go:21-230) -> tokens (token.go) + whole-file sum -> receiveData
-    (receiver.go:98-188) rebuilds the source and passes the seeded MD4 check;
-    a flipped sum byte is reported as corruption (receiver.go:171-173)."""
+@pytest.mark.parametrize("recv_md4", ["default", "gpu"])
+def test_delta_round_trip_on_gpu(eng, seed_case, recv_md4, monkeypatch):
+    """The whole delta path through the C-ABI: receiver block sums of the
+    basis (generator.go:325-350) -> sender search (match.go:21-230) -> tokens
+    (token.go) + whole-file sum (GPU file-sum kernel) -> receiveData
+    (receiver.go:98-188) rebuilds the source and passes the seeded MD4 check
+    (default: the host MD4 fused with token application, one file being one
+    serial chain; RSG_RECV_MD4=gpu: the GPU's file-sum kernel); a flipped sum
+    byte is reported as corruption (receiver.go:171-173)."""
     import rsync_amd
+    if recv_md4 != "default":
+        monkeypatch.setenv("RSG_RECV_MD4", recv_md4)
     rng = np.random.default_rng(900 + seed_case)
     basis = cases.splitmix64_bytes(910 + seed_case, int(rng.integers(50_000, 2_000_000)))
     src = cases.mutate(basis, 920 + seed_case, 0.4, 1, 5000, n_ins=3, n_del=3)
@@ -250,14 +255,19 @@ def test_long_blocks_prefix_pass(eng, blen):
     assert eng.hash_search(src, head, s1, s2, tg, seed) == want
 
 
-def test_receive_data_batch(eng):
+@pytest.mark.parametrize("mode", ["auto", "gpu", "host"])
+def test_receive_data_batch(eng, mode, monkeypatch):
     """rsg_receive_data_batch over a transfer's worth of files (RecvFiles'
     per-file receiveData, receiver.go:18-188): 48 random delta streams plus
     edge jobs -- a flipped whole-file sum byte (RSG_ERR_CORRUPT, receiver.go:
     171-173), a stream cut before its sum, a match token without a basis
     (RSG_ERR_INVALID), an empty file -- each job's status and bytes equal the
-    oracle's receive_data; the good jobs are unaffected by the bad ones."""
+    oracle's receive_data; the good jobs are unaffected by the bad ones.
+    mode: which side checks the whole-file sums (RSG_RECV_MD4; auto = the
+    batch's cost split)."""
     import rsync_amd
+    if mode != "auto":
+        monkeypatch.setenv("RSG_RECV_MD4", mode)
     from rsync_amd import _lib
     seed = 0x5EED
     jobs, want = [], []
@@ -291,3 +301,33 @@ def test_receive_data_batch(eng):
     assert e.value.status == _lib.ERR_CORRUPT
     assert [r[:2] for r in eng.receive_data_batch([j for j, w in zip(jobs, want) if w[0] == _lib.OK], seed)] \
         == [(w[1], w[2]) for w in want if w[0] == _lib.OK]
+
+
+def test_receive_data_batch_mixed_sizes(eng):
+    """A batch of three 20 MiB files and 60 small ones: the cost split sends
+    the large files' sums to host threads and the small ones' to the GPU
+    (one lane each).  A corrupt sum in one large and one small file is
+    reported on exactly those jobs; every other file equals the oracle's."""
+    from rsync_amd import _lib
+    seed = 0x1234
+    jobs, want = [], []
+    rng = np.random.default_rng(77)
+    for k in range(63):
+        n = (20 << 20) if k in (5, 30, 61) else int(rng.integers(1000, 300_000))
+        basis = cases.splitmix64_bytes(3000 + k, n)
+        src = cases.mutate(basis, 3100 + k, 0.3, 1, 5000, n_ins=2, n_del=2) if n < (1 << 20) else basis.copy()
+        head = orc.sum_head(basis.size, 0)
+        s1, s2 = orc.parse_records(orc.block_sums(basis, head[1], seed))
+        _, tok, fsum = orc.hash_search(src, head, s1, s2, orc.stable_targets(s1), seed)
+        stream = bytearray(tok + fsum)
+        if k in (30, 40):
+            stream[-1] ^= 0x80
+        jobs.append((bytes(stream), head, basis))
+        want.append(_lib.ERR_CORRUPT if k in (30, 40) else _lib.OK)
+        if k not in (30, 40):
+            assert orc.receive_data(bytes(stream), head, basis, seed)[0] == src.tobytes()
+    got = eng.receive_data_batch(jobs, seed, raise_on_error=False)
+    assert [g[0] for g in got] == want
+    for k, (st, data, used) in enumerate(got):
+        if st == _lib.OK:
+            assert data == orc.receive_data(jobs[k][0], jobs[k][1], jobs[k][2], seed)[0], k
