@@ -169,8 +169,8 @@ def main():
         res = {v: [] for v in names}
         for _ in range(5):
             for v in names:
-                _lib.check(_lib.lib.rsg_set_block_sums_kernel(v[0]))
-                _lib.check(_lib.lib.rsg_set_block_sums_diagnostic(v[1]))
+                eng.set_block_sums_kernel(v[0])
+                eng.set_block_sums_diagnostic(v[1])
                 for i in range(3):
                     step(i)
                 a0 = torch.cuda.Event(enable_timing=True)
@@ -181,8 +181,8 @@ def main():
                 a1.record(stream)
                 eng.synchronize(sptr)
                 res[v].append(a0.elapsed_time(a1) / args.steps)
-        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
-        _lib.check(_lib.lib.rsg_set_block_sums_diagnostic(0))
+        eng.set_block_sums_kernel(-1)
+        eng.set_block_sums_diagnostic(0)
         step(0)  # the records hold the product kernel's output again (diagnostics write garbage)
         eng.synchronize(sptr)
         extra["ab_kernel_ms"] = {names[v]: [round(x, 4) for x in sorted(res[v])] for v in names}

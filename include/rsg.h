@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RSG_ABI_VERSION 1
+#define RSG_ABI_VERSION 2  /* 2: per-context block-sum kernel knob, multi-GPU calls, rsg_hash_search_fd */
 /* One wire record: int32 LE sum1 then sum2[16] (generator.go:341-346). */
 #define RSG_RECORD_BYTES 20
 #define RSG_SUM2_BYTES 16
@@ -141,7 +141,7 @@ uint64_t rsg_plan_total_records(const rsg_plan *plan);
 rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void *d_arena,
                                   int32_t seed, void *d_records, void *stream);
 
-/* Tuning knob (process-wide): block-sum kernel variant.  Every variant
+/* Tuning knob of one context: block-sum kernel variant.  Every variant
  * gives identical records; only speed differs.  -1 = automatic (default),
  * 0 = direct per-lane loads, 1 = staged LDS-DMA slabs (256 bytes of every
  * block per segment), 2 = park (three loader waves stream 64-block tiles
@@ -153,21 +153,11 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
  * Automatic: aligned batches take 2 when 512 <= the largest block <= 703
  * bytes, 4 when it is 704..1536 bytes, else 1; unaligned batches (a block not 4-byte aligned) take 6 (3
  * for blocks >= 8 KiB, else 0, when the arena itself is not 4-byte aligned;
- * 1, 2, 4 and 5 fall back to 0 there).  The
- * environment variable RSG_BLOCKSUMS_KERNEL sets the initial value.  Returns
- * RSG_ERR_INVALID outside -1..6. */
-rsg_status rsg_set_block_sums_kernel(int32_t variant);
-
-/* Timing diagnostics for DESIGN.md's roofline analysis, NOT for use: while
- * diag != 0 every aligned block-sum launch runs the diagnostic instead of the
- * product kernel and the "records" it writes are meaningless.  1 = staged
- * memory only, 2 = staged hashing only, 3 = park memory only, 4 = park
- * hashing only, 5 = linear read of the arena (plain loads), 6 = linear read
- * (LDS DMA), 7 = linear read (LDS DMA) 4 bytes off 16-byte alignment, 8 = park
- * memory only with 16-byte aligned requests.  0 = off (default; environment RSG_BLOCKSUMS_DIAG).  Kept apart
- * from rsg_set_block_sums_kernel so the product knob can never select a
- * diagnostic. */
-rsg_status rsg_set_block_sums_diagnostic(int32_t diag);
+ * 1, 2, 4 and 5 fall back to 0 there).  The environment variable
+ * RSG_BLOCKSUMS_KERNEL sets a new context's initial value.  Returns
+ * RSG_ERR_INVALID outside -1..6.  (Timing diagnostics that write
+ * meaningless records live in include/rsg_testing.h, not here.) */
+rsg_status rsg_set_block_sums_kernel(rsg_ctx *ctx, int32_t variant);
 
 /* Fallback census of ctx's device since the last reset: counts[0] = full
  * 64-block waves of the staged kernels (1, 4, 5, 6), counts[1] = full

@@ -22,6 +22,16 @@ rsg_status rsg_testing_walk(const uint64_t *cand, uint64_t n, const int32_t *tru
                             const rsg_sum_head *head, rsg_match *out, uint64_t cap, uint64_t *n_out,
                             uint64_t stats[2]);
 
+/* Timing diagnostics for DESIGN.md's roofline analysis, on one context:
+ * while diag != 0 every aligned block-sum launch of ctx runs the diagnostic
+ * instead of the product kernel and the "records" it writes are
+ * meaningless.  1 = staged memory only, 2 = staged hashing only, 3 = park
+ * memory only, 4 = park hashing only, 5 = linear read of the arena (plain
+ * loads), 6 = linear read (LDS DMA), 7 = linear read (LDS DMA) 4 bytes off
+ * 16-byte alignment, 8 = park memory only with 16-byte aligned requests.
+ * 0 = off (default). */
+rsg_status rsg_testing_block_sums_diagnostic(rsg_ctx *ctx, int32_t diag);
+
 /* The product's host MD4 (RFC 1320; rsync_amd/csrc/rsg_md4_host.cpp), used
  * for whole-file sums whose bytes stream through host memory: the sender's
  * MD4(int32_LE(seed) || source) in rsg_hash_search_fd and receiveData's

@@ -24,7 +24,7 @@ RECORD_BYTES = 20
 FILESUM_PLAIN = 0   # MD4(file), rsyncchecksum.go:60-66
 FILESUM_SEEDED = 1  # MD4(int32_LE(seed) || file), match.go:52-53
 CHUNK_SIZE = 256 * 1024
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 OK = 0
 ERR_INVALID = -1
@@ -133,8 +133,7 @@ _PROTOS = {
     "rsg_plan_destroy": (None, [_vp]),
     "rsg_plan_total_records": (_u64, [_vp]),
     "rsg_block_sums_planned": (_st, [_vp, _vp, _vp, _i32, _vp, _vp]),
-    "rsg_set_block_sums_kernel": (_st, [_i32]),
-    "rsg_set_block_sums_diagnostic": (_st, [_i32]),
+    "rsg_set_block_sums_kernel": (_st, [_vp, _i32]),
     "rsg_block_sums_fallbacks": (_st, [_vp, ctypes.POINTER(_u64), _i32]),
     "rsg_block_sums_device": (_st, [_vp, _vp, _u64, ctypes.POINTER(File), _u64, _i32, _vp, _u64]),
     "rsg_block_sums_host": (_st, [_vp, ctypes.POINTER(File), _u64, _i32, _vp, _u64]),
@@ -184,6 +183,7 @@ _PROTOS = {
     "rsg_testing_walk": (_st, [_vp, _u64, _vp, _u64, ctypes.POINTER(SumHead), ctypes.POINTER(Match), _u64,
                                ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "rsg_testing_md4": (_st, [_vp, _u64, _i32, _i32, _u64, _vp]),
+    "rsg_testing_block_sums_diagnostic": (_st, [_vp, _i32]),
 }
 
 for _name, (_res, _args) in _PROTOS.items():

@@ -13,6 +13,7 @@
 #include <new>
 #include <thread>
 
+#include "../../include/rsg_testing.h"
 #include "rsg_host.h"
 
 using rsg::DevFile;
@@ -146,7 +147,8 @@ rsg_status launch_plan(rsg_ctx *ctx, const HostPlan &plan, const void *d_files, 
     RSG_HIP(ctx, rsg::launch_block_sums((const uint8_t *)d_arena, plan.arena_bytes, (const DevFile *)d_files,
                                         (const uint32_t *)d_wg, plan.total_blocks, plan.nwg, aligned,
                                         plan.max_blen, (uint32_t)seed, (uint8_t *)d_records,
-                                        (uint32_t *)d_scratch, plan.lds_reserve, stream));
+                                        (uint32_t *)d_scratch, plan.lds_reserve, ctx->bs_variant, ctx->bs_diag,
+                                        stream));
     return RSG_OK;
 }
 
@@ -238,6 +240,7 @@ rsg_status rsg_ctx_create(int32_t device, rsg_ctx **out) {
     if (hipGetDeviceProperties(&prop, device) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return fail(nullptr, RSG_ERR_NODEV, "device %d is %s, not gfx950 (MI355X)", device, prop.gcnArchName);
     rsg_ctx *c = new (std::nothrow) rsg_ctx();
+    if (c) c->bs_variant = rsg::block_sums_variant_env();
     if (!c) return fail(nullptr, RSG_ERR_NOMEM, "context allocation");
     c->device = device;
     if ((e = hipSetDevice(device)) != hipSuccess || (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
@@ -425,15 +428,19 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
                        pick_stream(ctx, stream));
 }
 
-rsg_status rsg_set_block_sums_kernel(int32_t variant) {
-    if (variant < -1 || variant > 6) return fail(nullptr, RSG_ERR_INVALID, "variant must be -1..6");
-    rsg::set_block_sums_variant(variant);
+rsg_status rsg_set_block_sums_kernel(rsg_ctx *ctx, int32_t variant) {
+    RSG_ENTER(ctx);
+    if (variant < -1 || variant > rsg::kBlockSumsVariantMax)
+        return fail(ctx, RSG_ERR_INVALID, "variant must be -1..%d", rsg::kBlockSumsVariantMax);
+    ctx->bs_variant = variant;
     return RSG_OK;
 }
 
-rsg_status rsg_set_block_sums_diagnostic(int32_t diag) {
-    if (diag < 0 || diag > 8) return fail(nullptr, RSG_ERR_INVALID, "diagnostic must be 0..8");
-    rsg::set_block_sums_diagnostic(diag);
+rsg_status rsg_testing_block_sums_diagnostic(rsg_ctx *ctx, int32_t diag) {
+    RSG_ENTER(ctx);
+    if (diag < 0 || diag > rsg::kBlockSumsDiagMax)
+        return fail(ctx, RSG_ERR_INVALID, "diagnostic must be 0..%d", rsg::kBlockSumsDiagMax);
+    ctx->bs_diag = diag;
     return RSG_OK;
 }
 

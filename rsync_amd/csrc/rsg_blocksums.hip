@@ -915,15 +915,22 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
 // unaligned batches take 6 (3 for blocks >= 8 KiB, else 0, when the arena
 // itself is not 4-byte aligned).
 //
-// Timing diagnostics (rsg_set_block_sums_diagnostic, a separate knob so the
-// product knob can never select one; their "records" are meaningless):
+// Timing diagnostics (rsg_testing_block_sums_diagnostic, a test-only knob of
+// one context, so the product knob can never select one; their "records" are
+// meaningless):
 // 1 = staged memory only, 2 = staged hashing only, 3 = park memory only,
 // 4 = park hashing only, 5 = linear read with plain loads, 6 = linear read
 // with LDS DMA, 7 = the same with every request 4 bytes off a 16-byte
 // boundary, 8 = park memory only with 16-byte aligned quad requests.
 constexpr int kParkLoaders = 3;  // 1 / 2 / 3 loaders measured
-static int g_variant = -2;  // -2 = not yet read from RSG_BLOCKSUMS_KERNEL
-static int g_diag = -2;     // -2 = not yet read from RSG_BLOCKSUMS_DIAG
+int block_sums_variant_env() {
+    static const int v = [] {
+        const char *e = getenv("RSG_BLOCKSUMS_KERNEL");
+        const int x = e ? atoi(e) : -1;
+        return (x < -1 || x > kBlockSumsVariantMax) ? -1 : x;
+    }();
+    return v;
+}
 
 static uint32_t park_grid(uint64_t total_blocks) {
     int dev = 0, cus = 256;
@@ -935,22 +942,13 @@ static uint32_t park_grid(uint64_t total_blocks) {
 hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const DevFile *files,
                              const uint32_t *wg_file, uint64_t total_blocks, uint32_t nwg, bool aligned,
                              uint32_t max_blen, uint32_t seed, uint8_t *out, uint32_t *scratch,
-                             uint32_t lds_reserve, hipStream_t stream) {
+                             uint32_t lds_reserve, int variant, int diag, hipStream_t stream) {
     (void)scratch;
     if (total_blocks == 0) return hipSuccess;
-    if (g_variant == -2) {
-        const char *e = getenv("RSG_BLOCKSUMS_KERNEL");
-        g_variant = e ? atoi(e) : -1;
-        if (g_variant < -1 || g_variant > 6) g_variant = -1;
-    }
-    if (g_diag == -2) {
-        const char *e = getenv("RSG_BLOCKSUMS_DIAG");
-        g_diag = e ? atoi(e) : 0;
-    }
     const dim3 block(kBlockSumThreads), grid(nwg);
     const dim3 pgrid(park_grid(total_blocks)), pblock(kPkThreads);
-    if (g_diag > 0 && aligned) {
-        switch (g_diag) {
+    if (diag > 0 && aligned) {
+        switch (diag) {
             case 1:
                 hipLaunchKernelGGL((block_sums_staged<1>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
                                    total_blocks, seed, out);
@@ -989,7 +987,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         }
         return hipGetLastError();
     }
-    int v = g_variant;
+    int v = variant;
     // Aligned: park for 512..703-byte blocks, 128-byte segments up to 1536
     // (B = 1024: 0.197-0.204 ms against 0.207-0.224 for 256-byte segments in
     // three sweeps), 256-byte segments beyond (equal at 4 KiB, 12 % better at
@@ -1060,8 +1058,6 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     return hipGetLastError();
 }
 
-void set_block_sums_variant(int v) { g_variant = v; }
-void set_block_sums_diagnostic(int d) { g_diag = d; }
 
 hipError_t read_block_sums_fallbacks(uint64_t out[2], bool reset) {
     unsigned long long v[2] = {0, 0};

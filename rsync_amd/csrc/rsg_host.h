@@ -81,6 +81,10 @@ struct rsg_ctx {
     };
     bool timing = false;
     std::vector<TimedSpan> spans;
+    // block-sum kernel knobs of this context (rsg_set_block_sums_kernel;
+    // rsg_testing_block_sums_diagnostic): -1 = automatic; 0 = no diagnostic
+    int bs_variant = -1;
+    int bs_diag = 0;
     uint64_t stat_candidates = 0, stat_windows = 0;  // roll candidates read back, windows confirmed
 };
 

@@ -23,19 +23,23 @@ struct DevFile {
 };
 static_assert(sizeof(DevFile) == 32, "DevFile layout");
 
+// variant / diag: the calling context's knobs (-1 automatic; 0 no diagnostic).
 hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const DevFile *files,
                              const uint32_t *wg_file, uint64_t total_blocks, uint32_t nwg, bool aligned,
                              uint32_t max_blen, uint32_t seed, uint8_t *out, uint32_t *scratch,
-                             uint32_t lds_reserve, hipStream_t stream);
+                             uint32_t lds_reserve, int variant, int diag, hipStream_t stream);
 
 // Device scratch a block-sum launch needs: 4 + 4 * ceil(total_blocks / 64) bytes.
 inline uint64_t block_sums_scratch_bytes(uint64_t total_blocks) { return 8 + 4 * ((total_blocks + 63) / 64); }
 
 // Product variants (-1 auto, 0 direct, 1 staged, 2 park, 3 long, 4/5 staged
 // with 128/512-byte segments, 6 staged at any byte offset) and timing
-// diagnostics (0 off, 1..6; outputs meaningless), rsg_blocksums.hip.
-void set_block_sums_variant(int v);
-void set_block_sums_diagnostic(int d);
+// diagnostics (0 off, 1..kBlockSumsDiagMax; outputs meaningless),
+// rsg_blocksums.hip; both per context (rsg_ctx::bs_variant / bs_diag).
+constexpr int kBlockSumsVariantMax = 6;
+constexpr int kBlockSumsDiagMax = 8;
+// RSG_BLOCKSUMS_KERNEL (read once): a context's initial variant.
+int block_sums_variant_env();
 // Fallback census of the current device: [0] staged waves, [1] park tiles
 // (full ones that took per-lane loads); synchronises the device.
 hipError_t read_block_sums_fallbacks(uint64_t out[2], bool reset);

@@ -210,6 +210,17 @@ class Engine:
     def plan(self, files: Sequence[Tuple[int, int, int]], arena_bytes: int) -> Plan:
         return Plan(self, files, arena_bytes)
 
+    def set_block_sums_kernel(self, variant: int):
+        """rsg_set_block_sums_kernel: this context's block-sum kernel variant
+        (-1 automatic; every variant gives identical records)."""
+        check(lib.rsg_set_block_sums_kernel(self.ctx, variant), self.ctx)
+
+    def set_block_sums_diagnostic(self, diag: int):
+        """rsg_testing_block_sums_diagnostic (test hook): while diag != 0 this
+        context's aligned block-sum launches run a timing diagnostic and write
+        meaningless records."""
+        check(lib.rsg_testing_block_sums_diagnostic(self.ctx, diag), self.ctx)
+
     def block_sums_fallbacks(self, reset: bool = True) -> Tuple[int, int]:
         """Fallback census (rsg_block_sums_fallbacks): (staged waves, park
         tiles) of full 64-block groups hashed with per-lane loads instead of

@@ -188,7 +188,7 @@ def test_kernel_variants_match(eng, variant, blen):
     files = [cases.splitmix64_bytes(4000 + i, n) for i, n in enumerate(lens)]
     want = b"".join(orc.block_sums(f, blen, cases.SEED) for f in files)
     try:
-        _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))
+        eng.set_block_sums_kernel(variant)
         _, rec, _ = eng.block_sums(files, cases.SEED, blen)
         arena = eng.alloc(sum(lens))
         offs = np.cumsum([0] + lens[:-1]).tolist()
@@ -196,7 +196,7 @@ def test_kernel_variants_match(eng, variant, blen):
         recs, total = eng.block_sums_device(arena, [(o, n, blen) for o, n in zip(offs, lens)], cases.SEED)
         rec_dev = recs.download(total * 20).tobytes()
     finally:
-        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+        eng.set_block_sums_kernel(-1)
     assert rec == want
     assert rec_dev == want
 
@@ -220,11 +220,11 @@ def test_unaligned_windows(eng, variant, blen):
     wins = [(o, blen) for o in offs] + [(size - blen // 3, blen // 3), (size - blen, blen), (size - 1, 1)]
     want = b"".join(orc.block_sums(src[o:o + n], blen, cases.SEED) for o, n in wins)
     try:
-        _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))
+        eng.set_block_sums_kernel(variant)
         recs, total = eng.block_sums_device(arena, [(o, n, blen) for o, n in wins], cases.SEED)
         got = recs.download(total * 20).tobytes()
     finally:
-        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+        eng.set_block_sums_kernel(-1)
     assert got == want
 
 
@@ -241,11 +241,11 @@ def test_variants_long_blocks_full_waves(eng, variant):
     arena.upload(np.concatenate(datas))
     want = b"".join(orc.block_sums(d, 131072, cases.SEED) for d in datas)
     try:
-        _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))
+        eng.set_block_sums_kernel(variant)
         recs, total = eng.block_sums_device(arena, [(o, n, 131072) for o, n in zip(offs, lens)], cases.SEED)
         got = recs.download(total * 20).tobytes()
     finally:
-        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+        eng.set_block_sums_kernel(-1)
     assert got == want
 
 
@@ -275,11 +275,11 @@ def test_variants_device_aligned_arena(eng, variant):
     for blen in (700, 64, 703, 704, 1024, 1536, 1537, 4096):
         want = b"".join(orc.block_sums(d, blen, cases.SEED) for d in datas)
         try:
-            _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))
+            eng.set_block_sums_kernel(variant)
             recs, total = eng.block_sums_device(arena, [(o, n, blen) for o, n in zip(offs, lens)], cases.SEED)
             got = recs.download(total * 20).tobytes()
         finally:
-            _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+            eng.set_block_sums_kernel(-1)
         assert got == want, blen
 
 
@@ -310,3 +310,28 @@ def test_pinned_sources_direct_dma(eng):
         assert rec_p[: len(exp)] == exp
     finally:
         eng.free_pinned(pin)
+
+
+def test_kernel_knobs_are_per_context():
+    """A timing diagnostic (meaningless records) set on one context leaves
+    another context's block sums exact: the knobs belong to a context
+    (process-global switches could corrupt a concurrent caller)."""
+    import rsync_amd
+    a, b = rsync_amd.Engine(0), rsync_amd.Engine(0)
+    try:
+        files = [cases.splitmix64_bytes(60 + i, 1 << 20) for i in range(8)]
+        a.set_block_sums_diagnostic(3)
+        a.set_block_sums_kernel(1)
+        _, rec, _ = b.block_sums(files, cases.SEED, 700)
+        assert rec == b"".join(orc.block_sums(f, 700, cases.SEED) for f in files)
+        a.set_block_sums_diagnostic(0)
+        a.set_block_sums_kernel(-1)
+        _, rec_a, _ = a.block_sums(files, cases.SEED, 700)
+        assert rec_a == rec
+        with pytest.raises(rsync_amd.RsgError):
+            a.set_block_sums_kernel(7)
+        with pytest.raises(rsync_amd.RsgError):
+            a.set_block_sums_diagnostic(9)
+    finally:
+        a.close()
+        b.close()

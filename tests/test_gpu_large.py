@@ -120,11 +120,11 @@ def _run(eng, unaligned, variant, B, seed=cases.SEED):
     recs = eng.alloc(plan.total_records * 20)
     eng.block_sums_fallbacks(reset=True)
     try:
-        _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))
+        eng.set_block_sums_kernel(variant)
         plan.run(arena, seed, recs)
         eng.synchronize()
     finally:
-        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+        eng.set_block_sums_kernel(-1)
     fb = eng.block_sums_fallbacks(reset=True)
     rec = recs.download(plan.total_records * 20)
     recs.free()
@@ -236,10 +236,10 @@ def test_fallback_census_counts(eng, variant, kind):
     arena.upload(d)
     eng.block_sums_fallbacks(reset=True)
     try:
-        _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))
+        eng.set_block_sums_kernel(variant)
         recs, total = eng.block_sums_device(arena, [(0, n, 700)], cases.SEED)
     finally:
-        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+        eng.set_block_sums_kernel(-1)
     fb = eng.block_sums_fallbacks(reset=True)
     assert recs.download(total * 20).tobytes() == orc.block_sums(d, 700, cases.SEED)
     assert fb[kind] >= 1 and fb[1 - kind] == 0, fb

@@ -56,15 +56,15 @@ def main():
             runs = [r for r in runs if r[1] not in (5, 6)]
         # the memory clock ramps up over the first ~15 ms of launches: warm up
         # before the first variant so it is not timed on a cold card
-        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+        eng.set_block_sums_kernel(-1)
         import time
         w0 = time.perf_counter()
         while time.perf_counter() - w0 < 0.3:
             plan.run(arenas[0], SEED, recs, stream=sp)
             eng.synchronize(sp)
         for v, d, name in runs:
-            _lib.check(_lib.lib.rsg_set_block_sums_kernel(v))
-            _lib.check(_lib.lib.rsg_set_block_sums_diagnostic(d))
+            eng.set_block_sums_kernel(v)
+            eng.set_block_sums_diagnostic(d)
             steps = 5 if total > (4 << 30) else 30
             print(f"shape {nf}x{fb} B={blen}: {name}", file=sys.stderr, flush=True)
             for i in range(10):
@@ -79,8 +79,8 @@ def main():
             ms = e0.elapsed_time(e1) / steps
             res[name] = {"kernel_ms": round(ms, 4), "gib_s": round(total / 2**30 / (ms / 1e3), 1),
                          "hbm_frac_8tbs": round((total + plan.total_records * 20) / (ms / 1e3) / 8e12, 4)}
-        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
-        _lib.check(_lib.lib.rsg_set_block_sums_diagnostic(0))
+        eng.set_block_sums_kernel(-1)
+        eng.set_block_sums_diagnostic(0)
         print(json.dumps({"files": nf, "file_bytes": fb, "block_len": blen, "records": plan.total_records,
                           "variants": res}), flush=True)
         plan.close()
@@ -115,7 +115,7 @@ def unaligned():
             eng.synchronize(sp)
         res = {}
         for v, name in VARIANTS_UNALIGNED.items():
-            _lib.check(_lib.lib.rsg_set_block_sums_kernel(v))
+            eng.set_block_sums_kernel(v)
             for i in range(10):
                 plan.run(arenas[i % narena], SEED, recs, stream=sp)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -126,7 +126,7 @@ def unaligned():
             eng.synchronize(sp)
             ms = e0.elapsed_time(e1) / 30
             res[name] = {"kernel_ms": round(ms, 4), "hbm_frac_8tbs": round((nf * fb + plan.total_records * 20) / (ms / 1e3) / 8e12, 4)}
-        _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+        eng.set_block_sums_kernel(-1)
         print(json.dumps({"files": nf, "file_bytes": fb, "block_len": blen, "unaligned": True, "variants": res}), flush=True)
         plan.close()
         for a in arenas:

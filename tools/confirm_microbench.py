@@ -21,7 +21,7 @@ def main():
     rng = np.random.default_rng(1)
     B = 32768
     variant = int(sys.argv[1]) if len(sys.argv) > 1 else -1
-    _lib.check(_lib.lib.rsg_set_block_sums_kernel(variant))
+    eng.set_block_sums_kernel(variant)
     for n in (3072, 6144, 12288, 24576, 49152):
         offs = np.sort(rng.choice(size - 2 * B, n, replace=False)) | 1  # odd: unaligned windows
         files = [(int(o), B, B) for o in offs]
@@ -38,7 +38,7 @@ def main():
         dt = (time.perf_counter() - t0) / reps
         print(json.dumps({"windows": n, "ms": round(dt * 1e3, 4), "variant": variant}), flush=True)
         out.free()
-    _lib.check(_lib.lib.rsg_set_block_sums_kernel(-1))
+    eng.set_block_sums_kernel(-1)
     eng.close()
 
 
