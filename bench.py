@@ -163,7 +163,7 @@ def main():
     if args.ab:
         from rsync_amd import _lib
         # (product variant, diagnostic) pairs; diagnostics write meaningless records
-        names = {(2, 0): "park", (1, 3): "diag_park_memory_only", (1, 4): "diag_park_hash_only",
+        names = {(2, 0): "park", (7, 0): "park_no_join", (1, 3): "diag_park_memory_only", (1, 4): "diag_park_hash_only",
                  (1, 6): "diag_linear_read_ldsdma", (1, 5): "diag_linear_read_plain",
                  (1, 7): "diag_linear_read_ldsdma_misaligned4", (1, 8): "diag_park_memory_only_aligned"}
         res = {v: [] for v in names}
@@ -572,6 +572,9 @@ def bench_sender(args, rank, world, local):
         cpu = {"value": round(P / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
                "sample": f"first {P >> 20} MiB of file 0 vs its basis sums, oracle/rsg_oracle.c orc_hash_search "
                          f"(scalar C restatement of match.go:21-282), 1 thread, {t_cpu:.1f} s"}
+    host_path = None
+    if rank == 0 and world == 1 and not args.no_host_path:
+        host_path = sender_host_path(eng, srcs[0], metas[0], res[0])
     if rank == 0:
         print(json.dumps({"metric": "GiB/s source scanned (sender rolling match), device-resident",
                           "value": round(scanned / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
@@ -596,8 +599,48 @@ def bench_sender(args, rank, world, local):
                                        "candidates_per_launch": kt["candidates"] // max(kt["roll_launches"], 1),
                                        "windows_confirmed_per_launch": kt["windows"] // max(kt["roll_launches"], 1)},
                           "oracle_parity_file0": parity,
+                          "host_path": host_path,
                           "cpu_baseline": cpu}), flush=True)
     eng.close()
+
+
+def sender_host_path(eng, src, meta, dev_res):
+    """The sender from a file (rsg_hash_search_fd, row a13): file 0's source
+    written to /dev/shm (page cache), read by the engine in 256 MiB windows
+    (pread -> pinned -> H2D, overlapped with the search), with and without the
+    whole-file sum MD4(seed || source) (match.go:52-53) computed on a host
+    thread over the same bytes.  PCIe-inclusive; never the line's value."""
+    import tempfile
+    n, head, s1, s2, tg = meta
+    data = src.download(n)
+    tmp = tempfile.mkdtemp(dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    p = os.path.join(tmp, "src0")
+    out = {}
+    try:
+        with open(p, "wb") as fh:
+            fh.write(data.tobytes())
+        del data
+        fd = os.open(p, os.O_RDONLY)
+        try:
+            want = [(int(o), int(i)) for o, i in zip(dev_res["offset"], dev_res["index"])]
+            eng.hash_search_fd(fd, n, head, s1, s2, tg, SEED)  # warm the staging buffers
+            for tag, fs in (("search_only", False), ("with_file_sum", True)):
+                ts = []
+                for _ in range(3):
+                    t0 = time.perf_counter()
+                    r = eng.hash_search_fd(fd, n, head, s1, s2, tg, SEED, file_sum=fs)
+                    ts.append(time.perf_counter() - t0)
+                m = r[0] if fs else r
+                dt = sorted(ts)[1]
+                out[tag] = {"gib_s": round(n / dt / GIB, 3), "s": round(dt, 4), "matches_equal_device_path": m == want}
+        finally:
+            os.close(fd)
+    finally:
+        import shutil
+        shutil.rmtree(tmp, ignore_errors=True)
+    out["sample"] = ("file 0 (1 GiB) in /dev/shm, rsg_hash_search_fd with 256 MiB windows; median of 3; "
+                     "with_file_sum adds MD4(seed || source) on a host thread (one serial chain per file)")
+    return out
 
 
 def cfg3_traffic():

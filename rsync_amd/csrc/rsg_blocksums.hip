@@ -770,7 +770,10 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
 // (A/B, profiles/r02f_ab_park_cache_policy*.json: the default policy, sc0 or
 // sc1 alone cost 6-9 %; nt combined with sc0 / sc1 equals nt.)
 // NL = loader waves (1 or 2); the other 8 - NL waves hash.
-template <int MODE, int NL, int AUX>
+// JOIN: a loader wave whose tiles are all issued and published joins the
+// hashers (the last tiles of a workgroup then wait for no hasher: the drain
+// after the memory stream ends is one tile's hashing, not up to two).
+template <int MODE, int NL, int AUX, bool JOIN = true>
 __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
@@ -851,7 +854,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) pk_store(&sh.full[prev % kPkSlots], prev);
         }
-        return;
+        if (!JOIN) return;
     }
 
     // ---------------------------------------------------------------- hashers
@@ -999,9 +1002,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v == 7)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
-    if (v == 2 && max_blen > kRegMaxBytes) v = 1;
+    if ((v == 2 || v == 7) && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
             hipLaunchKernelGGL((block_sums_staged<0>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
@@ -1010,6 +1013,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes, files,
                                wg_file, nwg, total_blocks, seed, out);
+            break;
+        case 7:  // A/B: park whose loader waves do not join the hashers (round 3's kernel)
+            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, false>), pgrid, pblock, 0, stream, arena, arena_bytes,
+                               files, wg_file, nwg, total_blocks, seed, out);
             break;
         case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel
             if (aligned)
