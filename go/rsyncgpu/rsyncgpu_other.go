@@ -104,3 +104,7 @@ func (nd *Node) BlockSums(files [][]byte, blockLen int32, seed int32) ([]rsync.S
 func (nd *Node) GenerateFiles(files []*os.File, idx []int32, sizes []int64, seed int32, w io.Writer, mux bool) error {
 	return ErrUnavailable
 }
+
+func (e *Engine) HashSearchFile(f *os.File, size int64, head rsync.SumHead, targets []int32, seed int32) ([]Match, [16]byte, error) {
+	return nil, [16]byte{}, ErrUnavailable
+}

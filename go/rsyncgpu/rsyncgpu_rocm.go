@@ -615,3 +615,31 @@ func (nd *Node) GenerateFiles(files []*os.File, idx []int32, sizes []int64, seed
 	runtime.KeepAlive(files)
 	return nd.err(st)
 }
+
+// HashSearchFile replaces hashSearch's byte loop for a source that is an open
+// file, as sendFile has it (sender.go:184-206, fileio.go:31-112): the engine
+// reads [0, size) of f itself in windows (rsg_hash_search_fd), each searched
+// on the GPU while the next is read; a short read is "file has changed
+// mid-transfer".  It also returns the whole-file sum MD4(int32_LE(seed) ||
+// source) (match.go:52-53), which the caller writes after matched(size, -1).
+func (e *Engine) HashSearchFile(f *os.File, size int64, head rsync.SumHead, targets []int32, seed int32) ([]Match, [16]byte, error) {
+	var sum [16]byte
+	sum1, sum2 := sums(head)
+	h := cHead(head)
+	capm := int(size)/max(int(head.BlockLength), 1) + 2
+	ms := make([]C.rsg_match, capm)
+	var nm C.uint64_t
+	var s1p *C.uint32_t
+	var tp *C.int32_t
+	if len(sum1) > 0 {
+		s1p = (*C.uint32_t)(unsafe.Pointer(&sum1[0]))
+		tp = (*C.int32_t)(unsafe.Pointer(&targets[0]))
+	}
+	st := C.rsg_hash_search_fd(e.ctx, C.int32_t(f.Fd()), 0, C.uint64_t(size), &h, s1p, bytePtr(sum2), tp,
+		C.int32_t(seed), &ms[0], C.uint64_t(capm), &nm, (*C.uint8_t)(unsafe.Pointer(&sum[0])))
+	runtime.KeepAlive(f)
+	if st != C.RSG_OK {
+		return nil, sum, e.err(st)
+	}
+	return goMatches(ms[:nm]), sum, nil
+}
