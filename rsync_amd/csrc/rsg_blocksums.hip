@@ -545,7 +545,9 @@ struct PkShared {
     uint32_t n[kPkSlots][64];  // block lengths of the slot's tile
     uint32_t full[kPkSlots];
     uint32_t freeq[kPkSlots];
-    uint32_t kind[kPkSlots];   // 1 = staged in the slot, 0 = direct
+    uint32_t kind[kPkSlots];   // 1 = staged per block, 2 = staged linear (LIN), 0 = direct
+    uint32_t shift[kPkSlots];  // linear: slot byte of the tile's first block
+    uint32_t blen[kPkSlots];   // linear: the tile's block length
     uint32_t ticket;
 };
 
@@ -565,6 +567,8 @@ struct PkDesc {
     uint64_t base;
     uint32_t B, jl, nl;
     bool regular, staged;
+    bool linear;   // LIN kernels: the tile's bytes are DMA'd as one aligned run (see pk_issue_linear)
+    uint32_t lin_bytes;  // bytes from base & ~15 through the tile's last byte
     uint64_t off;  // per lane
     uint32_t n;    // per lane
 };
@@ -593,8 +597,14 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
         d.off = d.base + (uint64_t)d.B * lane;
         const uint64_t top = d.base + (uint64_t)d.B * 63 + 704u;
         d.staged = d.B <= kRegMaxBytes && top <= arena_bytes && top - d.base <= 0x7FFFFFFFull;
+        // the tile's bytes as one 16-byte aligned run: [base & ~15, base + span)
+        const uint64_t span = d.jl < 64 ? (uint64_t)d.B * d.jl + d.nl : (uint64_t)d.B * 64;
+        const uint64_t lin = (d.base & 15u) + span;
+        d.lin_bytes = (uint32_t)((lin + 15) & ~15ull);
+        d.linear = d.staged && ((d.B >> 2) & 1u) && (d.base & ~15ull) + d.lin_bytes <= arena_bytes;
         return;
     }
+    d.linear = false;
     const uint64_t gend = min(g0 + 64, total_blocks);
     const uint32_t fmax = wg_file[nwg256];  // the batch's last block's file: no tile needs a later one
     uint64_t off = 0;
@@ -731,6 +741,26 @@ __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, con
 #undef RSG_PK_ONE
 }
 
+// Linear tile (a regular tile of blocks whose B/4 is odd): the tile's bytes
+// [base & ~15, base + span) as one run of naturally aligned 16-byte quads,
+// instruction i lane l -> slot bytes [1024 i + 16 l, +16) (44 instructions for
+// 64 blocks of <= 703 bytes; quads past the run are dropped by an offset past
+// num_records).  Every request is 16-byte aligned -- blocks at a 700-byte
+// stride put 3 of 4 per-block quads off that alignment -- and the hasher
+// copies block j from slot byte (base & 15) + B j with 4-byte LDS reads,
+// bank (a/4) mod 32 = (const + (B/4) j) mod 32: conflict-free for odd B/4.
+template <int AUX>
+__device__ __forceinline__ void pk_issue_linear(const uint8_t *arena, uint8_t *dst, const PkDesc &d, uint32_t lane) {
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(arena + (d.base & ~15ull)), (short)0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+    for (uint32_t i = 0; i < kPkDma - 1; i++) {
+        const uint32_t vo = 1024u * i + 16u * lane;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * i), 16,
+                                                 vo < d.lin_bytes ? vo : 0x80000000u, 0, 0, AUX);
+    }
+}
+
 // A block of a direct tile: the lane locates and loads it itself.
 __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uint64_t arena_bytes,
                                        const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file,
@@ -773,7 +803,9 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
 // JOIN: a loader wave whose tiles are all issued and published joins the
 // hashers (the last tiles of a workgroup then wait for no hasher: the drain
 // after the memory stream ends is one tile's hashing, not up to two).
-template <int MODE, int NL, int AUX, bool JOIN = true>
+// LIN: regular tiles with odd B/4 travel as one aligned linear run
+// (pk_issue_linear); the others keep the per-block layout.
+template <int MODE, int NL, int AUX, bool JOIN = true, bool LIN = false>
 __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
@@ -823,9 +855,17 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             // the slot's previous tile must have been copied out by its hasher
             while (pk_load(&sh.freeq[slot]) != k) __builtin_amdgcn_s_sleep(1);
             sh.n[slot][lane] = cur.n;
-            if (lane == 0) sh.kind[slot] = cur.staged ? 1u : 0u;
+            const bool lin = LIN && cur.linear;
+            if (lane == 0) {
+                sh.kind[slot] = cur.staged ? (lin ? 2u : 1u) : 0u;
+                sh.shift[slot] = (uint32_t)(cur.base & 15u);
+                sh.blen[slot] = cur.B;
+            }
             const bool staged = cur.staged;
-            if (staged && MODE != 2) pk_issue<AUX, true, MODE == 3>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
+            if (staged && MODE != 2) {
+                if (lin) pk_issue_linear<AUX>(arena, &sh.tile[slot][0], cur, lane);
+                else pk_issue<AUX, true, MODE == 3>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
+            }
             uint32_t kn = k + 1;
             while (!owned(kn)) kn++;
             const uint64_t tn = blockIdx.x + (uint64_t)kn * G;
@@ -841,7 +881,8 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
                 // a 6-bit counter: a wave cannot have more than 63 DMA
                 // instructions (63 KiB) in flight, so waiting for an older
                 // tile instead stalls the issue of this one (measured slower).
-                if (staged) asm volatile("s_waitcnt vmcnt(45)" ::: "memory");
+                if (staged && !lin) asm volatile("s_waitcnt vmcnt(45)" ::: "memory");
+                else if (staged) asm volatile("s_waitcnt vmcnt(44)" ::: "memory");
                 else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) pk_store(&sh.full[prev % kPkSlots], prev);
             }
@@ -876,11 +917,24 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             int32_t s1 = 0;
             uint32_t tw = 0;
             uint32_t R[16 * kRegChunks];
-            const uint8_t *mine = &sh.tile[slot][0] + lane * kPkPiece;
+            if (LIN && kind == 2) {
+                const uint32_t *mine = reinterpret_cast<const uint32_t *>(
+                    &sh.tile[slot][0] + __builtin_amdgcn_readfirstlane(sh.shift[slot]) +
+                    __builtin_amdgcn_readfirstlane(sh.blen[slot]) * lane);
 #pragma unroll
-            for (uint32_t q = 0; q < 4 * kRegChunks; q++) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
-                R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+                for (uint32_t q = 0; q < 16 * kRegChunks; q++) R[q] = mine[q];
+                // keeps the two copy-outs apart: merged behind one selected
+                // address they became 4-byte reads for both layouts (the
+                // per-block layout is conflict-free only with ds_read_b128)
+                asm volatile("" ::: "memory");
+            } else {
+                const uint8_t *mine = &sh.tile[slot][0] + lane * kPkPiece;
+#pragma unroll
+                for (uint32_t q = 0; q < 4 * kRegChunks; q++) {
+                    const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
+                    R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+                }
+                if (LIN) asm volatile("" ::: "memory");
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);
@@ -1002,9 +1056,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v == 7)) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v == 7 || v == 8)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
-    if ((v == 2 || v == 7) && max_blen > kRegMaxBytes) v = 1;
+    if ((v == 2 || v == 7 || v == 8) && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
             hipLaunchKernelGGL((block_sums_staged<0>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
@@ -1013,6 +1067,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes, files,
                                wg_file, nwg, total_blocks, seed, out);
+            break;
+        case 8:  // A/B: park (join) whose regular odd-B/4 tiles travel as aligned linear runs
+            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, true, true>), pgrid, pblock, 0, stream, arena,
+                               arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
             break;
         case 7:  // A/B: park whose loader waves do not join the hashers (round 3's kernel)
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, false>), pgrid, pblock, 0, stream, arena, arena_bytes,
