@@ -471,6 +471,163 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     store_record(out, g, n, s1, t, h);
 }
 
+// ---------------------------------------------------------------- persistent staged variant
+// The staged kernel with persistent waves: a wave hashes 64-block groups
+// grp, grp + stride, ... and issues the next group's first segment into its
+// slab while it hashes the current group's last one, so only the wave's very
+// first segment waits on HBM latency.  With B = 1-4 KiB a group is 4-16
+// segments of 256 bytes; the one-group-per-wave kernel pays a segment's
+// latency, the wave's locate/reductions and its launch per 4-16 segments of
+// work (its memory-only time was 0.209 ms at B = 1024 against 0.170 ms for a
+// linear read of the same arena).  Aligned batches only.
+template <uint32_t SEG>
+struct StagedGroup {
+    uint64_t off;
+    uint32_t n, S, rel;
+    uint64_t base;
+    bool staged, valid;
+};
+
+template <uint32_t SEG>
+__device__ __forceinline__ void staged_setup(uint64_t grp, uint64_t ngroups, StagedGroup<SEG> &G, uint32_t lane,
+                                             const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file,
+                                             uint32_t nwg256, uint64_t total_blocks, uint64_t arena_bytes) {
+    G.valid = grp < ngroups;
+    G.off = 0;
+    G.n = 0;
+    if (!G.valid) return;
+    const uint64_t g = grp * 64 + lane;
+    if (g < total_blocks) {
+        const uint32_t w = (uint32_t)(g >> 8);
+        uint32_t lo = wg_file[w], hi = wg_file[min(w + 1, nwg256)];
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (files[mid].first_block <= g) lo = mid; else hi = mid - 1;
+        }
+        const DevFile F = files[lo];
+        const uint64_t boff = (g - F.first_block) * F.blen;
+        const uint64_t left = F.len - boff;
+        G.n = left < F.blen ? (uint32_t)left : F.blen;
+        G.off = F.offset + boff;
+    }
+    const uint32_t nseg = G.n ? (G.n >> 6) / (SEG / 64) + 1 : 0;
+    G.S = rfl32((uint32_t)wave_max_u64(nseg));
+    G.base = rfl64(wave_min_u64(G.n ? G.off : ~0ull));
+    const uint64_t top = rfl64(wave_max_u64(G.n ? G.off + (uint64_t)SEG * G.S : 0));
+    const bool full = grp * 64 + 63 < total_blocks;
+    G.staged = full && top <= arena_bytes && (top - G.base) <= 0x7FFFFFFFull;
+    G.rel = G.staged ? (uint32_t)(G.off - G.base) : 0u;
+}
+
+template <uint32_t SEG>
+__global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged_persist(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    constexpr int DMA_AUX = 2;  // nt: every byte read once (as block_sums_staged)
+    constexpr uint32_t kSegBytes = Seg<SEG>::kSegBytes, kUnits = Seg<SEG>::kUnits, kPiece = Seg<SEG>::kPiece;
+    constexpr uint32_t kWaveSlab = Seg<SEG>::kWaveSlab, kDmaPerSeg = Seg<SEG>::kDmaPerSeg;
+    constexpr uint32_t kChunks = Seg<SEG>::kChunks;
+    constexpr uint32_t kWaves = kBlockSumThreads / 64;
+    __shared__ __attribute__((aligned(16))) uint8_t slab_all[kWaves * kWaveSlab];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t *slab = slab_all + wave * kWaveSlab;
+    const uint8_t *mine = slab + lane * kPiece;
+    const uint64_t ngroups = (total_blocks + 63) / 64;
+    const uint64_t stride = (uint64_t)gridDim.x * kWaves;
+    uint64_t grp = (uint64_t)blockIdx.x * kWaves + wave;
+    StagedGroup<SEG> cur, nxt;
+    uint32_t voff[kDmaPerSeg];
+    __amdgpu_buffer_rsrc_t rsrc;
+    // the DMA offsets of a staged group (instruction i, lane t -> piece
+    // (64 i + t) / kUnits, unit (64 i + t) % kUnits; the pad unit dropped)
+    auto prepare = [&](const StagedGroup<SEG> &G) {
+        rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(arena + G.base), (short)0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+        for (uint32_t i = 0; i < kDmaPerSeg; i++) {
+            const uint32_t idx = 64u * i + lane;
+            const uint32_t j = idx / kUnits, u = idx - kUnits * j;
+            const uint32_t v = (uint32_t)__shfl((int)G.rel, (int)j, 64) + 16u * u;
+            voff[i] = u + 1 < kUnits ? v : 0x80000000u;
+        }
+    };
+    auto dma = [&](uint32_t seg) {
+        const uint32_t so = kSegBytes * seg;
+#pragma unroll
+        for (uint32_t i = 0; i < kDmaPerSeg; i++)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(slab + 1024u * i),
+                                                     16, voff[i], so, 0, DMA_AUX);
+    };
+    uint32_t R[SEG / 4 + 4];
+    auto read_seg = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < (int)(SEG / 16); q++) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
+            R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+    staged_setup<SEG>(grp, ngroups, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+    if (cur.valid && cur.staged) {
+        prepare(cur);
+        dma(0);
+    }
+#pragma unroll 1
+    while (cur.valid) {
+        const uint64_t g = grp * 64 + lane;
+        const uint64_t ngrp = grp + stride;
+        if (!cur.staged) {
+            if (grp * 64 + 63 < total_blocks && lane == 0) count_fallback(0);
+            if (cur.n) {
+                uint32_t h[4];
+                md4_init(h);
+                int32_t s1 = 0;
+                uint32_t t = 0;
+                hash_block_direct<true>(arena, (uintptr_t)(arena + arena_bytes), cur.off, cur.n, seed, h, s1, t);
+                store_record(out, g, cur.n, s1, t, h);
+            }
+            staged_setup<SEG>(ngrp, ngroups, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+            grp = ngrp;
+            if (cur.valid && cur.staged) {
+                prepare(cur);
+                dma(0);
+            }
+            continue;
+        }
+        read_seg();
+        // the next group's descriptors while this group hashes (its loads
+        // are scalar-free vector loads: the first segment wait below covers them)
+        staged_setup<SEG>(ngrp, ngroups, nxt, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+        const uint32_t n = cur.n, nfull = n >> 6, S = cur.S;
+        uint32_t h[4];
+        md4_init(h);
+        int32_t s1 = 0;
+        uint32_t t = 0;
+#pragma unroll 1
+        for (uint32_t cs = 0; cs < S; cs++) {
+            const bool more = cs + 1 < S;
+            if (more) {
+                dma(cs + 1);  // in flight while segment cs hashes
+            } else if (nxt.valid && nxt.staged) {
+                prepare(nxt);  // the next group's first segment behind this group's last
+                dma(0);
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < kChunks; i++) {
+                const uint32_t c = kChunks * cs + i;
+                if (c < nfull) hash_chunk<true>(R + 16 * i, 0u, 0u, c, h, s1, t);
+                else if (c == nfull) hash_tail<true>(R + 16 * i, 0u, 0u, n, seed, h, s1, t);
+            }
+            if (more) read_seg();
+        }
+        if (n) store_record(out, g, n, s1, t, h);
+        cur = nxt;
+        grp = ngrp;
+    }
+}
+
 // ---------------------------------------------------------------- read ceilings
 // Timing diagnostics only: the fastest way to read the same arena with no
 // hashing, i.e. the empirical HBM-read roofline of this box for DESIGN.md.
@@ -996,6 +1153,23 @@ static uint32_t park_grid(uint64_t total_blocks) {
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus, ntile));
 }
 
+// Workgroups of the persistent staged kernel: every CU's resident share
+// (occupancy from the kernel's LDS and registers), at most one wave per group.
+static uint32_t persist_grid(bool seg128, uint64_t groups) {
+    static int per_cu[2] = {0, 0};
+    int &pc = per_cu[seg128 ? 1 : 0];
+    if (pc == 0) {
+        int nb = 0;
+        const hipError_t e = seg128
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, block_sums_staged_persist<128>, kBlockSumThreads, 0)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, block_sums_staged_persist<256>, kBlockSumThreads, 0);
+        pc = (e == hipSuccess && nb > 0) ? nb : 1;
+    }
+    const uint64_t want = (uint64_t)park_grid(~0ull >> 8) * (uint64_t)pc;
+    const uint64_t need = (groups + kBlockSumThreads / 64 - 1) / (kBlockSumThreads / 64);
+    return (uint32_t)std::max<uint64_t>(1, std::min(want, need));
+}
+
 hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const DevFile *files,
                              const uint32_t *wg_file, uint64_t total_blocks, uint32_t nwg, bool aligned,
                              uint32_t max_blen, uint32_t seed, uint8_t *out, uint32_t *scratch,
@@ -1056,7 +1230,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v == 7 || v == 8)) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v >= 7)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
     if ((v == 2 || v == 7 || v == 8) && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
@@ -1068,6 +1242,18 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes, files,
                                wg_file, nwg, total_blocks, seed, out);
             break;
+        case 9:
+        case 10: {  // A/B: persistent staged (128- / 256-byte segments)
+            const uint64_t groups = (total_blocks + 63) / 64;
+            const uint32_t g = persist_grid(v == 9, groups);
+            if (v == 9)
+                hipLaunchKernelGGL((block_sums_staged_persist<128>), dim3(g), block, 0, stream, arena, arena_bytes,
+                                   files, wg_file, nwg, total_blocks, seed, out);
+            else
+                hipLaunchKernelGGL((block_sums_staged_persist<256>), dim3(g), block, 0, stream, arena, arena_bytes,
+                                   files, wg_file, nwg, total_blocks, seed, out);
+            break;
+        }
         case 8:  // A/B: park (join) whose regular odd-B/4 tiles travel as aligned linear runs
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, true, true>), pgrid, pblock, 0, stream, arena,
                                arena_bytes, files, wg_file, nwg, total_blocks, seed, out);

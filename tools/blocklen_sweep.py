@@ -28,7 +28,8 @@ SHAPES = [  # (files, file bytes, block length, arenas)
     (256, 4 << 20, 4096, 2),      # 4 KiB blocks
     (1, 32 << 30, 131072, 1),     # cfg5's per-GPU share: one 32 GiB file
 ]
-VARIANTS = {1: "staged", 4: "staged_seg128", 5: "staged_seg512", 2: "park", 3: "long_deep_prefetch"}
+VARIANTS = {1: "staged", 4: "staged_seg128", 5: "staged_seg512", 2: "park", 3: "long_deep_prefetch",
+            9: "persist_seg128", 10: "persist_seg256"}
 DIAGS = {1: "diag_staged_memory_only", 2: "diag_staged_hash_only", 6: "diag_linear_read_ldsdma"}
 
 
@@ -41,7 +42,11 @@ def main():
     eng = rsync_amd.Engine(0)
     stream = torch.cuda.Stream()
     sp = stream.cuda_stream
-    for nf, fb, blen, narena in SHAPES:
+    # SWEEP_SHAPES="1,2": only those entries of SHAPES; SWEEP_ROUNDS: interleaved rounds
+    pick = os.environ.get("SWEEP_SHAPES")
+    shapes = [SHAPES[int(k)] for k in pick.split(",")] if pick else SHAPES
+    rounds = int(os.environ.get("SWEEP_ROUNDS", "1"))
+    for nf, fb, blen, narena in shapes:
         total = nf * fb
         arenas = [eng.alloc(total) for _ in range(narena)]
         for k, a in enumerate(arenas):
@@ -62,7 +67,7 @@ def main():
         while time.perf_counter() - w0 < 0.3:
             plan.run(arenas[0], SEED, recs, stream=sp)
             eng.synchronize(sp)
-        for v, d, name in runs:
+        for v, d, name in [r for _ in range(rounds) for r in runs]:
             eng.set_block_sums_kernel(v)
             eng.set_block_sums_diagnostic(d)
             steps = 5 if total > (4 << 30) else 30
@@ -77,8 +82,12 @@ def main():
             e1.record(stream)
             eng.synchronize(sp)
             ms = e0.elapsed_time(e1) / steps
-            res[name] = {"kernel_ms": round(ms, 4), "gib_s": round(total / 2**30 / (ms / 1e3), 1),
-                         "hbm_frac_8tbs": round((total + plan.total_records * 20) / (ms / 1e3) / 8e12, 4)}
+            r = {"kernel_ms": round(ms, 4), "gib_s": round(total / 2**30 / (ms / 1e3), 1),
+                 "hbm_frac_8tbs": round((total + plan.total_records * 20) / (ms / 1e3) / 8e12, 4)}
+            if name in res:  # interleaved rounds: keep every round's time
+                prev = res[name]
+                r["rounds_ms"] = prev.get("rounds_ms", [prev["kernel_ms"]]) + [r["kernel_ms"]]
+            res[name] = r
         eng.set_block_sums_kernel(-1)
         eng.set_block_sums_diagnostic(0)
         print(json.dumps({"files": nf, "file_bytes": fb, "block_len": blen, "records": plan.total_records,
