@@ -38,6 +38,19 @@ BLOCK_LEN = 700
 SEED = 0x1BADB002
 
 
+def cpu_model() -> str:
+    """The host CPU the CPU baseline ran on (state the model)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -333,7 +346,7 @@ def main():
                 got = recs.download(1498 * 20, offset=plan.first_record[f] * 20)
                 sample_parity &= bool((got == out).all())
             f += 1
-        cpu = {"value": round(done_bytes / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+        cpu = {"value": round(done_bytes / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
                "sample": f"{f} x 1 MiB files (cycling the first 64 of the workload's files) at B=700, "
                          f"oracle/rsg_oracle.c orc_block_sums (scalar C restatement of generator.go:325-350), "
                          f"1 thread, {t_cpu:.1f} s",
@@ -363,7 +376,7 @@ def main():
             t.join()
         wdt = time.perf_counter() - w0
         extra["cpu_baseline_all_cores"] = {
-            "value": round(sum(counts) / wdt / GIB, 4), "unit": "GiB/s", "cores": T, "kind": "port",
+            "value": round(sum(counts) / wdt / GIB, 4), "unit": "GiB/s", "cores": T, "kind": "port", "cpu_model": cpu_model(),
             "sample": f"{sum(counts) // FILE_BYTES} x 1 MiB files on {T} threads (files partitioned), "
                       f"same orc_block_sums, {wdt:.1f} s wall"}
 
@@ -569,7 +582,7 @@ def bench_sender(args, rank, world, local):
         gm = [(int(o), int(i)) for o, i in zip(res[0]["offset"], res[0]["index"])]
         want = [m for m in om if m[0] + B0 <= cut]
         parity = {"matches_compared": len(want), "equal": want == [m for m in gm if m[0] + B0 <= cut]}
-        cpu = {"value": round(P / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+        cpu = {"value": round(P / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
                "sample": f"first {P >> 20} MiB of file 0 vs its basis sums, oracle/rsg_oracle.c orc_hash_search "
                          f"(scalar C restatement of match.go:21-282), 1 thread, {t_cpu:.1f} s"}
     host_path = None
@@ -749,7 +762,7 @@ def bench_mixed(args, rank, world, local):
             if k < 64:
                 parity &= bool((recs.download(cnt * 20, offset=first[j] * 20) == out).all())
             k += 1
-        cpu = {"value": round(done / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+        cpu = {"value": round(done / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
                "sample": f"{k} pieces of rank 0's cfg4 shard at B=700, oracle/rsg_oracle.c orc_block_sums, "
                          f"1 thread, {t_cpu:.1f} s", "gpu_parity_on_sample": parity}
     algo = my_bytes + sb.my_records * rsync_amd.RECORD_BYTES
@@ -848,7 +861,7 @@ def bench_long(args, rank, world, local):
             t_cpu += time.perf_counter() - c0
             parity &= bool((got_all[b] == out).all())
         if not args.no_cpu:
-            cpu = {"value": round(len(sample) * B / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            cpu = {"value": round(len(sample) * B / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
                    "sample": f"{len(sample)} sampled 128 KiB blocks of rank 0's file (1024 random + the last), "
                              f"oracle/rsg_oracle.c orc_block_sums, 1 thread, {t_cpu:.1f} s"}
         algo = size + nrec * rsync_amd.RECORD_BYTES
@@ -956,7 +969,7 @@ def bench_filesums(args, rank, world, local):
                      "kernel_ms": res["seeded"]["kernel_ms"], "algorithmic_bytes_per_launch": int(total),
                      "note": "value = per call (descriptor staging + lane order + upload + launch + wait); "
                              "roofline = the kernel alone (HIP events)"},
-        "cpu_baseline": {"value": round(done / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+        "cpu_baseline": {"value": round(done / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
                          "sample": f"{k} random files of the set, oracle/rsg_oracle.c orc_file_sum (plain), "
                                    f"1 thread, {t_cpu:.1f} s"}}), flush=True)
     eng.close()
