@@ -607,6 +607,7 @@ def bench_sender(args, rank, world, local):
                                        "traffic": cfg3_traffic(), "kernel_ms": round(roll_ms, 4),
                                        "launches": kt["roll_launches"],
                                        "algorithmic_bytes_per_launch": int(src_bytes),
+                                       "valu_issue": roll_valu_issue(roll_ms, world),
                                        "confirm_ms_per_batch": round(confirm_ms, 4),
                                        "confirm_batches": kt["confirm_batches"],
                                        "candidates_per_launch": kt["candidates"] // max(kt["roll_launches"], 1),
@@ -654,6 +655,24 @@ def sender_host_path(eng, src, meta, dev_res):
     out["sample"] = ("file 0 (1 GiB) in /dev/shm, rsg_hash_search_fd with 256 MiB windows; median of 3; "
                      "with_file_sum adds MD4(seed || source) on a host thread (one serial chain per file)")
     return out
+
+
+def roll_valu_issue(roll_ms, world):
+    """The roll's VALU-issue bound (it is VALU-issue-bound, not HBM-bound,
+    DESIGN.md §4.2): SQ_INSTS_VALU per launch from the committed PMC pass of
+    the cfg3 bench (profiles/counters.json; not measured in this run) x 2
+    cycles per wave64 instruction (two waves interleaving,
+    MI355X_MICROARCH.md) / the SIMDs of the roll's CUs / the clock -> the
+    floor; frac = floor / the measured roll time."""
+    try:
+        c = json.load(open(os.path.join(ROOT, "profiles", "counters.json")))["roll_packed_kernel_cfg3"]
+    except Exception:
+        return None
+    simds = 4 * int(c["roll_cus"])
+    floor_ms = float(c["valu_wave_insts_per_launch"]) * 2 / simds / (float(c["clock_ghz"]) * 1e9) * 1e3
+    return {"valu_wave_insts_per_launch": c["valu_wave_insts_per_launch"], "simds": simds,
+            "clock_ghz": c["clock_ghz"], "floor_ms": round(floor_ms, 4), "frac": round(floor_ms / roll_ms, 4),
+            "source": c.get("source")}
 
 
 def cfg3_traffic():
