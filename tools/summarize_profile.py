@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--kernel", default="block_sums", help="substring of the kernel name to summarize")
     ap.add_argument("--no-traffic", action="store_true", help="do not rewrite profiles/traffic.json")
     ap.add_argument("--outdir", default="profiles")
+    ap.add_argument("--roll-cus", type=int, default=224,
+                    help="CUs the roll's workgroups occupy (cfg3 batch: all but RSG_CONFIRM_CUS = 32 of 256)")
     a = ap.parse_args()
     tag, kernel, outdir = a.tag, a.kernel, a.outdir
     src = f"gpurun_out/prof_{tag}"
@@ -60,9 +62,31 @@ def main():
         out["note_units"] = "SQ_* wave/active counters count quad-cycles (MI355X_MICROARCH.md constants table)"
     os.makedirs(outdir, exist_ok=True)
     json.dump(out, open(f"{outdir}/{tag}_summary.json", "w"), indent=1)
+    def merge(name, upd):
+        path = f"{outdir}/{name}"
+        cur = json.load(open(path)) if os.path.exists(path) else {}
+        cur.update(upd)
+        json.dump(cur, open(path, "w"), indent=1)
+
     if "hbm_bytes_per_launch" in out and kernel == "block_sums" and not a.no_traffic:
-        json.dump({"block_sums_kernel_cfg2_bytes_per_launch": out["hbm_bytes_per_launch"]["total"],
-                   "source": f"profiles/{tag}_summary.json"}, open(f"{outdir}/traffic.json", "w"), indent=1)
+        merge("traffic.json", {"block_sums_kernel_cfg2_bytes_per_launch": out["hbm_bytes_per_launch"]["total"],
+                               "source": f"profiles/{tag}_summary.json"})
+    if "roll" in kernel and not a.no_traffic:
+        if "FETCH_SIZE" in avg:
+            merge("traffic.json", {"roll_packed_kernel_cfg3_bytes_per_launch": int(avg["FETCH_SIZE"] * 1024 * 2),
+                                   "roll_packed_kernel_cfg3_source": f"profiles/{tag}_summary.json: FETCH_SIZE x 2 "
+                                   "(the gfx950 correction) per roll launch over a 1 GiB cfg3 source"})
+        if "SQ_INSTS_VALU" in avg:
+            merge("counters.json", {"roll_packed_kernel_cfg3": {
+                "valu_wave_insts_per_launch": int(avg["SQ_INSTS_VALU"]),
+                "salu_insts_per_launch": int(avg.get("SQ_INSTS_SALU", 0)),
+                "branch_insts_per_launch": int(avg.get("SQ_INSTS_BRANCH", 0)),
+                "lds_bank_conflict_frac": round(avg["SQ_LDS_BANK_CONFLICT"] / avg["SQ_LDS_IDX_ACTIVE"], 4)
+                if avg.get("SQ_LDS_IDX_ACTIVE") else None,
+                "clock_ghz": out.get("effective_clock_ghz") or 2.4,
+                "roll_cus": a.roll_cus,
+                "kernel_us_mean": out["us_mean"],
+                "source": f"profiles/{tag}_summary.json (rocprofv3 --pmc passes of bench.py --workload cfg3)"}})
     print(json.dumps(out, indent=1)[:3000])
 
 
