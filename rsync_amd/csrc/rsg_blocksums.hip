@@ -693,6 +693,7 @@ constexpr uint32_t kPkPiece = 720;                // LDS bytes per block (44 dat
 constexpr uint32_t kPkTile = 64 * kPkPiece;       // 46080 B
 constexpr uint32_t kPkDma = kPkTile / 1024;       // 45 DMA instructions per tile
 constexpr uint32_t kPkSlots = 3;
+constexpr uint32_t kParkLoaders2 = 3;  // the two-part kernel: one loader per slot
 constexpr uint32_t kPkWaves = 8;
 constexpr uint32_t kPkThreads = 64 * kPkWaves;
 static_assert(kPkTile % 1024 == 0 && kPkPiece % 16 == 0, "tile = whole DMA instructions");
@@ -730,6 +731,9 @@ struct PkDesc {
     uint32_t n;    // per lane
 };
 
+// EXT: bytes read past a block's start (704: one 720-byte piece of 44 data
+// quads; 1408 for the two-part kernel), MAXB: the largest block it stages.
+template <uint32_t EXT = 704u, uint32_t MAXB = kRegMaxBytes>
 __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, const DevFile *__restrict__ files,
                                           const uint32_t *__restrict__ wg_file, uint32_t nwg256,
                                           uint64_t total_blocks, uint64_t arena_bytes) {
@@ -752,8 +756,8 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
         d.nl = (uint32_t)(F0.len - (uint64_t)(F0.nblocks - 1) * F0.blen);
         d.n = lane == d.jl ? d.nl : d.B;
         d.off = d.base + (uint64_t)d.B * lane;
-        const uint64_t top = d.base + (uint64_t)d.B * 63 + 704u;
-        d.staged = d.B <= kRegMaxBytes && top <= arena_bytes && top - d.base <= 0x7FFFFFFFull;
+        const uint64_t top = d.base + (uint64_t)d.B * 63 + EXT;
+        d.staged = d.B <= MAXB && top <= arena_bytes && top - d.base <= 0x7FFFFFFFull;
         // the tile's bytes as one 16-byte aligned run: [base & ~15, base + span)
         const uint64_t span = d.jl < 64 ? (uint64_t)d.B * d.jl + d.nl : (uint64_t)d.B * 64;
         const uint64_t lin = (d.base & 15u) + span;
@@ -794,7 +798,7 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
             if (fe > fb && fe > g0 && fb < gend) {  // the file has blocks in this tile
                 const uint64_t b_first = (g0 > fb ? g0 : fb) - fb, b_last = (gend < fe ? gend : fe) - 1 - fb;
                 const uint64_t o_first = F[i].offset + b_first * F[i].blen;
-                const uint64_t o_top = F[i].offset + b_last * F[i].blen + 704u;
+                const uint64_t o_top = F[i].offset + b_last * F[i].blen + EXT;
                 lo_off = o_first < lo_off ? o_first : lo_off;
                 top = o_top > top ? o_top : top;
                 bmax = F[i].blen > bmax ? F[i].blen : bmax;
@@ -805,7 +809,7 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
     d.base = rfl64(lo_off);
     top = rfl64(top);
     bmax = rfl32(bmax);
-    d.staged = (g0 + 64 <= total_blocks) && bmax <= kRegMaxBytes && top <= arena_bytes &&
+    d.staged = (g0 + 64 <= total_blocks) && bmax <= MAXB && top <= arena_bytes &&
                top - d.base <= 0x7FFFFFFFull;
     d.off = off;
     d.n = n;
@@ -819,9 +823,12 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
 // jj/uu: per-lane block index and byte offset (0x40000000 for the pad) of
 // each instruction, precomputed by the loader (UNROLL); otherwise computed on
 // the fly (a caller short of VGPRs).
+// poff: the part of each block this issue fetches starts poff bytes in (the
+// two-part kernel's second part: 704).
 template <int AUX, bool UNROLL, bool ALN = false>
 __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, const PkDesc &d, uint32_t lane,
-                                         const uint32_t *jj = nullptr, const uint32_t *uu = nullptr) {
+                                         const uint32_t *jj = nullptr, const uint32_t *uu = nullptr,
+                                         uint32_t poff = 0) {
     // ALN (timing diagnostic only): every quad request rounded down to a
     // 16-byte boundary of the arena -- the same bytes per tile, naturally
     // aligned, to price the misaligned quads of blocks at a 700-byte stride
@@ -844,11 +851,12 @@ __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, con
         uint32_t vo_;                                                                                           \
         if (REG) {                                                                                              \
             const uint32_t nj_ = j_ == d.jl ? d.nl : d.B;                                                       \
-            vo_ = u16_ < nj_ ? (ALN ? ((d.B * j_ + u16_ + amis) & ~15u) : d.B * j_ + u16_) : 0x80000000u;     \
+            vo_ = u16_ + poff < nj_ ? (ALN ? ((d.B * j_ + u16_ + amis) & ~15u) : d.B * j_ + poff + u16_)      \
+                                    : 0x80000000u;                                                              \
         } else {                                                                                                \
             const uint32_t rj_ = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * j_), rel);                  \
             const uint32_t nj_ = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * j_), (int)d.n);             \
-            vo_ = u16_ < nj_ ? rj_ + u16_ : 0x80000000u;                                                        \
+            vo_ = u16_ + poff < nj_ ? rj_ + poff + u16_ : 0x80000000u;                                          \
         }                                                                                                       \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * (I_)), \
                                                  16, vo_, 0, 0, AUX);                                           \
@@ -884,7 +892,8 @@ __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, con
 #pragma unroll
                 for (uint32_t k = 0; k < kBatch; k++) {
                     const uint32_t u16 = uu[i0 + k];
-                    const uint32_t vo = u16 < nj[k] ? (ALN ? ((rj[k] + u16 + amis) & ~15u) : rj[k] + u16) : 0x80000000u;
+                    const uint32_t vo = u16 + poff < nj[k] ? (ALN ? ((rj[k] + u16 + amis) & ~15u) : rj[k] + poff + u16)
+                                                           : 0x80000000u;
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(
                         rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * (i0 + k)), 16, vo, 0, 0, AUX);
                 }
@@ -1118,6 +1127,123 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
 }
 
 
+// ---------------------------------------------------------------- two-part park (704 < B <= 1407)
+// The park kernel for blocks longer than one parked piece (the reference's
+// own sizing gives B = 1024 for 1 MiB files, rsynccommon.go:22): a tile's
+// 64 blocks travel as two tickets, part 0 = the first 704 bytes of every
+// block (11 chunks) and part 1 = the rest (<= 703 bytes), each in the
+// park's 720-byte-per-block slot layout.  A hasher takes a tile, copies part
+// 0 into its registers, frees the slot, hashes chunks 0..10, then copies part
+// 1 (which the loaders fetched meanwhile) and hashes the rest and the tail.
+// Loader L owns slot L and loads tickets k = L, L + 3, ... (tile k / 2,
+// part k % 2).  No wait cycle: a hasher frees each slot right after its
+// copy-out, before it waits for its next part.
+constexpr uint32_t kPark2MaxBytes = 2 * 64 * kRegChunks - 1;  // 1407
+
+template <int AUX>
+__global__ __launch_bounds__(kPkThreads) void block_sums_park2(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    constexpr uint32_t NL = kParkLoaders2;
+    __shared__ __attribute__((aligned(16))) PkShared sh;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x < kPkSlots) {
+        sh.full[threadIdx.x] = ~0u;
+        sh.freeq[threadIdx.x] = threadIdx.x;
+    }
+    if (threadIdx.x == 0) sh.ticket = 0;
+    __syncthreads();
+    const uint64_t ntiles = (total_blocks + 63) / 64;
+    const uint32_t G = gridDim.x;
+    if (wave < NL) {
+        uint32_t jj[kPkDma], uu[kPkDma];
+#pragma unroll
+        for (uint32_t i = 0; i < kPkDma; i++) {
+            const uint32_t idx = 64u * i + lane;
+            jj[i] = idx / 45u;
+            const uint32_t u = idx - 45u * jj[i];
+            uu[i] = u < 44u ? 16u * u : 0x40000000u;
+        }
+        uint32_t k = wave;  // tickets k = wave + 3 m
+        PkDesc cur;
+        uint64_t t = blockIdx.x + (uint64_t)(k >> 1) * G;
+        if (t < ntiles) pk_locate<1408u, kPark2MaxBytes>(t, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+#pragma unroll 1
+        while (t < ntiles) {
+            const uint32_t slot = k % kPkSlots;
+            while (pk_load(&sh.freeq[slot]) != k) __builtin_amdgcn_s_sleep(1);
+            if ((k & 1u) == 0) sh.n[slot][lane] = cur.n;
+            if (lane == 0) sh.kind[slot] = cur.staged ? 1u : 0u;
+            if (cur.staged) pk_issue<AUX, true>(arena, &sh.tile[slot][0], cur, lane, jj, uu, (k & 1u) * 704u);
+            // the next ticket (k + 3: another tile) while this one is in flight
+            const uint32_t kn = k + kPkSlots;
+            const uint64_t tn = blockIdx.x + (uint64_t)(kn >> 1) * G;
+            if (tn < ntiles)
+                pk_locate<1408u, kPark2MaxBytes>(tn, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+            // one slot per loader: publish before waiting for the slot again
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) pk_store(&sh.full[slot], k);
+            k = kn;
+            t = tn;
+        }
+    }
+    // ---------------------------------------------------------------- hashers (and, once done, the loaders)
+#pragma unroll 1
+    for (;;) {
+        uint32_t i = 0;
+        if (lane == 0) i = __hip_atomic_fetch_add(&sh.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        i = __builtin_amdgcn_readfirstlane(i);
+        const uint64_t t = blockIdx.x + (uint64_t)i * G;
+        if (t >= ntiles) break;
+        const uint64_t g = t * 64 + lane;
+        uint32_t h[4];
+        md4_init(h);
+        int32_t s1 = 0;
+        uint32_t tw = 0;
+        uint32_t n = 0;
+        bool direct = false;
+#pragma unroll 1
+        for (uint32_t p = 0; p < 2; p++) {
+            const uint32_t k = 2 * i + p;
+            const uint32_t slot = k % kPkSlots;
+            while (pk_load(&sh.full[slot]) != k) __builtin_amdgcn_s_sleep(1);
+            if (p == 0) n = sh.n[slot][lane];
+            const uint32_t kind = __builtin_amdgcn_readfirstlane(sh.kind[slot]);
+            if (!kind) {
+                if (lane == 0) {
+                    pk_store(&sh.freeq[slot], k + kPkSlots);
+                    if (p == 0 && t * 64 + 64 <= total_blocks) count_fallback(1);
+                }
+                direct = true;
+                continue;
+            }
+            uint32_t R[16 * kRegChunks];
+            const uint8_t *mine = &sh.tile[slot][0] + lane * kPkPiece;
+#pragma unroll
+            for (uint32_t q = 0; q < 4 * kRegChunks; q++) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
+                R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);
+            const uint32_t nfull = n >> 6;
+#pragma unroll
+            for (uint32_t q = 0; q < kRegChunks; q++) {
+                const uint32_t c = kRegChunks * p + q;
+                if (c < nfull) hash_chunk<true>(R + 16 * q, 0u, 0u, c, h, s1, tw);
+                else if (c == nfull) hash_tail<true>(R + 16 * q, 0u, 0u, n, seed, h, s1, tw);
+            }
+        }
+        if (direct) {
+            if (g < total_blocks) pk_direct(arena, arena_bytes, files, wg_file, nwg256, g, seed, out);
+        } else {
+            store_record(out, g, n, s1, tw, h);
+        }
+    }
+}
+
 // Kernel variants (rsg_set_block_sums_kernel; identical results, only speed
 // differs): -1 = automatic, 0 = direct per-lane loads, 1 = staged LDS-DMA
 // slabs (256-byte segments), 2 = park (three loader waves + five hashers with
@@ -1233,6 +1359,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v >= 7)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
     if ((v == 2 || v == 7 || v == 8) && max_blen > kRegMaxBytes) v = 1;
+    if (v == 11 && max_blen > kPark2MaxBytes) v = 1;
     switch (v) {
         case 1:
             hipLaunchKernelGGL((block_sums_staged<0>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
@@ -1241,6 +1368,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes, files,
                                wg_file, nwg, total_blocks, seed, out);
+            break;
+        case 11:  // A/B: two-part park (704 < B <= 1407)
+            hipLaunchKernelGGL((block_sums_park2<2>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file, nwg,
+                               total_blocks, seed, out);
             break;
         case 9:
         case 10: {  // A/B: persistent staged (128- / 256-byte segments)
