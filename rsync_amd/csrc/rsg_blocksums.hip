@@ -538,7 +538,10 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged_persist(
     const uint64_t stride = (uint64_t)gridDim.x * kWaves;
     uint64_t grp = (uint64_t)blockIdx.x * kWaves + wave;
     StagedGroup<SEG> cur, nxt;
-    uint32_t voff[kDmaPerSeg];
+    // fixed bounds (entries past kDmaPerSeg / SEG / 4 + 4 are dead): an array
+    // sized by a template-dependent constant makes hipcc's host pass drop the
+    // kernel's launch stub (as in block_sums_staged)
+    uint32_t voff[Seg<256>::kDmaPerSeg];
     __amdgpu_buffer_rsrc_t rsrc;
     // the DMA offsets of a staged group (instruction i, lane t -> piece
     // (64 i + t) / kUnits, unit (64 i + t) % kUnits; the pad unit dropped)
@@ -559,7 +562,7 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged_persist(
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(slab + 1024u * i),
                                                      16, voff[i], so, 0, DMA_AUX);
     };
-    uint32_t R[SEG / 4 + 4];
+    uint32_t R[Seg<256>::kSegBytes / 4 + 4];
     auto read_seg = [&]() {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
