@@ -331,9 +331,9 @@ def test_kernel_knobs_are_per_context():
         _, rec_a, _ = a.block_sums(files, cases.SEED, 700)
         assert rec_a == rec
         with pytest.raises(rsync_amd.RsgError):
-            a.set_block_sums_kernel(7)
+            a.set_block_sums_kernel(99)
         with pytest.raises(rsync_amd.RsgError):
-            a.set_block_sums_diagnostic(9)
+            a.set_block_sums_diagnostic(99)
     finally:
         a.close()
         b.close()
