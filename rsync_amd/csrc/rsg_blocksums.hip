@@ -471,166 +471,6 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     store_record(out, g, n, s1, t, h);
 }
 
-// ---------------------------------------------------------------- persistent staged variant
-// The staged kernel with persistent waves: a wave hashes 64-block groups
-// grp, grp + stride, ... and issues the next group's first segment into its
-// slab while it hashes the current group's last one, so only the wave's very
-// first segment waits on HBM latency.  With B = 1-4 KiB a group is 4-16
-// segments of 256 bytes; the one-group-per-wave kernel pays a segment's
-// latency, the wave's locate/reductions and its launch per 4-16 segments of
-// work (its memory-only time was 0.209 ms at B = 1024 against 0.170 ms for a
-// linear read of the same arena).  Aligned batches only.
-template <uint32_t SEG>
-struct StagedGroup {
-    uint64_t off;
-    uint32_t n, S, rel;
-    uint64_t base;
-    bool staged, valid;
-};
-
-template <uint32_t SEG>
-__device__ __forceinline__ void staged_setup(uint64_t grp, uint64_t ngroups, StagedGroup<SEG> &G, uint32_t lane,
-                                             const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file,
-                                             uint32_t nwg256, uint64_t total_blocks, uint64_t arena_bytes) {
-    G.valid = grp < ngroups;
-    G.off = 0;
-    G.n = 0;
-    if (!G.valid) return;
-    const uint64_t g = grp * 64 + lane;
-    if (g < total_blocks) {
-        const uint32_t w = (uint32_t)(g >> 8);
-        uint32_t lo = wg_file[w], hi = wg_file[min(w + 1, nwg256)];
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (files[mid].first_block <= g) lo = mid; else hi = mid - 1;
-        }
-        const DevFile F = files[lo];
-        const uint64_t boff = (g - F.first_block) * F.blen;
-        const uint64_t left = F.len - boff;
-        G.n = left < F.blen ? (uint32_t)left : F.blen;
-        G.off = F.offset + boff;
-    }
-    const uint32_t nseg = G.n ? (G.n >> 6) / (SEG / 64) + 1 : 0;
-    G.S = rfl32((uint32_t)wave_max_u64(nseg));
-    G.base = rfl64(wave_min_u64(G.n ? G.off : ~0ull));
-    const uint64_t top = rfl64(wave_max_u64(G.n ? G.off + (uint64_t)SEG * G.S : 0));
-    const bool full = grp * 64 + 63 < total_blocks;
-    G.staged = full && top <= arena_bytes && (top - G.base) <= 0x7FFFFFFFull;
-    G.rel = G.staged ? (uint32_t)(G.off - G.base) : 0u;
-}
-
-template <uint32_t SEG>
-__global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged_persist(
-    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
-    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
-    uint8_t *__restrict__ out) {
-    constexpr int DMA_AUX = 2;  // nt: every byte read once (as block_sums_staged)
-    constexpr uint32_t kSegBytes = Seg<SEG>::kSegBytes, kUnits = Seg<SEG>::kUnits, kPiece = Seg<SEG>::kPiece;
-    constexpr uint32_t kWaveSlab = Seg<SEG>::kWaveSlab, kDmaPerSeg = Seg<SEG>::kDmaPerSeg;
-    constexpr uint32_t kChunks = Seg<SEG>::kChunks;
-    constexpr uint32_t kWaves = kBlockSumThreads / 64;
-    __shared__ __attribute__((aligned(16))) uint8_t slab_all[kWaves * kWaveSlab];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint8_t *slab = slab_all + wave * kWaveSlab;
-    const uint8_t *mine = slab + lane * kPiece;
-    const uint64_t ngroups = (total_blocks + 63) / 64;
-    const uint64_t stride = (uint64_t)gridDim.x * kWaves;
-    uint64_t grp = (uint64_t)blockIdx.x * kWaves + wave;
-    StagedGroup<SEG> cur, nxt;
-    // fixed bounds (entries past kDmaPerSeg / SEG / 4 + 4 are dead): an array
-    // sized by a template-dependent constant makes hipcc's host pass drop the
-    // kernel's launch stub (as in block_sums_staged)
-    uint32_t voff[Seg<256>::kDmaPerSeg];
-    __amdgpu_buffer_rsrc_t rsrc;
-    // the DMA offsets of a staged group (instruction i, lane t -> piece
-    // (64 i + t) / kUnits, unit (64 i + t) % kUnits; the pad unit dropped)
-    auto prepare = [&](const StagedGroup<SEG> &G) {
-        rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(arena + G.base), (short)0, 0x7FFFFFFF, 0x00020000);
-#pragma unroll
-        for (uint32_t i = 0; i < kDmaPerSeg; i++) {
-            const uint32_t idx = 64u * i + lane;
-            const uint32_t j = idx / kUnits, u = idx - kUnits * j;
-            const uint32_t v = (uint32_t)__shfl((int)G.rel, (int)j, 64) + 16u * u;
-            voff[i] = u + 1 < kUnits ? v : 0x80000000u;
-        }
-    };
-    auto dma = [&](uint32_t seg) {
-        const uint32_t so = kSegBytes * seg;
-#pragma unroll
-        for (uint32_t i = 0; i < kDmaPerSeg; i++)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(slab + 1024u * i),
-                                                     16, voff[i], so, 0, DMA_AUX);
-    };
-    uint32_t R[Seg<256>::kSegBytes / 4 + 4];
-    auto read_seg = [&]() {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int q = 0; q < (int)(SEG / 16); q++) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
-            R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    };
-    staged_setup<SEG>(grp, ngroups, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
-    if (cur.valid && cur.staged) {
-        prepare(cur);
-        dma(0);
-    }
-#pragma unroll 1
-    while (cur.valid) {
-        const uint64_t g = grp * 64 + lane;
-        const uint64_t ngrp = grp + stride;
-        if (!cur.staged) {
-            if (grp * 64 + 63 < total_blocks && lane == 0) count_fallback(0);
-            if (cur.n) {
-                uint32_t h[4];
-                md4_init(h);
-                int32_t s1 = 0;
-                uint32_t t = 0;
-                hash_block_direct<true>(arena, (uintptr_t)(arena + arena_bytes), cur.off, cur.n, seed, h, s1, t);
-                store_record(out, g, cur.n, s1, t, h);
-            }
-            staged_setup<SEG>(ngrp, ngroups, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
-            grp = ngrp;
-            if (cur.valid && cur.staged) {
-                prepare(cur);
-                dma(0);
-            }
-            continue;
-        }
-        read_seg();
-        // the next group's descriptors while this group hashes (its loads
-        // are scalar-free vector loads: the first segment wait below covers them)
-        staged_setup<SEG>(ngrp, ngroups, nxt, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
-        const uint32_t n = cur.n, nfull = n >> 6, S = cur.S;
-        uint32_t h[4];
-        md4_init(h);
-        int32_t s1 = 0;
-        uint32_t t = 0;
-#pragma unroll 1
-        for (uint32_t cs = 0; cs < S; cs++) {
-            const bool more = cs + 1 < S;
-            if (more) {
-                dma(cs + 1);  // in flight while segment cs hashes
-            } else if (nxt.valid && nxt.staged) {
-                prepare(nxt);  // the next group's first segment behind this group's last
-                dma(0);
-            }
-#pragma unroll
-            for (uint32_t i = 0; i < kChunks; i++) {
-                const uint32_t c = kChunks * cs + i;
-                if (c < nfull) hash_chunk<true>(R + 16 * i, 0u, 0u, c, h, s1, t);
-                else if (c == nfull) hash_tail<true>(R + 16 * i, 0u, 0u, n, seed, h, s1, t);
-            }
-            if (more) read_seg();
-        }
-        if (n) store_record(out, g, n, s1, t, h);
-        cur = nxt;
-        grp = ngrp;
-    }
-}
-
 // ---------------------------------------------------------------- read ceilings
 // Timing diagnostics only: the fastest way to read the same arena with no
 // hashing, i.e. the empirical HBM-read roofline of this box for DESIGN.md.
@@ -696,7 +536,6 @@ constexpr uint32_t kPkPiece = 720;                // LDS bytes per block (44 dat
 constexpr uint32_t kPkTile = 64 * kPkPiece;       // 46080 B
 constexpr uint32_t kPkDma = kPkTile / 1024;       // 45 DMA instructions per tile
 constexpr uint32_t kPkSlots = 3;
-constexpr uint32_t kParkLoaders2 = 3;  // the two-part kernel: one loader per slot
 constexpr uint32_t kPkWaves = 8;
 constexpr uint32_t kPkThreads = 64 * kPkWaves;
 static_assert(kPkTile % 1024 == 0 && kPkPiece % 16 == 0, "tile = whole DMA instructions");
@@ -706,9 +545,7 @@ struct PkShared {
     uint32_t n[kPkSlots][64];  // block lengths of the slot's tile
     uint32_t full[kPkSlots];
     uint32_t freeq[kPkSlots];
-    uint32_t kind[kPkSlots];   // 1 = staged per block, 2 = staged linear (LIN), 0 = direct
-    uint32_t shift[kPkSlots];  // linear: slot byte of the tile's first block
-    uint32_t blen[kPkSlots];   // linear: the tile's block length
+    uint32_t kind[kPkSlots];   // 1 = staged in the slot, 0 = direct
     uint32_t ticket;
 };
 
@@ -728,15 +565,10 @@ struct PkDesc {
     uint64_t base;
     uint32_t B, jl, nl;
     bool regular, staged;
-    bool linear;   // LIN kernels: the tile's bytes are DMA'd as one aligned run (see pk_issue_linear)
-    uint32_t lin_bytes;  // bytes from base & ~15 through the tile's last byte
     uint64_t off;  // per lane
     uint32_t n;    // per lane
 };
 
-// EXT: bytes read past a block's start (704: one 720-byte piece of 44 data
-// quads; 1408 for the two-part kernel), MAXB: the largest block it stages.
-template <uint32_t EXT = 704u, uint32_t MAXB = kRegMaxBytes>
 __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, const DevFile *__restrict__ files,
                                           const uint32_t *__restrict__ wg_file, uint32_t nwg256,
                                           uint64_t total_blocks, uint64_t arena_bytes) {
@@ -759,16 +591,10 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
         d.nl = (uint32_t)(F0.len - (uint64_t)(F0.nblocks - 1) * F0.blen);
         d.n = lane == d.jl ? d.nl : d.B;
         d.off = d.base + (uint64_t)d.B * lane;
-        const uint64_t top = d.base + (uint64_t)d.B * 63 + EXT;
-        d.staged = d.B <= MAXB && top <= arena_bytes && top - d.base <= 0x7FFFFFFFull;
-        // the tile's bytes as one 16-byte aligned run: [base & ~15, base + span)
-        const uint64_t span = d.jl < 64 ? (uint64_t)d.B * d.jl + d.nl : (uint64_t)d.B * 64;
-        const uint64_t lin = (d.base & 15u) + span;
-        d.lin_bytes = (uint32_t)((lin + 15) & ~15ull);
-        d.linear = d.staged && ((d.B >> 2) & 1u) && (d.base & ~15ull) + d.lin_bytes <= arena_bytes;
+        const uint64_t top = d.base + (uint64_t)d.B * 63 + 704u;
+        d.staged = d.B <= kRegMaxBytes && top <= arena_bytes && top - d.base <= 0x7FFFFFFFull;
         return;
     }
-    d.linear = false;
     const uint64_t gend = min(g0 + 64, total_blocks);
     const uint32_t fmax = wg_file[nwg256];  // the batch's last block's file: no tile needs a later one
     uint64_t off = 0;
@@ -801,7 +627,7 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
             if (fe > fb && fe > g0 && fb < gend) {  // the file has blocks in this tile
                 const uint64_t b_first = (g0 > fb ? g0 : fb) - fb, b_last = (gend < fe ? gend : fe) - 1 - fb;
                 const uint64_t o_first = F[i].offset + b_first * F[i].blen;
-                const uint64_t o_top = F[i].offset + b_last * F[i].blen + EXT;
+                const uint64_t o_top = F[i].offset + b_last * F[i].blen + 704u;
                 lo_off = o_first < lo_off ? o_first : lo_off;
                 top = o_top > top ? o_top : top;
                 bmax = F[i].blen > bmax ? F[i].blen : bmax;
@@ -812,7 +638,7 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
     d.base = rfl64(lo_off);
     top = rfl64(top);
     bmax = rfl32(bmax);
-    d.staged = (g0 + 64 <= total_blocks) && bmax <= MAXB && top <= arena_bytes &&
+    d.staged = (g0 + 64 <= total_blocks) && bmax <= kRegMaxBytes && top <= arena_bytes &&
                top - d.base <= 0x7FFFFFFFull;
     d.off = off;
     d.n = n;
@@ -826,12 +652,9 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
 // jj/uu: per-lane block index and byte offset (0x40000000 for the pad) of
 // each instruction, precomputed by the loader (UNROLL); otherwise computed on
 // the fly (a caller short of VGPRs).
-// poff: the part of each block this issue fetches starts poff bytes in (the
-// two-part kernel's second part: 704).
 template <int AUX, bool UNROLL, bool ALN = false>
 __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, const PkDesc &d, uint32_t lane,
-                                         const uint32_t *jj = nullptr, const uint32_t *uu = nullptr,
-                                         uint32_t poff = 0) {
+                                         const uint32_t *jj = nullptr, const uint32_t *uu = nullptr) {
     // ALN (timing diagnostic only): every quad request rounded down to a
     // 16-byte boundary of the arena -- the same bytes per tile, naturally
     // aligned, to price the misaligned quads of blocks at a 700-byte stride
@@ -854,12 +677,11 @@ __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, con
         uint32_t vo_;                                                                                           \
         if (REG) {                                                                                              \
             const uint32_t nj_ = j_ == d.jl ? d.nl : d.B;                                                       \
-            vo_ = u16_ + poff < nj_ ? (ALN ? ((d.B * j_ + u16_ + amis) & ~15u) : d.B * j_ + poff + u16_)      \
-                                    : 0x80000000u;                                                              \
+            vo_ = u16_ < nj_ ? (ALN ? ((d.B * j_ + u16_ + amis) & ~15u) : d.B * j_ + u16_) : 0x80000000u;     \
         } else {                                                                                                \
             const uint32_t rj_ = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * j_), rel);                  \
             const uint32_t nj_ = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * j_), (int)d.n);             \
-            vo_ = u16_ + poff < nj_ ? rj_ + poff + u16_ : 0x80000000u;                                          \
+            vo_ = u16_ < nj_ ? rj_ + u16_ : 0x80000000u;                                                        \
         }                                                                                                       \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * (I_)), \
                                                  16, vo_, 0, 0, AUX);                                           \
@@ -895,8 +717,7 @@ __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, con
 #pragma unroll
                 for (uint32_t k = 0; k < kBatch; k++) {
                     const uint32_t u16 = uu[i0 + k];
-                    const uint32_t vo = u16 + poff < nj[k] ? (ALN ? ((rj[k] + u16 + amis) & ~15u) : rj[k] + poff + u16)
-                                                           : 0x80000000u;
+                    const uint32_t vo = u16 < nj[k] ? (ALN ? ((rj[k] + u16 + amis) & ~15u) : rj[k] + u16) : 0x80000000u;
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(
                         rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * (i0 + k)), 16, vo, 0, 0, AUX);
                 }
@@ -908,26 +729,6 @@ __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, con
         }
     }
 #undef RSG_PK_ONE
-}
-
-// Linear tile (a regular tile of blocks whose B/4 is odd): the tile's bytes
-// [base & ~15, base + span) as one run of naturally aligned 16-byte quads,
-// instruction i lane l -> slot bytes [1024 i + 16 l, +16) (44 instructions for
-// 64 blocks of <= 703 bytes; quads past the run are dropped by an offset past
-// num_records).  Every request is 16-byte aligned -- blocks at a 700-byte
-// stride put 3 of 4 per-block quads off that alignment -- and the hasher
-// copies block j from slot byte (base & 15) + B j with 4-byte LDS reads,
-// bank (a/4) mod 32 = (const + (B/4) j) mod 32: conflict-free for odd B/4.
-template <int AUX>
-__device__ __forceinline__ void pk_issue_linear(const uint8_t *arena, uint8_t *dst, const PkDesc &d, uint32_t lane) {
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(arena + (d.base & ~15ull)), (short)0, 0x7FFFFFFF, 0x00020000);
-#pragma unroll
-    for (uint32_t i = 0; i < kPkDma - 1; i++) {
-        const uint32_t vo = 1024u * i + 16u * lane;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * i), 16,
-                                                 vo < d.lin_bytes ? vo : 0x80000000u, 0, 0, AUX);
-    }
 }
 
 // A block of a direct tile: the lane locates and loads it itself.
@@ -969,12 +770,7 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
 // (A/B, profiles/r02f_ab_park_cache_policy*.json: the default policy, sc0 or
 // sc1 alone cost 6-9 %; nt combined with sc0 / sc1 equals nt.)
 // NL = loader waves (1 or 2); the other 8 - NL waves hash.
-// JOIN: a loader wave whose tiles are all issued and published joins the
-// hashers (the last tiles of a workgroup then wait for no hasher: the drain
-// after the memory stream ends is one tile's hashing, not up to two).
-// LIN: regular tiles with odd B/4 travel as one aligned linear run
-// (pk_issue_linear); the others keep the per-block layout.
-template <int MODE, int NL, int AUX, bool JOIN = true, bool LIN = false>
+template <int MODE, int NL, int AUX>
 __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
@@ -1024,17 +820,9 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             // the slot's previous tile must have been copied out by its hasher
             while (pk_load(&sh.freeq[slot]) != k) __builtin_amdgcn_s_sleep(1);
             sh.n[slot][lane] = cur.n;
-            const bool lin = LIN && cur.linear;
-            if (lane == 0) {
-                sh.kind[slot] = cur.staged ? (lin ? 2u : 1u) : 0u;
-                sh.shift[slot] = (uint32_t)(cur.base & 15u);
-                sh.blen[slot] = cur.B;
-            }
+            if (lane == 0) sh.kind[slot] = cur.staged ? 1u : 0u;
             const bool staged = cur.staged;
-            if (staged && MODE != 2) {
-                if (lin) pk_issue_linear<AUX>(arena, &sh.tile[slot][0], cur, lane);
-                else pk_issue<AUX, true, MODE == 3>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
-            }
+            if (staged && MODE != 2) pk_issue<AUX, true, MODE == 3>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
             uint32_t kn = k + 1;
             while (!owned(kn)) kn++;
             const uint64_t tn = blockIdx.x + (uint64_t)kn * G;
@@ -1050,8 +838,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
                 // a 6-bit counter: a wave cannot have more than 63 DMA
                 // instructions (63 KiB) in flight, so waiting for an older
                 // tile instead stalls the issue of this one (measured slower).
-                if (staged && !lin) asm volatile("s_waitcnt vmcnt(45)" ::: "memory");
-                else if (staged) asm volatile("s_waitcnt vmcnt(44)" ::: "memory");
+                if (staged) asm volatile("s_waitcnt vmcnt(45)" ::: "memory");
                 else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) pk_store(&sh.full[prev % kPkSlots], prev);
             }
@@ -1064,7 +851,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) pk_store(&sh.full[prev % kPkSlots], prev);
         }
-        if (!JOIN) return;
+        return;
     }
 
     // ---------------------------------------------------------------- hashers
@@ -1086,24 +873,11 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             int32_t s1 = 0;
             uint32_t tw = 0;
             uint32_t R[16 * kRegChunks];
-            if (LIN && kind == 2) {
-                const uint32_t *mine = reinterpret_cast<const uint32_t *>(
-                    &sh.tile[slot][0] + __builtin_amdgcn_readfirstlane(sh.shift[slot]) +
-                    __builtin_amdgcn_readfirstlane(sh.blen[slot]) * lane);
+            const uint8_t *mine = &sh.tile[slot][0] + lane * kPkPiece;
 #pragma unroll
-                for (uint32_t q = 0; q < 16 * kRegChunks; q++) R[q] = mine[q];
-                // keeps the two copy-outs apart: merged behind one selected
-                // address they became 4-byte reads for both layouts (the
-                // per-block layout is conflict-free only with ds_read_b128)
-                asm volatile("" ::: "memory");
-            } else {
-                const uint8_t *mine = &sh.tile[slot][0] + lane * kPkPiece;
-#pragma unroll
-                for (uint32_t q = 0; q < 4 * kRegChunks; q++) {
-                    const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
-                    R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
-                }
-                if (LIN) asm volatile("" ::: "memory");
+            for (uint32_t q = 0; q < 4 * kRegChunks; q++) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
+                R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);
@@ -1129,123 +903,6 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     }
 }
 
-
-// ---------------------------------------------------------------- two-part park (704 < B <= 1407)
-// The park kernel for blocks longer than one parked piece (the reference's
-// own sizing gives B = 1024 for 1 MiB files, rsynccommon.go:22): a tile's
-// 64 blocks travel as two tickets, part 0 = the first 704 bytes of every
-// block (11 chunks) and part 1 = the rest (<= 703 bytes), each in the
-// park's 720-byte-per-block slot layout.  A hasher takes a tile, copies part
-// 0 into its registers, frees the slot, hashes chunks 0..10, then copies part
-// 1 (which the loaders fetched meanwhile) and hashes the rest and the tail.
-// Loader L owns slot L and loads tickets k = L, L + 3, ... (tile k / 2,
-// part k % 2).  No wait cycle: a hasher frees each slot right after its
-// copy-out, before it waits for its next part.
-constexpr uint32_t kPark2MaxBytes = 2 * 64 * kRegChunks - 1;  // 1407
-
-template <int AUX>
-__global__ __launch_bounds__(kPkThreads) void block_sums_park2(
-    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
-    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
-    uint8_t *__restrict__ out) {
-    constexpr uint32_t NL = kParkLoaders2;
-    __shared__ __attribute__((aligned(16))) PkShared sh;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (threadIdx.x < kPkSlots) {
-        sh.full[threadIdx.x] = ~0u;
-        sh.freeq[threadIdx.x] = threadIdx.x;
-    }
-    if (threadIdx.x == 0) sh.ticket = 0;
-    __syncthreads();
-    const uint64_t ntiles = (total_blocks + 63) / 64;
-    const uint32_t G = gridDim.x;
-    if (wave < NL) {
-        uint32_t jj[kPkDma], uu[kPkDma];
-#pragma unroll
-        for (uint32_t i = 0; i < kPkDma; i++) {
-            const uint32_t idx = 64u * i + lane;
-            jj[i] = idx / 45u;
-            const uint32_t u = idx - 45u * jj[i];
-            uu[i] = u < 44u ? 16u * u : 0x40000000u;
-        }
-        uint32_t k = wave;  // tickets k = wave + 3 m
-        PkDesc cur;
-        uint64_t t = blockIdx.x + (uint64_t)(k >> 1) * G;
-        if (t < ntiles) pk_locate<1408u, kPark2MaxBytes>(t, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
-#pragma unroll 1
-        while (t < ntiles) {
-            const uint32_t slot = k % kPkSlots;
-            while (pk_load(&sh.freeq[slot]) != k) __builtin_amdgcn_s_sleep(1);
-            if ((k & 1u) == 0) sh.n[slot][lane] = cur.n;
-            if (lane == 0) sh.kind[slot] = cur.staged ? 1u : 0u;
-            if (cur.staged) pk_issue<AUX, true>(arena, &sh.tile[slot][0], cur, lane, jj, uu, (k & 1u) * 704u);
-            // the next ticket (k + 3: another tile) while this one is in flight
-            const uint32_t kn = k + kPkSlots;
-            const uint64_t tn = blockIdx.x + (uint64_t)(kn >> 1) * G;
-            if (tn < ntiles)
-                pk_locate<1408u, kPark2MaxBytes>(tn, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
-            // one slot per loader: publish before waiting for the slot again
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) pk_store(&sh.full[slot], k);
-            k = kn;
-            t = tn;
-        }
-    }
-    // ---------------------------------------------------------------- hashers (and, once done, the loaders)
-#pragma unroll 1
-    for (;;) {
-        uint32_t i = 0;
-        if (lane == 0) i = __hip_atomic_fetch_add(&sh.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        i = __builtin_amdgcn_readfirstlane(i);
-        const uint64_t t = blockIdx.x + (uint64_t)i * G;
-        if (t >= ntiles) break;
-        const uint64_t g = t * 64 + lane;
-        uint32_t h[4];
-        md4_init(h);
-        int32_t s1 = 0;
-        uint32_t tw = 0;
-        uint32_t n = 0;
-        bool direct = false;
-#pragma unroll 1
-        for (uint32_t p = 0; p < 2; p++) {
-            const uint32_t k = 2 * i + p;
-            const uint32_t slot = k % kPkSlots;
-            while (pk_load(&sh.full[slot]) != k) __builtin_amdgcn_s_sleep(1);
-            if (p == 0) n = sh.n[slot][lane];
-            const uint32_t kind = __builtin_amdgcn_readfirstlane(sh.kind[slot]);
-            if (!kind) {
-                if (lane == 0) {
-                    pk_store(&sh.freeq[slot], k + kPkSlots);
-                    if (p == 0 && t * 64 + 64 <= total_blocks) count_fallback(1);
-                }
-                direct = true;
-                continue;
-            }
-            uint32_t R[16 * kRegChunks];
-            const uint8_t *mine = &sh.tile[slot][0] + lane * kPkPiece;
-#pragma unroll
-            for (uint32_t q = 0; q < 4 * kRegChunks; q++) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
-                R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);
-            const uint32_t nfull = n >> 6;
-#pragma unroll
-            for (uint32_t q = 0; q < kRegChunks; q++) {
-                const uint32_t c = kRegChunks * p + q;
-                if (c < nfull) hash_chunk<true>(R + 16 * q, 0u, 0u, c, h, s1, tw);
-                else if (c == nfull) hash_tail<true>(R + 16 * q, 0u, 0u, n, seed, h, s1, tw);
-            }
-        }
-        if (direct) {
-            if (g < total_blocks) pk_direct(arena, arena_bytes, files, wg_file, nwg256, g, seed, out);
-        } else {
-            store_record(out, g, n, s1, tw, h);
-        }
-    }
-}
 
 // Kernel variants (rsg_set_block_sums_kernel; identical results, only speed
 // differs): -1 = automatic, 0 = direct per-lane loads, 1 = staged LDS-DMA
@@ -1280,23 +937,6 @@ static uint32_t park_grid(uint64_t total_blocks) {
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint64_t ntile = (total_blocks + 63) / 64;
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus, ntile));
-}
-
-// Workgroups of the persistent staged kernel: every CU's resident share
-// (occupancy from the kernel's LDS and registers), at most one wave per group.
-static uint32_t persist_grid(bool seg128, uint64_t groups) {
-    static int per_cu[2] = {0, 0};
-    int &pc = per_cu[seg128 ? 1 : 0];
-    if (pc == 0) {
-        int nb = 0;
-        const hipError_t e = seg128
-            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, block_sums_staged_persist<128>, kBlockSumThreads, 0)
-            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, block_sums_staged_persist<256>, kBlockSumThreads, 0);
-        pc = (e == hipSuccess && nb > 0) ? nb : 1;
-    }
-    const uint64_t want = (uint64_t)park_grid(~0ull >> 8) * (uint64_t)pc;
-    const uint64_t need = (groups + kBlockSumThreads / 64 - 1) / (kBlockSumThreads / 64);
-    return (uint32_t)std::max<uint64_t>(1, std::min(want, need));
 }
 
 hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const DevFile *files,
@@ -1359,10 +999,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v >= 7)) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
-    if ((v == 2 || v == 7 || v == 8) && max_blen > kRegMaxBytes) v = 1;
-    if (v == 11 && max_blen > kPark2MaxBytes) v = 1;
+    if (v == 2 && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
             hipLaunchKernelGGL((block_sums_staged<0>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
@@ -1371,30 +1010,6 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes, files,
                                wg_file, nwg, total_blocks, seed, out);
-            break;
-        case 11:  // A/B: two-part park (704 < B <= 1407)
-            hipLaunchKernelGGL((block_sums_park2<2>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file, nwg,
-                               total_blocks, seed, out);
-            break;
-        case 9:
-        case 10: {  // A/B: persistent staged (128- / 256-byte segments)
-            const uint64_t groups = (total_blocks + 63) / 64;
-            const uint32_t g = persist_grid(v == 9, groups);
-            if (v == 9)
-                hipLaunchKernelGGL((block_sums_staged_persist<128>), dim3(g), block, 0, stream, arena, arena_bytes,
-                                   files, wg_file, nwg, total_blocks, seed, out);
-            else
-                hipLaunchKernelGGL((block_sums_staged_persist<256>), dim3(g), block, 0, stream, arena, arena_bytes,
-                                   files, wg_file, nwg, total_blocks, seed, out);
-            break;
-        }
-        case 8:  // A/B: park (join) whose regular odd-B/4 tiles travel as aligned linear runs
-            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, true, true>), pgrid, pblock, 0, stream, arena,
-                               arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
-            break;
-        case 7:  // A/B: park whose loader waves do not join the hashers (round 3's kernel)
-            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, false>), pgrid, pblock, 0, stream, arena, arena_bytes,
-                               files, wg_file, nwg, total_blocks, seed, out);
             break;
         case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel
             if (aligned)

@@ -513,7 +513,7 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
     filter16.clear();
     if ((uint32_t)B <= rsg::kFusedMaxB && rsg::roll_packed()) {
         filter16.assign(rsg::kFilter16Words, 0);
-        const int nbits = rsg::roll_filter_bits() % 10;
+        const int nbits = rsg::roll_filter_bits();
         for (auto &kv : keys)
             filter16[rsg::f16_word(kv.first, (uint32_t)B)] |= (uint16_t)rsg::f16_mask(kv.first, nbits);
     }

@@ -654,9 +654,6 @@ __device__ __forceinline__ u16x2 pair_bytes(uint32_t wa, uint32_t wb, int p) {
 // NBITS: filter bits per sum, S2[0..3], S2[4..7] (and S2[8..11]); EDGE: the
 // kernel rolls the range's edge tiles itself (else the host leaves them to
 // roll_kernel and passes t_int = tile_hi).
-// NBITS >= 10 (RSG_ROLL_BITS=d, timing diagnostic only: candidates
-// meaningless): NBITS % 10 bits, and the tile loop's workgroup barrier
-// skipped (stale scan partials), to price what the per-tile barrier costs.
 template <int NBITS, bool EDGE>
 __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
@@ -810,7 +807,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
             const uint32_t b = (so2 + (uint32_t)(q0 + B) * (uint32_t)s1) - (oo2 + (uint32_t)q0 * (uint32_t)o1);
             const uint32_t ia = wave_incl_scan(a), ib = wave_incl_scan(b);
             if (lane == 63) wsum[parity][wave] = make_uint2(ia, ib);
-            if constexpr (NBITS < 10) __syncthreads();
+            __syncthreads();
             const uint32_t w = lane & 15u;
             uint2 p = wsum[parity][min(w, kWaves - 1)];
             if (w >= wave) p = make_uint2(0, 0);
@@ -875,7 +872,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 for (int jj = 0; jj < GE; jj++) {
                     const uint32_t s2 = raw[jj] >> 16;
                     uint32_t bits = (word[jj] >> (s2 & 15u)) & (word[jj] >> ((s2 >> 4) & 15u));
-                    if constexpr (NBITS % 10 == 3) bits &= word[jj] >> ((s2 >> 8) & 15u);
+                    if constexpr (NBITS == 3) bits &= word[jj] >> ((s2 >> 8) & 15u);
                     park((bits & 1u) && (lol + g0 + jj < end_rel), (uint32_t)(g0 + jj), raw[jj]);
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -921,7 +918,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 const u16x2 x = pk_shr(wd[jj], p2[jj]);
                 const u16x2 y = pk_shr(wd[jj], p2[jj] >> (uint16_t)4);
                 u16x2 xy = x & y;
-                if constexpr (NBITS % 10 == 3) xy &= pk_shr(wd[jj], p2[jj] >> (uint16_t)8);
+                if constexpr (NBITS == 3) xy &= pk_shr(wd[jj], p2[jj] >> (uint16_t)8);
                 uint32_t z = as_u32(xy) & 0x00010001u;
                 asm("" : "+v"(z));
                 const uint32_t r1 = as_u32(p1[jj]), r2 = as_u32(p2[jj]);
@@ -1051,7 +1048,7 @@ int roll_filter_bits() {
         // (0.6 % instead of 1.0 % false hits: fewer parks for 2-3 more VALU
         // per two offsets; roll 0.83-0.85 vs 0.86-0.87 ms per GiB)
         const char *e = getenv("RSG_ROLL_BITS");
-        return (e && e[0] == '2') ? 2 : ((e && e[0] == 'd') ? 13 : 3);
+        return (e && e[0] == '2') ? 2 : 3;
     }();
     return v;
 }
@@ -1084,14 +1081,12 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
             if (roll_edge_inside()) {
                 // the whole range: the packed kernel rolls its edge tiles itself
                 const uint32_t ga = min(grid, tile_hi - tile_lo);
-                auto kern = roll_filter_bits() == 3    ? roll_packed_kernel<3, true>
-                            : roll_filter_bits() == 13 ? roll_packed_kernel<13, true>
-                                                       : roll_packed_kernel<2, true>;
+                auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, true> : roll_packed_kernel<2, true>;
                 hipLaunchKernelGGL(kern, dim3(ga), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
                                    t_int, tile_hi, filter16, table_keys, bmask, cand, cap, count);
                 return hipGetLastError();
             }
-            auto kern = roll_filter_bits() % 10 == 3 ? roll_packed_kernel<3, false> : roll_packed_kernel<2, false>;
+            auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, false> : roll_packed_kernel<2, false>;
             hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, t_int,
                                t_int, filter16, table_keys, bmask, cand, cap, count);
             const hipError_t e = hipGetLastError();

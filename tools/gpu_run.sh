@@ -17,7 +17,6 @@ for S in "$@"; do
     variants) timeout -k 10 300 python -u -m pytest tests/test_gpu_blocksums.py -m gpu -x -q $T -k "variants or per_context or cfg2_full" > gpurun_out/${TAG}_variants.log 2>&1 || { tail -30 gpurun_out/${TAG}_variants.log; exit 1; } ;;
     ab) timeout -k 10 200 python bench.py --ab --steps 30 --no-cpu --no-host-path --no-delivery > gpurun_out/${TAG}_ab.json 2> gpurun_out/${TAG}_ab.err || exit 1 ;;
     bench) timeout -k 10 200 python bench.py --steps 20 --warmup 5 > gpurun_out/${TAG}_cfg2.json 2> gpurun_out/${TAG}_cfg2.err || exit 1 ;;
-    cfg3ab) for r in 1 2; do for b in 3 d; do RSG_ROLL_BITS=$b timeout -k 10 200 python bench.py --workload cfg3 --steps 3 --no-cpu --no-host-path > gpurun_out/${TAG}_cfg3_bits${b}_r$r.json 2>> gpurun_out/${TAG}_cfg3ab.err || exit 1; done; done ;;
     cfg3) timeout -k 10 240 python bench.py --workload cfg3 > gpurun_out/${TAG}_cfg3.json 2> gpurun_out/${TAG}_cfg3.err || exit 1 ;;
     cfg4) timeout -k 10 200 python bench.py --workload cfg4 --steps 50 > gpurun_out/${TAG}_cfg4.json 2> gpurun_out/${TAG}_cfg4.err || exit 1 ;;
     cfg5) timeout -k 10 200 python bench.py --workload cfg5 --steps 50 > gpurun_out/${TAG}_cfg5.json 2> gpurun_out/${TAG}_cfg5.err || exit 1 ;;
