@@ -199,6 +199,29 @@ def main():
         step(0)  # the records hold the product kernel's output again (diagnostics write garbage)
         eng.synchronize(sptr)
         extra["ab_kernel_ms"] = {names[v]: [round(x, 4) for x in sorted(res[v])] for v in names}
+        # consecutive batches on two streams (the generator's two-slot
+        # pipeline): batch i+1's workgroups take the CUs batch i's leave
+        s2 = torch.cuda.Stream(device=local)
+        recs2 = eng.alloc(plan.total_records * rsync_amd.RECORD_BYTES)
+        two = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                if i & 1:
+                    plan.run(arenas[1], SEED, recs2, stream=s2.cuda_stream)
+                else:
+                    plan.run(arenas[0], SEED, recs, stream=sptr)
+            torch.cuda.synchronize()
+            two.append((time.perf_counter() - t0) * 1e3 / args.steps)
+            one0 = time.perf_counter()
+            for i in range(args.steps):
+                step(i)
+            eng.synchronize(sptr)
+            two.append(-(time.perf_counter() - one0) * 1e3 / args.steps)
+        extra["ab_wall_ms_per_step"] = {"two_streams": sorted(round(x, 4) for x in two if x > 0),
+                                        "one_stream": sorted(round(-x, 4) for x in two if x < 0)}
+        recs2.free()
 
     in_bytes = float(arena_bytes)
     out_bytes = float(plan.total_records * rsync_amd.RECORD_BYTES)
