@@ -1085,12 +1085,14 @@ def bench_receive(args, rank, world, local):
                     "equal": all(g[0] == d.tobytes() for g, d in zip(got, files)),
                     "cpu_md4_1core_gib_s": round(n * size / t_cpu / GIB, 4)}
         if n >= 64:
-            os.environ["RSG_RECV_MD4"] = "host"
-            try:
-                _, dh = timed(lambda: eng.receive_data_batch(jobs, seed), 2)
-            finally:
-                del os.environ["RSG_RECV_MD4"]
-            res[tag]["all_host_threads_gib_s"] = round(n * size / dh / GIB, 3)
+            for mode in ("host", "gpu"):
+                os.environ["RSG_RECV_MD4"] = mode
+                try:
+                    _, dh = timed(lambda: eng.receive_data_batch(jobs, seed), 2)
+                finally:
+                    del os.environ["RSG_RECV_MD4"]
+                res[tag]["all_host_threads_gib_s" if mode == "host" else "all_gpu_lanes_gib_s"] = \
+                    round(n * size / dh / GIB, 3)
 
     batch("batch_1024x1MiB", 1024, 1 << 20)
     batch("batch_4x256MiB", 4, 256 << 20)
