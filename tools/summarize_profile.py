@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--kernel", default="block_sums", help="substring of the kernel name to summarize")
     ap.add_argument("--no-traffic", action="store_true", help="do not rewrite profiles/traffic.json")
     ap.add_argument("--outdir", default="profiles")
+    ap.add_argument("--timed", type=int, default=0,
+                    help="the bench's timed launches are the last N dispatches: report their mean too")
     ap.add_argument("--roll-cus", type=int, default=224,
                     help="CUs the roll's workgroups occupy (cfg3 batch: all but RSG_CONFIRM_CUS = 32 of 256)")
     a = ap.parse_args()
@@ -40,7 +42,8 @@ def main():
         for r in rows(f):
             counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
     avg = {k: sum(v) / len(v) for k, v in counters.items()}
-    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in trace if kernel in r["Kernel_Name"]]
+    mine = sorted((r for r in trace if kernel in r["Kernel_Name"]), key=lambda r: int(r["Start_Timestamp"]))
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in mine]
     steady = sorted(durs)[len(durs) // 4: 3 * len(durs) // 4] if len(durs) >= 8 else durs
     out = {
         "tag": tag,
@@ -49,6 +52,8 @@ def main():
         "dispatches": len(durs),
         "us_mean": round(sum(durs) / max(len(durs), 1), 2),
         "us_interquartile_mean": round(sum(steady) / max(len(steady), 1), 2),
+        **({"timed_launches": a.timed, "timed_launches_us_mean": round(sum(durs[-a.timed:]) / a.timed, 2)}
+           if a.timed and len(durs) >= a.timed else {}),
         "pmc_mean_per_dispatch": {k: round(v, 1) for k, v in sorted(avg.items())},
     }
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
