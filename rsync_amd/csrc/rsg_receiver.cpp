@@ -13,8 +13,8 @@
 // file, but a lane is ~10x slower than a host core, so a
 // single file (rsg_receive_data) is hashed on the host while its tokens are
 // applied, as the reference writes h as it goes (receiver.go:159-164), and
-// a batch (rsg_receive_data_batch) sends its largest files to host threads
-// when that shortens the batch (pick_host below) and the rest to the GPU.
+// a batch (rsg_receive_data_batch) hashes its small files on the GPU and its
+// large ones (on_host below) on a host pool beside the GPU pipeline.
 #include <string.h>
 
 #include <algorithm>
@@ -90,43 +90,21 @@ void md4_seeded(Md4 &h, int32_t seed) {
     h.update(sb, 4);
 }
 
-// Which jobs of a batch hash on the host.  The GPU batch takes about
-// (largest GPU file) / lane rate + (GPU bytes) / staging rate (the host
-// copies into pinned memory and the PCIe upload); host threads take about
-// max(largest host file / core rate, host bytes / (threads x core rate)),
-// the two running side by side.  The k largest files go to the host for the
-// k that minimises the longer of the two.  RSG_RECV_MD4 = gpu / host forces
-// one side (tests, A/B).  Rates (GiB/s): one GPU lane 0.09 and one host core
-// 0.9 (profiles/r03f_receive_line.json), staging 3.
-std::vector<uint8_t> pick_host(const rsg_recv_job *jobs, uint64_t i0, uint64_t i1, int threads) {
-    const uint64_t n = i1 - i0;
-    std::vector<uint8_t> host(n, 0);
+// Which jobs hash on the host.  One GPU lane hashes ~0.09 GiB/s (one serial
+// MD4 chain); the GPU path as a whole -- token application,
+// staging, upload, many lanes at once -- moves a transfer's small files at
+// ~5.5 GiB/s.  A file whose lane would take longer than the GPU path needs
+// for a whole 256 MiB batch (> ~4 MiB) is hashed on host threads instead,
+// beside the GPU pipeline: a host core does one chain at ~1 GiB/s.
+// RSG_RECV_MD4 = gpu / host forces one side (tests, A/B).
+constexpr uint64_t kHostMd4MinBytes = 4ull << 20;
+int recv_md4_mode() {  // read per call: tests switch it within one process
     const char *e = getenv("RSG_RECV_MD4");
-    if (e && !strcmp(e, "gpu")) return host;
-    if (e && !strcmp(e, "host")) {
-        std::fill(host.begin(), host.end(), 1);
-        return host;
-    }
-    constexpr double kLane = 0.09, kCore = 0.9, kStage = 3.0, kGiB = 1073741824.0;
-    std::vector<uint64_t> ord(n);
-    for (uint64_t k = 0; k < n; k++) ord[k] = k;
-    std::sort(ord.begin(), ord.end(), [&](uint64_t a, uint64_t b) { return jobs[i0 + a].out_cap > jobs[i0 + b].out_cap; });
-    double total = 0;
-    for (uint64_t k = 0; k < n; k++) total += (double)jobs[i0 + k].out_cap;
-    double best = 1e300, pre = 0;
-    uint64_t best_k = 0;
-    for (uint64_t k = 0; k <= n; k++) {  // the k largest on the host
-        const double gpu = k < n ? ((double)jobs[i0 + ord[k]].out_cap / kLane + (total - pre) / kStage) / kGiB : 0;
-        const double hst = k ? std::max((double)jobs[i0 + ord[0]].out_cap / kCore, pre / (threads * kCore)) / kGiB : 0;
-        const double t = std::max(gpu, hst);
-        if (t < best) {
-            best = t;
-            best_k = k;
-        }
-        if (k < n) pre += (double)jobs[i0 + ord[k]].out_cap;
-    }
-    for (uint64_t k = 0; k < best_k; k++) host[ord[k]] = 1;
-    return host;
+    return (e && !strcmp(e, "gpu")) ? 1 : ((e && !strcmp(e, "host")) ? 2 : 0);
+}
+bool on_host(const rsg_recv_job &j, int mode) {
+    if (mode) return mode == 2;
+    return j.out_cap >= kHostMd4MinBytes;
 }
 
 int copy_threads() {
@@ -138,37 +116,49 @@ int copy_threads() {
 // Token application of many jobs on a few host threads (byte copying; each
 // job writes only its own output).  Sets every job's out_len / consumed /
 // status; returns nothing (failures are per job).
-// host[k - i0]: job k's whole-file sum is checked on this thread while its
-// tokens are applied (status RSG_ERR_CORRUPT on a mismatch, consumed set).
+// One job entirely on this thread: tokens applied with the seeded MD4 fed as
+// the bytes are written (receiver.go:117-120,159-164), then the sum check.
+void run_host_job(rsg_recv_job &j, int32_t seed) {
+    j.out_len = 0;
+    j.consumed = 0;
+    uint64_t at = 0;
+    Md4 h;
+    md4_seeded(h, seed);
+    rsg_status st = apply(nullptr, j.tokens, j.tokens_len, &j.head, j.basis, j.basis_len, j.out, j.out_cap,
+                          &j.out_len, &at, &h);
+    if (st == RSG_OK && at + 16 > j.tokens_len) st = RSG_ERR_INVALID;  // receiver.go:167-170
+    if (st == RSG_OK && j.out_len && !j.out) st = RSG_ERR_INVALID;
+    if (st == RSG_OK) {
+        uint8_t local[16];
+        h.final(local);
+        j.consumed = at + 16;
+        if (memcmp(local, j.tokens + at, 16) != 0) st = RSG_ERR_CORRUPT;  // receiver.go:171-173
+    }
+    j.status = st;
+}
+
+// host[k - i0] != 0: job k belongs to the host pool (run_host_job), skip it.
 void apply_jobs(rsg_recv_job *jobs, uint64_t i0, uint64_t i1, std::vector<uint64_t> &sum_at,
-                const std::vector<uint8_t> &host, int32_t seed) {
+                const std::vector<uint8_t> &host) {
     const int threads = copy_threads();
     std::atomic<uint64_t> next{i0};
     auto worker = [&] {
         for (uint64_t k; (k = next.fetch_add(1)) < i1;) {
+            if (host[k - i0]) continue;
             rsg_recv_job &j = jobs[k];
             j.out_len = 0;
             j.consumed = 0;
             uint64_t at = 0;
-            Md4 h;
-            const bool on_host = host[k - i0] != 0;
-            if (on_host) md4_seeded(h, seed);
             rsg_status st = apply(nullptr, j.tokens, j.tokens_len, &j.head, j.basis, j.basis_len, j.out, j.out_cap,
-                                  &j.out_len, &at, on_host ? &h : nullptr);
+                                  &j.out_len, &at);
             if (st == RSG_OK && at + 16 > j.tokens_len) st = RSG_ERR_INVALID;  // receiver.go:167-170
             if (st == RSG_OK && j.out_len && !j.out) st = RSG_ERR_INVALID;
             sum_at[k - i0] = at;
-            if (st == RSG_OK && on_host) {
-                uint8_t local[16];
-                h.final(local);
-                j.consumed = at + 16;
-                if (memcmp(local, j.tokens + at, 16) != 0) st = RSG_ERR_CORRUPT;  // receiver.go:171-173
-            }
             j.status = st;
         }
     };
     uint64_t bytes = 0;
-    for (uint64_t k = i0; k < i1; k++) bytes += jobs[k].tokens_len + (host[k - i0] ? (16ull << 20) : 0);
+    for (uint64_t k = i0; k < i1; k++) bytes += host[k - i0] ? 0 : jobs[k].tokens_len;
     const int nt = (int)std::min<uint64_t>((uint64_t)threads, std::min<uint64_t>(i1 - i0, 1 + bytes / (1ull << 20)));
     std::vector<std::thread> pool;
     for (int t = 1; t < nt; t++) pool.emplace_back(worker);
@@ -265,20 +255,44 @@ rsg_status rsg_receive_data_batch(rsg_ctx *ctx, rsg_recv_job *jobs, uint64_t njo
         sl.busy = false;
         return RSG_OK;
     };
+    // large files: a host pool beside the GPU pipeline (on_host)
+    std::vector<uint8_t> is_host(njobs, 0);
+    std::vector<uint64_t> host_jobs;
+    const int md4_mode = recv_md4_mode();
+    for (uint64_t q = 0; q < njobs; q++)
+        if (on_host(jobs[q], md4_mode)) {
+            is_host[q] = 1;
+            host_jobs.push_back(q);
+        }
+    std::atomic<uint64_t> next_host{0};
+    std::vector<std::thread> pool;
+    const int npool = (int)std::min<uint64_t>((uint64_t)copy_threads(), host_jobs.size());
+    for (int t = 0; t < npool; t++)
+        pool.emplace_back([&] {
+            for (uint64_t x; (x = next_host.fetch_add(1)) < host_jobs.size();) run_host_job(jobs[host_jobs[x]], seed);
+        });
+    struct Join {
+        std::vector<std::thread> &p;
+        ~Join() {
+            for (auto &t : p)
+                if (t.joinable()) t.join();
+        }
+    } join_pool{pool};
     rsg_status fatal = RSG_OK;
     uint64_t i = 0;
     for (int k = 0; i < njobs; k ^= 1) {
         Slot &sl = slots[k];
         if ((fatal = finish(sl, k)) != RSG_OK) break;
-        // the batch: jobs until ~kBatchBytes of rebuilt bytes (bounded by
-        // out_cap, known before applying)
+        // the batch: GPU jobs until ~kBatchBytes of rebuilt bytes (bounded
+        // by out_cap, known before applying)
         uint64_t i1 = i, est = 0;
-        while (i1 < njobs && (i1 == i || est + jobs[i1].out_cap <= kBatchBytes)) est += jobs[i1++].out_cap;
+        while (i1 < njobs && (i1 == i || est + (is_host[i1] ? 0 : jobs[i1].out_cap) <= kBatchBytes))
+            est += is_host[i1] ? 0 : jobs[i1].out_cap, i1++;
         sl.i0 = i;
         sl.i1 = i1;
         sl.sum_at.assign(i1 - i, 0);
-        const std::vector<uint8_t> host = pick_host(jobs, i, i1, copy_threads());
-        apply_jobs(jobs, i, i1, sl.sum_at, host, seed);
+        const std::vector<uint8_t> host(is_host.begin() + (int64_t)i, is_host.begin() + (int64_t)i1);
+        apply_jobs(jobs, i, i1, sl.sum_at, host);
         sl.lane.clear();
         std::vector<rsg::FileSpan> spans;
         std::vector<CopyJob> copies;
@@ -321,9 +335,10 @@ rsg_status rsg_receive_data_batch(rsg_ctx *ctx, rsg_recv_job *jobs, uint64_t njo
         sl.busy = true;
     }
     for (int k = 0; k < 2 && fatal == RSG_OK; k++) fatal = finish(slots[k], k);
+    for (auto &t : pool) t.join();  // the host pool's jobs are done (and keep their own statuses)
     if (fatal != RSG_OK) {
         for (uint64_t q = 0; q < njobs; q++)
-            if (jobs[q].status == RSG_OK) jobs[q].status = fatal;
+            if (jobs[q].status == RSG_OK && !is_host[q]) jobs[q].status = fatal;
         return fatal;
     }
     for (uint64_t q = 0; q < njobs; q++) {
