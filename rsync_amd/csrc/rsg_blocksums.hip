@@ -770,7 +770,10 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
 // (A/B, profiles/r02f_ab_park_cache_policy*.json: the default policy, sc0 or
 // sc1 alone cost 6-9 %; nt combined with sc0 / sc1 equals nt.)
 // NL = loader waves (1 or 2); the other 8 - NL waves hash.
-template <int MODE, int NL, int AUX>
+// PRIO (A/B): 1 = loader waves at wave priority 3 (a slot's next DMA issues
+// ahead of the hasher sharing the SIMD); 2 = also hashers at priority 2
+// while they copy a slot out (the slot frees sooner), 0 while they hash.
+template <int MODE, int NL, int AUX, int PRIO = 0>
 __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
@@ -788,6 +791,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint32_t G = gridDim.x;  // one persistent workgroup per CU; tile t belongs to workgroup t % G
 
     if (wave < NL) {
+        if (PRIO >= 1) __builtin_amdgcn_s_setprio(3);
         // ------------------------------------------------------------ loaders
         // DMA instruction i, lane l fills tile bytes [1024 i + 16 l, +16):
         // block j = (64 i + l) / 45, quad u = (64 i + l) % 45 (u = 44: pad,
@@ -864,6 +868,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
         if (t >= ntiles) break;
         const uint32_t slot = k % kPkSlots;
         while (pk_load(&sh.full[slot]) != k) __builtin_amdgcn_s_sleep(1);
+        if (PRIO >= 2) __builtin_amdgcn_s_setprio(2);
         const uint32_t n = sh.n[slot][lane];
         const uint32_t kind = __builtin_amdgcn_readfirstlane(sh.kind[slot]);
         const uint64_t g = t * 64 + lane;
@@ -881,6 +886,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);
+            if (PRIO >= 2) __builtin_amdgcn_s_setprio(0);
             const uint32_t nfull = n >> 6;
             if (MODE == 1 || MODE == 3) {
 #pragma unroll
@@ -999,9 +1005,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v == 7 || v == 8)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
-    if (v == 2 && max_blen > kRegMaxBytes) v = 1;
+    if ((v == 2 || v == 7 || v == 8) && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
             hipLaunchKernelGGL((block_sums_staged<0>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
@@ -1010,6 +1016,15 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes, files,
                                wg_file, nwg, total_blocks, seed, out);
+            break;
+        case 7:  // A/B: park, loaders at priority 3
+        case 8:  // A/B: park, loaders at 3, hashers at 2 during copy-out
+            if (v == 7)
+                hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 1>), pgrid, pblock, 0, stream, arena,
+                                   arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+            else
+                hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 2>), pgrid, pblock, 0, stream, arena,
+                                   arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
             break;
         case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel
             if (aligned)
