@@ -868,7 +868,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
         if (t >= ntiles) break;
         const uint32_t slot = k % kPkSlots;
         while (pk_load(&sh.full[slot]) != k) __builtin_amdgcn_s_sleep(1);
-        if (PRIO >= 2) __builtin_amdgcn_s_setprio(2);
+        if (PRIO >= 2) __builtin_amdgcn_s_setprio(PRIO >= 3 ? 3 : 2);
         const uint32_t n = sh.n[slot][lane];
         const uint32_t kind = __builtin_amdgcn_readfirstlane(sh.kind[slot]);
         const uint64_t g = t * 64 + lane;
@@ -1005,9 +1005,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v == 7 || v == 8)) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v >= 7)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
-    if ((v == 2 || v == 7 || v == 8) && max_blen > kRegMaxBytes) v = 1;
+    if ((v == 2 || v >= 7) && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
             hipLaunchKernelGGL((block_sums_staged<0>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
@@ -1016,6 +1016,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes, files,
                                wg_file, nwg, total_blocks, seed, out);
+            break;
+        case 9:  // A/B: park, loaders at 3, hashers at 3 during copy-out
+            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
+                               files, wg_file, nwg, total_blocks, seed, out);
             break;
         case 7:  // A/B: park, loaders at priority 3
         case 8:  // A/B: park, loaders at 3, hashers at 2 during copy-out
