@@ -359,7 +359,9 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 // 4-byte aligned): each piece is fetched from the block's start rounded down
 // to 4 bytes, one 16-byte unit longer (the pad unit carries data), and the
 // lane funnel-shifts its words (alignbyte) as the direct kernel does.
-template <int KIND>
+// PRIO (A/B) = 3: the wave runs at priority 3 from its segment wait through
+// the next segment's DMA issue, 0 while it hashes.
+template <int KIND, int PRIO = 0>
 __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
@@ -435,6 +437,7 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     } while (0)
 #define RSG_READ_SEGMENT()                                                                                       \
     do {                                                                                                         \
+        if (PRIO) __builtin_amdgcn_s_setprio(3);                                                                 \
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                                         \
         _Pragma("unroll") for (int q_ = 0; q_ < (int)(SEG / 16) + (UNAL ? 1 : 0); q_++) {                        \
             const uint4 v_ = *reinterpret_cast<const uint4 *>(mine + 16 * q_);                                  \
@@ -453,6 +456,7 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     for (uint32_t cs = 0; cs < S; cs++) {
         const bool more = cs + 1 < S;
         if (MODE != 2 && more) RSG_DMA_SEGMENT(cs + 1);  // in flight while segment cs hashes
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
         if (MODE == 1) {
 #pragma unroll
             for (int q = 0; q < (int)(SEG / 4); q++) h[q & 3] ^= R[q];
@@ -770,9 +774,12 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
 // (A/B, profiles/r02f_ab_park_cache_policy*.json: the default policy, sc0 or
 // sc1 alone cost 6-9 %; nt combined with sc0 / sc1 equals nt.)
 // NL = loader waves (1 or 2); the other 8 - NL waves hash.
-// PRIO (A/B): 1 = loader waves at wave priority 3 (a slot's next DMA issues
-// ahead of the hasher sharing the SIMD); 2 = also hashers at priority 2
-// while they copy a slot out (the slot frees sooner), 0 while they hash.
+// PRIO: wave priorities (s_setprio) -- 0 = none; 3 (the product) = loader
+// waves at priority 3 (a slot's next DMA issues ahead of the hasher sharing
+// the SIMD) and hashers at 3 while they copy a slot out (the slot frees
+// sooner), 0 while they hash; 4 (A/B) = as 3, the hasher raised already while
+// it waits for its slot.  (8-round A/B, profiles/r04f_ab_park_prio.json:
+// none 0.1984 ms, loaders only 0.1962, copy-out at 2 0.1950, 3 0.1942.)
 template <int MODE, int NL, int AUX, int PRIO = 0>
 __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
@@ -791,7 +798,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint32_t G = gridDim.x;  // one persistent workgroup per CU; tile t belongs to workgroup t % G
 
     if (wave < NL) {
-        if (PRIO >= 1) __builtin_amdgcn_s_setprio(3);
+        if (PRIO >= 3) __builtin_amdgcn_s_setprio(3);
         // ------------------------------------------------------------ loaders
         // DMA instruction i, lane l fills tile bytes [1024 i + 16 l, +16):
         // block j = (64 i + l) / 45, quad u = (64 i + l) % 45 (u = 44: pad,
@@ -867,8 +874,9 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
         const uint64_t t = blockIdx.x + (uint64_t)k * G;
         if (t >= ntiles) break;
         const uint32_t slot = k % kPkSlots;
+        if (PRIO == 4) __builtin_amdgcn_s_setprio(3);
         while (pk_load(&sh.full[slot]) != k) __builtin_amdgcn_s_sleep(1);
-        if (PRIO >= 2) __builtin_amdgcn_s_setprio(PRIO >= 3 ? 3 : 2);
+        if (PRIO == 3) __builtin_amdgcn_s_setprio(3);
         const uint32_t n = sh.n[slot][lane];
         const uint32_t kind = __builtin_amdgcn_readfirstlane(sh.kind[slot]);
         const uint64_t g = t * 64 + lane;
@@ -886,7 +894,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);
-            if (PRIO >= 2) __builtin_amdgcn_s_setprio(0);
+            if (PRIO >= 3) __builtin_amdgcn_s_setprio(0);
             const uint32_t nfull = n >> 6;
             if (MODE == 1 || MODE == 3) {
 #pragma unroll
@@ -900,6 +908,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             }
             store_record(out, g, n, s1, tw, h);
         } else {
+            if (PRIO >= 3) __builtin_amdgcn_s_setprio(0);
             if (lane == 0) {
                 pk_store(&sh.freeq[slot], k + kPkSlots);
                 if (MODE == 0 && t * 64 + 64 <= total_blocks) count_fallback(1);
@@ -1007,28 +1016,23 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     // staged kernel (6) needs a 4-byte aligned arena
     if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v >= 7)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
-    if ((v == 2 || v >= 7) && max_blen > kRegMaxBytes) v = 1;
+    if ((v == 2 || v == 7) && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
             hipLaunchKernelGGL((block_sums_staged<0>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
                                total_blocks, seed, out);
             break;
         case 2:
-            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes, files,
-                               wg_file, nwg, total_blocks, seed, out);
-            break;
-        case 9:  // A/B: park, loaders at 3, hashers at 3 during copy-out
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                files, wg_file, nwg, total_blocks, seed, out);
             break;
-        case 7:  // A/B: park, loaders at priority 3
-        case 8:  // A/B: park, loaders at 3, hashers at 2 during copy-out
-            if (v == 7)
-                hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 1>), pgrid, pblock, 0, stream, arena,
-                                   arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
-            else
-                hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 2>), pgrid, pblock, 0, stream, arena,
-                                   arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+        case 7:  // A/B: park, the hasher at priority 3 from its ticket through the copy-out
+            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 4>), pgrid, pblock, 0, stream, arena, arena_bytes,
+                               files, wg_file, nwg, total_blocks, seed, out);
+            break;
+        case 8:  // A/B: 128-byte segments (4) with the copy-out and next DMA at priority 3
+            hipLaunchKernelGGL((block_sums_staged<10, 3>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
+                               total_blocks, seed, out);
             break;
         case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel
             if (aligned)
