@@ -359,9 +359,10 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 // 4-byte aligned): each piece is fetched from the block's start rounded down
 // to 4 bytes, one 16-byte unit longer (the pad unit carries data), and the
 // lane funnel-shifts its words (alignbyte) as the direct kernel does.
-// PRIO (A/B) = 3: the wave runs at priority 3 from its segment wait through
-// the next segment's DMA issue, 0 while it hashes.
-template <int KIND, int PRIO = 0>
+// (Wave priority 3 from the segment wait through the next DMA issue, 0 while
+// hashing, as park does: no gain at B = 1024 / 4096 / 128 KiB,
+// profiles/r04g_blocklen_sweep.jsonl, so not kept.)
+template <int KIND>
 __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
@@ -437,7 +438,6 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     } while (0)
 #define RSG_READ_SEGMENT()                                                                                       \
     do {                                                                                                         \
-        if (PRIO) __builtin_amdgcn_s_setprio(3);                                                                 \
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                                         \
         _Pragma("unroll") for (int q_ = 0; q_ < (int)(SEG / 16) + (UNAL ? 1 : 0); q_++) {                        \
             const uint4 v_ = *reinterpret_cast<const uint4 *>(mine + 16 * q_);                                  \
@@ -456,7 +456,6 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     for (uint32_t cs = 0; cs < S; cs++) {
         const bool more = cs + 1 < S;
         if (MODE != 2 && more) RSG_DMA_SEGMENT(cs + 1);  // in flight while segment cs hashes
-        if (PRIO) __builtin_amdgcn_s_setprio(0);
         if (MODE == 1) {
 #pragma unroll
             for (int q = 0; q < (int)(SEG / 4); q++) h[q & 3] ^= R[q];
@@ -777,9 +776,10 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
 // PRIO: wave priorities (s_setprio) -- 0 = none; 3 (the product) = loader
 // waves at priority 3 (a slot's next DMA issues ahead of the hasher sharing
 // the SIMD) and hashers at 3 while they copy a slot out (the slot frees
-// sooner), 0 while they hash; 4 (A/B) = as 3, the hasher raised already while
-// it waits for its slot.  (8-round A/B, profiles/r04f_ab_park_prio.json:
-// none 0.1984 ms, loaders only 0.1962, copy-out at 2 0.1950, 3 0.1942.)
+// sooner), 0 while they hash.  (8-round A/B, profiles/r04f_ab_park_prio.json:
+// none 0.1984 ms, loaders only 0.1962, copy-out at 2 0.1950, at 3 0.1942;
+// raising the hasher already while it waits for its slot: no gain,
+// profiles/r04g_ab_park_prio_ticket.json.)
 template <int MODE, int NL, int AUX, int PRIO = 0>
 __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
@@ -874,9 +874,8 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
         const uint64_t t = blockIdx.x + (uint64_t)k * G;
         if (t >= ntiles) break;
         const uint32_t slot = k % kPkSlots;
-        if (PRIO == 4) __builtin_amdgcn_s_setprio(3);
         while (pk_load(&sh.full[slot]) != k) __builtin_amdgcn_s_sleep(1);
-        if (PRIO == 3) __builtin_amdgcn_s_setprio(3);
+        if (PRIO >= 3) __builtin_amdgcn_s_setprio(3);
         const uint32_t n = sh.n[slot][lane];
         const uint32_t kind = __builtin_amdgcn_readfirstlane(sh.kind[slot]);
         const uint64_t g = t * 64 + lane;
@@ -974,12 +973,12 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                 break;
             case 3:
                 if (max_blen <= kRegMaxBytes)
-                    hipLaunchKernelGGL((block_sums_park<1, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes,
+                    hipLaunchKernelGGL((block_sums_park<1, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                        files, wg_file, nwg, total_blocks, seed, out);
                 break;
             case 4:
                 if (max_blen <= kRegMaxBytes)
-                    hipLaunchKernelGGL((block_sums_park<2, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes,
+                    hipLaunchKernelGGL((block_sums_park<2, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                        files, wg_file, nwg, total_blocks, seed, out);
                 break;
             case 5:
@@ -996,7 +995,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                 break;
             case 8:
                 if (max_blen <= kRegMaxBytes)
-                    hipLaunchKernelGGL((block_sums_park<3, kParkLoaders, 2>), pgrid, pblock, 0, stream, arena, arena_bytes,
+                    hipLaunchKernelGGL((block_sums_park<3, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                        files, wg_file, nwg, total_blocks, seed, out);
                 break;
         }
@@ -1014,9 +1013,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v >= 7)) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
-    if ((v == 2 || v == 7) && max_blen > kRegMaxBytes) v = 1;
+    if (v == 2 && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
             hipLaunchKernelGGL((block_sums_staged<0>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
@@ -1025,14 +1024,6 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                files, wg_file, nwg, total_blocks, seed, out);
-            break;
-        case 7:  // A/B: park, the hasher at priority 3 from its ticket through the copy-out
-            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 4>), pgrid, pblock, 0, stream, arena, arena_bytes,
-                               files, wg_file, nwg, total_blocks, seed, out);
-            break;
-        case 8:  // A/B: 128-byte segments (4) with the copy-out and next DMA at priority 3
-            hipLaunchKernelGGL((block_sums_staged<10, 3>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
-                               total_blocks, seed, out);
             break;
         case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel
             if (aligned)

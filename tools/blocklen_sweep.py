@@ -28,7 +28,7 @@ SHAPES = [  # (files, file bytes, block length, arenas)
     (256, 4 << 20, 4096, 2),      # 4 KiB blocks
     (1, 32 << 30, 131072, 1),     # cfg5's per-GPU share: one 32 GiB file
 ]
-VARIANTS = {1: "staged", 4: "staged_seg128", 8: "staged_seg128_prio", 5: "staged_seg512", 2: "park", 3: "long_deep_prefetch"}
+VARIANTS = {1: "staged", 4: "staged_seg128", 5: "staged_seg512", 2: "park", 3: "long_deep_prefetch"}
 DIAGS = {1: "diag_staged_memory_only", 2: "diag_staged_hash_only", 6: "diag_linear_read_ldsdma"}
 
 
