@@ -1118,16 +1118,16 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                files, wg_file, nwg, total_blocks, seed, out);
             break;
-        case 7:  // A/B: self-loading park, publish after chunk 3 / 6 / 9
+        case 7:  // A/B: self-loading park, publish after chunk 3 / 0 / 1
             hipLaunchKernelGGL((block_sums_selfpark<3>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file,
                                nwg, total_blocks, seed, out);
             break;
         case 8:
-            hipLaunchKernelGGL((block_sums_selfpark<6>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file,
+            hipLaunchKernelGGL((block_sums_selfpark<0>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file,
                                nwg, total_blocks, seed, out);
             break;
         case 9:
-            hipLaunchKernelGGL((block_sums_selfpark<9>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file,
+            hipLaunchKernelGGL((block_sums_selfpark<1>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file,
                                nwg, total_blocks, seed, out);
             break;
         case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel
