@@ -917,100 +917,6 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     }
 }
 
-// Self-loading park (A/B): the same 3-slot ring and tiles as park, but all 8
-// waves hash (two per SIMD: one wave alone issues VALU at half the SIMD's
-// rate, MI355X_MICROARCH.md constants table) and there are no loader waves.
-// The hasher that copies ticket k out of slot s refills s with ticket k + 3
-// right away (the slot is free once its own ds_reads completed), hashes its
-// block, and publishes k + 3 after chunk CW once its vmcnt drains (the DMA
-// had CW chunks of hashing to land).  Waves 0..2 fill tickets 0..2 first.
-template <int CW>
-__global__ __launch_bounds__(kPkThreads) void block_sums_selfpark(
-    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
-    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
-    uint8_t *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) PkShared sh;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (threadIdx.x < kPkSlots) sh.full[threadIdx.x] = ~0u;
-    if (threadIdx.x == 0) sh.ticket = 0;
-    __syncthreads();
-    const uint64_t ntiles = (total_blocks + 63) / 64;
-    const uint32_t G = gridDim.x;
-    // Fill slot kk % 3 with ticket kk: lengths and kind to LDS, the DMA issued.
-    // Returns true when a DMA is in flight (publish after vmcnt); a direct
-    // tile is published here.
-    auto fill = [&](uint32_t kk) -> bool {
-        const uint64_t tt = blockIdx.x + (uint64_t)kk * G;
-        if (tt >= ntiles) return false;
-        const uint32_t s = kk % kPkSlots;
-        PkDesc d;
-        pk_locate(tt, d, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
-        sh.n[s][lane] = d.n;
-        if (lane == 0) sh.kind[s] = d.staged ? 1u : 0u;
-        if (d.staged) {
-            pk_issue<2, false>(arena, &sh.tile[s][0], d, lane);
-            return true;
-        }
-        if (lane == 0) pk_store(&sh.full[s], kk);
-        return false;
-    };
-    auto publish = [&](uint32_t kk) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) pk_store(&sh.full[kk % kPkSlots], kk);
-    };
-    if (wave < kPkSlots) {
-        __builtin_amdgcn_s_setprio(3);
-        if (fill(wave)) publish(wave);
-        __builtin_amdgcn_s_setprio(0);
-    }
-#pragma unroll 1
-    for (;;) {
-        uint32_t k = 0;
-        if (lane == 0) k = __hip_atomic_fetch_add(&sh.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        k = __builtin_amdgcn_readfirstlane(k);
-        const uint64_t t = blockIdx.x + (uint64_t)k * G;
-        if (t >= ntiles) break;
-        const uint32_t slot = k % kPkSlots;
-        while (pk_load(&sh.full[slot]) != k) __builtin_amdgcn_s_sleep(1);
-        __builtin_amdgcn_s_setprio(3);
-        const uint32_t n = sh.n[slot][lane];
-        const uint32_t kind = __builtin_amdgcn_readfirstlane(sh.kind[slot]);
-        const uint64_t g = t * 64 + lane;
-        const uint32_t kn = k + kPkSlots;
-        if (kind) {
-            uint32_t h[4];
-            md4_init(h);
-            int32_t s1 = 0;
-            uint32_t tw = 0;
-            uint32_t R[16 * kRegChunks];
-            const uint8_t *mine = &sh.tile[slot][0] + lane * kPkPiece;
-#pragma unroll
-            for (uint32_t q = 0; q < 4 * kRegChunks; q++) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
-                R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            const bool pend = fill(kn);
-            __builtin_amdgcn_s_setprio(0);
-            const uint32_t nfull = n >> 6;
-#pragma unroll
-            for (uint32_t c = 0; c < kRegChunks; c++) {
-                if (c == (uint32_t)CW && pend) publish(kn);
-                if (c < nfull) hash_chunk<true>(R + 16 * c, 0u, 0u, c, h, s1, tw);
-                else if (c == nfull) hash_tail<true>(R + 16 * c, 0u, 0u, n, seed, h, s1, tw);
-            }
-            store_record(out, g, n, s1, tw, h);
-        } else {
-            if (fill(kn)) publish(kn);
-            __builtin_amdgcn_s_setprio(0);
-            if (lane == 0 && t * 64 + 64 <= total_blocks) count_fallback(1);
-            if (g < total_blocks) pk_direct(arena, arena_bytes, files, wg_file, nwg256, g, seed, out);
-        }
-    }
-}
-
-
 // Kernel variants (rsg_set_block_sums_kernel; identical results, only speed
 // differs): -1 = automatic, 0 = direct per-lane loads, 1 = staged LDS-DMA
 // slabs (256-byte segments), 2 = park (three loader waves + five hashers with
@@ -1106,9 +1012,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v >= 7)) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
-    if ((v == 2 || v >= 7) && max_blen > kRegMaxBytes) v = 1;
+    if (v == 2 && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
             hipLaunchKernelGGL((block_sums_staged<0>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
@@ -1117,18 +1023,6 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                files, wg_file, nwg, total_blocks, seed, out);
-            break;
-        case 7:  // A/B: self-loading park, publish after chunk 3 / 0 / 1
-            hipLaunchKernelGGL((block_sums_selfpark<3>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file,
-                               nwg, total_blocks, seed, out);
-            break;
-        case 8:
-            hipLaunchKernelGGL((block_sums_selfpark<0>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file,
-                               nwg, total_blocks, seed, out);
-            break;
-        case 9:
-            hipLaunchKernelGGL((block_sums_selfpark<1>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file,
-                               nwg, total_blocks, seed, out);
             break;
         case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel
             if (aligned)
