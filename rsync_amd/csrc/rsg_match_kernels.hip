@@ -657,7 +657,10 @@ __device__ __forceinline__ u16x2 pair_bytes(uint32_t wa, uint32_t wb, int p) {
 // DIAG (timing only, RSG_ROLL_DIAG; candidates meaningless): 1 = interior
 // hits never parked (ORed into a sink), 2 = no filter reads (an opaque zero
 // word: nothing hits).
-template <int NBITS, bool EDGE, int DIAG = 0>
+// MASK (A/B): interior hits collect in a per-lane 32-bit mask (bit j = the
+// lane's offset j) and are parked once per tile; the hit's packed sum is
+// re-rolled from a snapshot taken at its group's first pair.
+template <int NBITS, bool EDGE, int DIAG = 0, bool MASK = false>
 __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
     uint32_t t_int, uint32_t tile_hi, const uint16_t *__restrict__ filter_g, const uint32_t *__restrict__ keys,
@@ -901,9 +904,15 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
             Sx[k] = S[k] ^ 0x80808080u;
         }
         constexpr int G = 4;  // pair steps per group: 8 filter reads in flight
+        uint32_t hmask = 0;           // MASK: bit j = a hit at the lane's offset j
+        u16x2 sn1[H / G], sn2[H / G];  // MASK: (P1, P2) at each group's first pair
 #pragma unroll
         for (int g0 = 0; g0 < H; g0 += G) {
             u16x2 p1[G], p2[G], wd[G];
+            if constexpr (MASK) {
+                sn1[g0 / G] = P1;
+                sn2[g0 / G] = P2;
+            }
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
                 const int j = g0 + jj;
@@ -934,12 +943,54 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 const uint32_t r1 = as_u32(p1[jj]), r2 = as_u32(p2[jj]);
                 if constexpr (DIAG == 1) {
                     dsink |= z ^ r1 ^ r2;
+                } else if constexpr (MASK) {
+                    hmask |= z << j;  // stream a's offset j -> bit j, stream b's -> bit 16 + j
                 } else {
                     park((z & 0xffffu) != 0, (uint32_t)j, __builtin_amdgcn_perm(r2, r1, 0x05040100u));
                     park(z > 0xffffu, (uint32_t)(H + j), __builtin_amdgcn_perm(r2, r1, 0x07060302u));
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (MASK) {
+            // Park the tile's hits, one per lane per round.  Hit b = offset
+            // j = b & 15 of stream b >> 4: (P1, P2) re-rolled from the
+            // snapshot at pair 4 (j >> 2), j & 3 steps, with that group's
+            // bytes (word j >> 2 of each stream).
+#pragma unroll 1
+            for (;;) {
+                const bool hit = hmask != 0;
+                if (!__ballot(hit)) break;
+                uint32_t b = 0, raw = 0;
+                if (hit) {
+                    b = (uint32_t)__builtin_ctz(hmask);
+                    hmask &= hmask - 1u;
+                    const uint32_t j = b & 15u, g = j >> 2, r = j & 3u;
+                    auto pick = [&](const uint32_t *w, uint32_t base) {
+                        const uint32_t lo = (g & 1u) ? w[base + 1] : w[base + 0];
+                        const uint32_t hi = (g & 1u) ? w[base + 3] : w[base + 2];
+                        return (g & 2u) ? hi : lo;
+                    };
+                    const uint32_t oa = pick(Ox, 0), ob = pick(Ox, OW / 2), sa = pick(Sx, 0), sb = pick(Sx, OW / 2);
+                    const uint32_t c1lo = (g & 1u) ? as_u32(sn1[1]) : as_u32(sn1[0]);
+                    const uint32_t c1hi = (g & 1u) ? as_u32(sn1[3]) : as_u32(sn1[2]);
+                    const uint32_t c2lo = (g & 1u) ? as_u32(sn2[1]) : as_u32(sn2[0]);
+                    const uint32_t c2hi = (g & 1u) ? as_u32(sn2[3]) : as_u32(sn2[2]);
+                    u16x2 q1 = as_u16x2((g & 2u) ? c1hi : c1lo), q2 = as_u16x2((g & 2u) ? c2hi : c2lo);
+#pragma unroll
+                    for (int p = 0; p < G - 1; p++) {
+                        const u16x2 uo = pair_bytes(oa, ob, p), ui = pair_bytes(sa, sb, p);
+                        const u16x2 n1 = q1 + ui - uo;
+                        const u16x2 n2 = q2 + uo * negB + n1;
+                        if ((uint32_t)p < r) {
+                            q1 = n1;
+                            q2 = n2;
+                        }
+                    }
+                    raw = __builtin_amdgcn_perm(as_u32(q2), as_u32(q1), (b >> 4) ? 0x07060302u : 0x05040100u);
+                }
+                park(hit, b, raw);
+            }
         }
         // the tile's last lane ends at the next tile's first window
         if (threadIdx.x == kRollThreads - 1) {
@@ -1057,6 +1108,14 @@ static bool roll_edge_inside() {
     return v;
 }
 
+bool roll_mask() {  // A/B switch: RSG_ROLL_MASK=1 parks hits per tile (roll_packed_kernel MASK)
+    static const bool v = [] {
+        const char *e = getenv("RSG_ROLL_MASK");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 int roll_diag() {  // timing diagnostics only (roll_packed_kernel DIAG)
     static const int v = [] {
         const char *e = getenv("RSG_ROLL_DIAG");
@@ -1105,6 +1164,7 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                 // the whole range: the packed kernel rolls its edge tiles itself
                 const uint32_t ga = min(grid, tile_hi - tile_lo);
                 auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, true> : roll_packed_kernel<2, true>;
+                if (roll_mask()) kern = roll_packed_kernel<3, true, 0, true>;
                 if (roll_diag() == 1) kern = roll_packed_kernel<3, true, 1>;
                 if (roll_diag() == 2) kern = roll_packed_kernel<3, true, 2>;
                 hipLaunchKernelGGL(kern, dim3(ga), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
