@@ -966,17 +966,20 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                     b = (uint32_t)__builtin_ctz(hmask);
                     hmask &= hmask - 1u;
                     const uint32_t j = b & 15u, g = j >> 2, r = j & 3u;
-                    auto pick = [&](const uint32_t *w, uint32_t base) {
-                        const uint32_t lo = (g & 1u) ? w[base + 1] : w[base + 0];
-                        const uint32_t hi = (g & 1u) ? w[base + 3] : w[base + 2];
-                        return (g & 2u) ? hi : lo;
+                    // register selects as bit masks (v_bfi): a ?: tree over
+                    // the arrays becomes a scratch-indexed load otherwise
+                    uint32_t m1 = 0u - (g & 1u), m2 = 0u - ((g >> 1) & 1u);
+                    asm("" : "+v"(m1), "+v"(m2));
+                    auto sel4 = [&](uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+                        const uint32_t lo = (w1 & m1) | (w0 & ~m1), hi = (w3 & m1) | (w2 & ~m1);
+                        return (hi & m2) | (lo & ~m2);
                     };
-                    const uint32_t oa = pick(Ox, 0), ob = pick(Ox, OW / 2), sa = pick(Sx, 0), sb = pick(Sx, OW / 2);
-                    const uint32_t c1lo = (g & 1u) ? as_u32(sn1[1]) : as_u32(sn1[0]);
-                    const uint32_t c1hi = (g & 1u) ? as_u32(sn1[3]) : as_u32(sn1[2]);
-                    const uint32_t c2lo = (g & 1u) ? as_u32(sn2[1]) : as_u32(sn2[0]);
-                    const uint32_t c2hi = (g & 1u) ? as_u32(sn2[3]) : as_u32(sn2[2]);
-                    u16x2 q1 = as_u16x2((g & 2u) ? c1hi : c1lo), q2 = as_u16x2((g & 2u) ? c2hi : c2lo);
+                    const uint32_t oa = sel4(Ox[0], Ox[1], Ox[2], Ox[3]);
+                    const uint32_t ob = sel4(Ox[OW / 2], Ox[OW / 2 + 1], Ox[OW / 2 + 2], Ox[OW / 2 + 3]);
+                    const uint32_t sa = sel4(Sx[0], Sx[1], Sx[2], Sx[3]);
+                    const uint32_t sb = sel4(Sx[OW / 2], Sx[OW / 2 + 1], Sx[OW / 2 + 2], Sx[OW / 2 + 3]);
+                    u16x2 q1 = as_u16x2(sel4(as_u32(sn1[0]), as_u32(sn1[1]), as_u32(sn1[2]), as_u32(sn1[3])));
+                    u16x2 q2 = as_u16x2(sel4(as_u32(sn2[0]), as_u32(sn2[1]), as_u32(sn2[2]), as_u32(sn2[3])));
 #pragma unroll
                     for (int p = 0; p < G - 1; p++) {
                         const u16x2 uo = pair_bytes(oa, ob, p), ui = pair_bytes(sa, sb, p);
