@@ -408,7 +408,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         // the previous tile's first 64 parked hits: entry and bucket loads now
         uint2 pe = make_uint2(0, 0);
         uint64_t pb[2 * kBucketWays];
-        const bool pv = lane < prev_n;
+        const bool pv = DIAG != 3 && lane < prev_n;
         if (pv) {
             pe = queue[wave][qh ^ 1][lane];
             const uint64_t *b1 = table + (uint64_t)(bucket_hash1(pe.y) & bmask) * kBucketWays;
@@ -656,7 +656,7 @@ __device__ __forceinline__ u16x2 pair_bytes(uint32_t wa, uint32_t wb, int p) {
 // roll_kernel and passes t_int = tile_hi).
 // DIAG (timing only, RSG_ROLL_DIAG; candidates meaningless): 1 = interior
 // hits never parked (ORed into a sink), 2 = no filter reads (an opaque zero
-// word: nothing hits).
+// word: nothing hits), 3 = hits parked but never probed.
 // MASK (A/B): interior hits collect in a per-lane 32-bit mask (bit j = the
 // lane's offset j) and are parked once per tile; the hit's packed sum is
 // re-rolled from a snapshot taken at its group's first pair.
@@ -784,7 +784,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         if (next) fetch_plain(t + 1, On, A);
         uint2 pe = make_uint2(0, 0);
         uint4 pba, pbb;
-        const bool pv = lane < prev_n;
+        const bool pv = DIAG != 3 && lane < prev_n;
         if (pv) {
             pe = queue[wave][qh ^ 1][lane];
             pe.y = unraw(pe.y);
@@ -1002,7 +1002,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         }
         }  // interior tile
         if (pv) probe(prev_q0 + pe.x, table_has(pba, pbb, pe.y));
-        if (prev_n > 64) drain_rest(qh ^ 1, prev_q0, 64, prev_n);
+        if (DIAG != 3 && prev_n > 64) drain_rest(qh ^ 1, prev_q0, 64, prev_n);
         prev_n = nq;
         prev_q0 = q0;
         qh ^= 1u;
@@ -1012,7 +1012,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         }
         have = next;
     }
-    drain_rest(qh ^ 1, prev_q0, 0, prev_n);
+    if (DIAG != 3) drain_rest(qh ^ 1, prev_q0, 0, prev_n);
     if (DIAG == 1 && dsink == 0x9e3779b9u) cand[0] = dsink;  // keeps the diagnostic's checks alive
 }
 
@@ -1170,6 +1170,7 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                 if (roll_mask()) kern = roll_packed_kernel<3, true, 0, true>;
                 if (roll_diag() == 1) kern = roll_packed_kernel<3, true, 1>;
                 if (roll_diag() == 2) kern = roll_packed_kernel<3, true, 2>;
+                if (roll_diag() == 3) kern = roll_mask() ? roll_packed_kernel<3, true, 3, true> : roll_packed_kernel<3, true, 3>;
                 hipLaunchKernelGGL(kern, dim3(ga), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
                                    t_int, tile_hi, filter16, table_keys, bmask, cand, cap, count);
                 return hipGetLastError();
