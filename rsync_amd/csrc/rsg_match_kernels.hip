@@ -408,7 +408,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
         // the previous tile's first 64 parked hits: entry and bucket loads now
         uint2 pe = make_uint2(0, 0);
         uint64_t pb[2 * kBucketWays];
-        const bool pv = DIAG != 3 && lane < prev_n;
+        const bool pv = lane < prev_n;
         if (pv) {
             pe = queue[wave][qh ^ 1][lane];
             const uint64_t *b1 = table + (uint64_t)(bucket_hash1(pe.y) & bmask) * kBucketWays;
