@@ -38,7 +38,7 @@ int32_t rd_i32(const uint8_t *p) {
 // reference's h.Write of every token's data, receiver.go:159-164).
 rsg_status apply(rsg_ctx *ctx, const uint8_t *tokens, uint64_t tokens_len, const rsg_sum_head *head,
                  const uint8_t *basis, uint64_t basis_len, uint8_t *out, uint64_t out_cap, uint64_t *out_len,
-                 uint64_t *sum_at, Md4 *h = nullptr) {
+                 uint64_t *sum_at, Md4 *h = nullptr, std::atomic<uint64_t> *progress = nullptr) {
     if (!head || !out_len || (tokens_len && !tokens))
         return fail(ctx, RSG_ERR_INVALID, "NULL argument");
     uint64_t pos = 0, off = 0;
@@ -71,6 +71,7 @@ rsg_status apply(rsg_ctx *ctx, const uint8_t *tokens, uint64_t tokens_len, const
         if (out && off + n <= out_cap) {
             memcpy(out + off, data, n);
             if (h) h->update(out + off, n);
+            if (progress) progress->store(off + n, std::memory_order_release);
         } else if (out) {
             fits = false;
         }
@@ -98,6 +99,10 @@ void md4_seeded(Md4 &h, int32_t seed) {
 // beside the GPU pipeline: a host core does one chain at ~1 GiB/s.
 // RSG_RECV_MD4 = gpu / host forces one side (tests, A/B).
 constexpr uint64_t kHostMd4MinBytes = 4ull << 20;
+// rsg_receive_data: files at least this large apply their tokens on a second
+// thread while the caller's thread hashes behind it (one thread below: the
+// thread start costs more than it saves).
+constexpr uint64_t kPipelineMinBytes = 8ull << 20;
 int recv_md4_mode() {  // read per call: tests switch it within one process
     const char *e = getenv("RSG_RECV_MD4");
     return (e && !strcmp(e, "gpu")) ? 1 : ((e && !strcmp(e, "host")) ? 2 : 0);
@@ -193,8 +198,37 @@ rsg_status rsg_receive_data(rsg_ctx *ctx, const uint8_t *tokens, uint64_t tokens
     Md4 h;
     md4_seeded(h, seed);
     uint64_t sum_at = 0;
-    rsg_status s = apply(ctx, tokens, tokens_len, head, basis, basis_len, out, out_cap, out_len, &sum_at,
-                         gpu ? nullptr : &h);
+    rsg_status s;
+    if (!gpu && out && out_cap >= kPipelineMinBytes) {
+        // A large file: the tokens are applied (byte copies, first touches
+        // of out) on a worker thread while this thread hashes the rebuilt
+        // prefix behind it, so the call takes about the MD4 chain alone.
+        std::atomic<uint64_t> done{0};
+        std::atomic<bool> finished{false};
+        std::thread copier([&] {
+            s = apply(ctx, tokens, tokens_len, head, basis, basis_len, out, out_cap, out_len, &sum_at, nullptr,
+                      &done);
+            finished.store(true, std::memory_order_release);
+        });
+        uint64_t hashed = 0;
+        for (;;) {
+            const bool fin = finished.load(std::memory_order_acquire);
+            const uint64_t d = done.load(std::memory_order_acquire);
+            if (d > hashed) {
+                h.update(out + hashed, d - hashed);
+                hashed = d;
+            } else if (fin) {
+                break;
+            } else {
+                std::this_thread::yield();
+            }
+        }
+        copier.join();
+        if (s == RSG_OK && hashed != *out_len) s = fail(ctx, RSG_ERR_INVALID, "internal: hashed %llu of %llu bytes",
+                                                        (unsigned long long)hashed, (unsigned long long)*out_len);
+    } else {
+        s = apply(ctx, tokens, tokens_len, head, basis, basis_len, out, out_cap, out_len, &sum_at, gpu ? nullptr : &h);
+    }
     if (s != RSG_OK) return s;
     if (sum_at + 16 > tokens_len)  // io.ReadFull(remoteSum), receiver.go:167-170
         return fail(ctx, RSG_ERR_INVALID, "token stream ends before the whole-file sum");

@@ -167,6 +167,33 @@ def test_delta_round_trip_on_gpu(eng, seed_case, recv_md4, monkeypatch):
     assert e.value.status == rsync_amd._lib.ERR_CORRUPT
 
 
+@pytest.mark.gpu
+def test_receive_data_large_pipelined(eng):
+    """A file past rsg_receive_data's pipeline threshold (8 MiB): tokens are
+    applied on a worker thread while the caller's thread hashes behind it.
+    Same bytes, same sum check (receiver.go:117-120,159-173), corruption
+    still caught."""
+    import rsync_amd
+    basis = cases.splitmix64_bytes(931, (24 << 20) + 12345)
+    src = cases.mutate(basis, 932, 0.3, 1, 200_000, n_ins=4, n_del=4)
+    seed = -123456789
+    heads, rec, _ = eng.block_sums([basis], seed, 0)
+    head = heads[0].astuple()
+    s1, s2 = orc.parse_records(rec)
+    matches = eng.hash_search(src, head, s1, s2, orc.stable_targets(s1), seed)
+    fsum = eng.file_sums([src], rsync_amd.FILESUM_SEEDED, seed)[0]
+    stream = rsync_amd.encode_tokens(src, head, matches) + fsum
+    want, used_o = orc.receive_data(stream, head, basis, seed)
+    got, used = eng.receive_data(stream, head, basis, seed)
+    assert len(got) >= (8 << 20)
+    assert got == want == src.tobytes() and used == used_o == len(stream)
+    bad = bytearray(stream)
+    bad[-1] ^= 0x01
+    with pytest.raises(rsync_amd.RsgError) as e:
+        eng.receive_data(bytes(bad), head, basis, seed)
+    assert e.value.status == rsync_amd._lib.ERR_CORRUPT
+
+
 def _random_delta(k, seed):
     rng = np.random.default_rng(500 + k)
     n = int(rng.integers(1, 400_000))
