@@ -660,7 +660,7 @@ __device__ __forceinline__ u16x2 pair_bytes(uint32_t wa, uint32_t wb, int p) {
 // MASK (A/B): interior hits collect in a per-lane 32-bit mask (bit j = the
 // lane's offset j) and are parked once per tile; the hit's packed sum is
 // re-rolled from a snapshot taken at its group's first pair.
-template <int NBITS, bool EDGE, int DIAG = 0, bool MASK = false>
+template <int NBITS, bool EDGE, int DIAG = 0, bool MASK = false, bool MASK_G8 = false>
 __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
     uint32_t t_int, uint32_t tile_hi, const uint16_t *__restrict__ filter_g, const uint32_t *__restrict__ keys,
@@ -903,19 +903,21 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
             Ox[k] = O[k] ^ 0x80808080u;
             Sx[k] = S[k] ^ 0x80808080u;
         }
-        constexpr int G = 4;  // pair steps per group: 8 filter reads in flight
-        uint32_t hmask = 0;           // MASK: bit j = a hit at the lane's offset j
-        u16x2 sn1[H / G], sn2[H / G];  // MASK: (P1, P2) at each group's first pair
+        // pair steps per group: 2 G filter reads in flight (MASK_G8: 8)
+        constexpr int G = (MASK && MASK_G8) ? 8 : 4;
+        constexpr int SG = 4;          // MASK: snapshot every SG pairs
+        uint32_t hmask = 0;            // MASK: bit j = a hit at the lane's offset j
+        u16x2 sn1[H / SG], sn2[H / SG];  // MASK: (P1, P2) at pairs 0, SG, 2 SG, ...
 #pragma unroll
         for (int g0 = 0; g0 < H; g0 += G) {
             u16x2 p1[G], p2[G], wd[G];
-            if constexpr (MASK) {
-                sn1[g0 / G] = P1;
-                sn2[g0 / G] = P2;
-            }
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
                 const int j = g0 + jj;
+                if (MASK && j % SG == 0) {
+                    sn1[j / SG] = P1;
+                    sn2[j / SG] = P2;
+                }
                 p1[jj] = P1;
                 p2[jj] = P2;
                 const u16x2 X = P1 ^ P2;  // the word index of both windows
@@ -981,7 +983,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                     u16x2 q1 = as_u16x2(sel4(as_u32(sn1[0]), as_u32(sn1[1]), as_u32(sn1[2]), as_u32(sn1[3])));
                     u16x2 q2 = as_u16x2(sel4(as_u32(sn2[0]), as_u32(sn2[1]), as_u32(sn2[2]), as_u32(sn2[3])));
 #pragma unroll
-                    for (int p = 0; p < G - 1; p++) {
+                    for (int p = 0; p < SG - 1; p++) {
                         const u16x2 uo = pair_bytes(oa, ob, p), ui = pair_bytes(sa, sb, p);
                         const u16x2 n1 = q1 + ui - uo;
                         const u16x2 n2 = q2 + uo * negB + n1;
@@ -1119,6 +1121,14 @@ bool roll_mask() {  // A/B switch: RSG_ROLL_MASK=1 parks hits per tile (roll_pac
     return v;
 }
 
+bool roll_mask_g8() {  // A/B switch: RSG_ROLL_MASK=8: MASK with 8-pair groups
+    static const bool v = [] {
+        const char *e = getenv("RSG_ROLL_MASK");
+        return e && e[0] == '8';
+    }();
+    return v;
+}
+
 int roll_diag() {  // timing diagnostics only (roll_packed_kernel DIAG)
     static const int v = [] {
         const char *e = getenv("RSG_ROLL_DIAG");
@@ -1168,6 +1178,7 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                 const uint32_t ga = min(grid, tile_hi - tile_lo);
                 auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, true> : roll_packed_kernel<2, true>;
                 if (roll_mask()) kern = roll_packed_kernel<3, true, 0, true>;
+                if (roll_mask_g8()) kern = roll_packed_kernel<3, true, 0, true, true>;
                 if (roll_diag() == 1) kern = roll_packed_kernel<3, true, 1>;
                 if (roll_diag() == 2) kern = roll_packed_kernel<3, true, 2>;
                 if (roll_diag() == 3) kern = roll_mask() ? roll_packed_kernel<3, true, 3, true> : roll_packed_kernel<3, true, 3>;
