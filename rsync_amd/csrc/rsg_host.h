@@ -48,6 +48,7 @@ struct SearchSlot {
     PinBuf count;                      // candidate count read back
     DevBuf res;                        // confirmation results (block index per window)
     PinBuf hres;                       // ... read back; the job's walk reads them on a worker thread
+    PinBuf hlist;                      // candidate list read back (pinned: a pageable D2H waits on other streams)
     hipEvent_t scanned = nullptr;      // prefix pass done (side stream)
     hipEvent_t rolled = nullptr;       // roll kernel + count read-back done
     hipEvent_t confirmed = nullptr;    // confirmation batch + result read-back done

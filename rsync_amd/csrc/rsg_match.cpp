@@ -416,10 +416,14 @@ rsg_status confirm_all(Search &S, uint32_t n, std::vector<uint64_t> &key) {
     if ((s = run_hook(S, false)) != RSG_OK) return s;  // the next job's roll, if its tables are built
     // the list, keyed (offset << 22 | list index) so the sort carries each
     // offset's record index (offsets < 2^42, indices < kCandCap = 2^22)
-    key.resize(n);
-    RSG_HIP(ctx, hipMemcpyAsync(key.data(), sl.list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, S.copy));
+    // (into pinned memory: a copy into pageable memory is staged by the
+    // runtime and measured 0.5-1.1 ms here, waiting behind the next roll)
+    if ((s = ensure_pin(ctx, sl.hlist, (uint64_t)n * 8)) != RSG_OK) return s;
+    RSG_HIP(ctx, hipMemcpyAsync(sl.hlist.p, sl.list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, S.copy));
     RSG_HIP(ctx, hipStreamSynchronize(S.copy));
-    for (uint32_t i = 0; i < n; i++) key[i] = (key[i] << 22) | i;
+    key.resize(n);
+    const uint64_t *hl = (const uint64_t *)sl.hlist.p;
+    for (uint32_t i = 0; i < n; i++) key[i] = (hl[i] << 22) | i;
     sort_offsets(key, 22);
     S.pt.mark("c.sort");
     return run_hook(S, false);
@@ -697,9 +701,11 @@ rsg_status finish(Search &S) {
             continue;
         }
         C.resize(n);
-        if (n) {
-            RSG_HIP(ctx, hipMemcpyAsync(C.data(), sl.list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, S.copy));
+        if (n) {  // through pinned memory, as confirm_all
+            if ((s = ensure_pin(ctx, sl.hlist, (uint64_t)n * 8)) != RSG_OK) return s;
+            RSG_HIP(ctx, hipMemcpyAsync(sl.hlist.p, sl.list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, S.copy));
             RSG_HIP(ctx, hipStreamSynchronize(S.copy));
+            memcpy(C.data(), sl.hlist.p, (size_t)n * 8);
         }
         sort_offsets(C);
         C.erase(std::unique(C.begin(), C.end()), C.end());
