@@ -48,7 +48,10 @@ rsg_status ensure_dev(rsg_ctx *ctx, DevBuf &b, uint64_t bytes) {
         b.p = nullptr;
         b.cap = 0;
     }
-    uint64_t want = std::max<uint64_t>(bytes, 4096);
+    // headroom: a regrow frees first (hipFree waits for the whole device), so
+    // a buffer that grows a little per call (the sender's per-file candidate
+    // counts) should not regrow every call
+    uint64_t want = std::max<uint64_t>(bytes + std::min<uint64_t>(bytes / 4, 64ull << 20), 4096);
     RSG_HIP(ctx, hipMalloc(&b.p, want));
     b.cap = want;
     return RSG_OK;
@@ -61,7 +64,7 @@ rsg_status ensure_pin(rsg_ctx *ctx, PinBuf &b, uint64_t bytes) {
         b.p = nullptr;
         b.cap = 0;
     }
-    uint64_t want = std::max<uint64_t>(bytes, 4096);
+    uint64_t want = std::max<uint64_t>(bytes + std::min<uint64_t>(bytes / 4, 64ull << 20), 4096);
     RSG_HIP(ctx, hipHostMalloc(&b.p, want, hipHostMallocDefault));
     b.cap = want;
     return RSG_OK;
@@ -269,10 +272,11 @@ void rsg_ctx_destroy(rsg_ctx *c) {
     for (DevBuf *b : dbs)
         if (b->p) hipFree(b->p);
     for (SearchSlot &sl : c->search) {
-        DevBuf *sbs[] = {&sl.agg, &sl.prefix, &sl.counts, &sl.list, &sl.blob, &sl.src, &sl.res};
+        DevBuf *sbs[] = {&sl.agg, &sl.prefix, &sl.counts, &sl.blob, &sl.src, &sl.res};
         for (DevBuf *b : sbs)
             if (b->p) hipFree(b->p);
         if (sl.count.p) hipHostFree(sl.count.p);
+        if (sl.list.p) hipHostFree(sl.list.p);
         if (sl.stage.p) hipHostFree(sl.stage.p);
         if (sl.hres.p) hipHostFree(sl.hres.p);
         if (sl.scanned) hipEventDestroy(sl.scanned);

@@ -413,16 +413,14 @@ rsg_status confirm_all(Search &S, uint32_t n, std::vector<uint64_t> &key) {
     RSG_HIP(ctx, hipMemcpyAsync(sl.hres.p, sl.res.p, (uint64_t)n * 4, hipMemcpyDeviceToHost, S.cst));
     if (!sl.confirmed) RSG_HIP(ctx, hipEventCreateWithFlags(&sl.confirmed, sync_event_flags()));
     RSG_HIP(ctx, hipEventRecord(sl.confirmed, S.cst));
+    S.pt.mark("c.launch");
     if ((s = run_hook(S, false)) != RSG_OK) return s;  // the next job's roll, if its tables are built
+    S.pt.mark("c.hook");
     // the list, keyed (offset << 22 | list index) so the sort carries each
     // offset's record index (offsets < 2^42, indices < kCandCap = 2^22)
-    // (into pinned memory: a copy into pageable memory is staged by the
-    // runtime and measured 0.5-1.1 ms here, waiting behind the next roll)
-    if ((s = ensure_pin(ctx, sl.hlist, (uint64_t)n * 8)) != RSG_OK) return s;
-    RSG_HIP(ctx, hipMemcpyAsync(sl.hlist.p, sl.list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, S.copy));
-    RSG_HIP(ctx, hipStreamSynchronize(S.copy));
+    // (the roll wrote it to pinned host memory; `rolled` was waited for)
     key.resize(n);
-    const uint64_t *hl = (const uint64_t *)sl.hlist.p;
+    const uint64_t *hl = (const uint64_t *)sl.list.p;
     for (uint32_t i = 0; i < n; i++) key[i] = (hl[i] << 22) | i;
     sort_offsets(key, 22);
     S.pt.mark("c.sort");
@@ -582,7 +580,7 @@ rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
     if (!sl.rolled) RSG_HIP(ctx, hipEventCreateWithFlags(&sl.rolled, sync_event_flags()));
     if ((s = ensure_dev(ctx, sl.agg, (uint64_t)S.ntiles * sizeof(TileAgg) + 64)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, sl.prefix, ((uint64_t)S.ntiles + 1) * sizeof(TilePrefix) + 64)) != RSG_OK) return s;
-    if ((s = ensure_dev(ctx, sl.list, (uint64_t)kCandCap * 8)) != RSG_OK) return s;
+    if ((s = ensure_pin(ctx, sl.list, (uint64_t)kCandCap * 8)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, sl.counts, 64)) != RSG_OK) return s;
     if ((s = ensure_pin(ctx, sl.count, 64)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, sl.blob, S.blob_bytes)) != RSG_OK) return s;
@@ -701,12 +699,7 @@ rsg_status finish(Search &S) {
             continue;
         }
         C.resize(n);
-        if (n) {  // through pinned memory, as confirm_all
-            if ((s = ensure_pin(ctx, sl.hlist, (uint64_t)n * 8)) != RSG_OK) return s;
-            RSG_HIP(ctx, hipMemcpyAsync(sl.hlist.p, sl.list.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, S.copy));
-            RSG_HIP(ctx, hipStreamSynchronize(S.copy));
-            memcpy(C.data(), sl.hlist.p, (size_t)n * 8);
-        }
+        if (n) memcpy(C.data(), sl.list.p, (size_t)n * 8);  // pinned host memory the roll wrote
         sort_offsets(C);
         C.erase(std::unique(C.begin(), C.end()), C.end());
         if ((s = walk(S, C, pos)) != RSG_OK) return s;
