@@ -654,13 +654,7 @@ __device__ __forceinline__ u16x2 pair_bytes(uint32_t wa, uint32_t wb, int p) {
 // NBITS: filter bits per sum, S2[0..3], S2[4..7] (and S2[8..11]); EDGE: the
 // kernel rolls the range's edge tiles itself (else the host leaves them to
 // roll_kernel and passes t_int = tile_hi).
-// DIAG (timing only, RSG_ROLL_DIAG; candidates meaningless): 1 = interior
-// hits never parked (ORed into a sink), 2 = no filter reads (an opaque zero
-// word: nothing hits), 3 = hits parked but never probed.
-// MASK (A/B): interior hits collect in a per-lane 32-bit mask (bit j = the
-// lane's offset j) and are parked once per tile; the hit's packed sum is
-// re-rolled from a snapshot taken at its group's first pair.
-template <int NBITS, bool EDGE, int DIAG = 0, bool MASK = false, bool MASK_G8 = false>
+template <int NBITS, bool EDGE>
 __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
     uint32_t t_int, uint32_t tile_hi, const uint16_t *__restrict__ filter_g, const uint32_t *__restrict__ keys,
@@ -764,7 +758,6 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         }
     };
     const u16x2 negB = as_u16x2(((0x10000u - (B & 0xffffu)) & 0xffffu) * 0x10001u);
-    uint32_t dsink = 0;  // DIAG 1
     bool have = false;  // O, A already hold tile t's bytes (prefetched)
     for (uint32_t t = t_begin; t < t_end; t++) {
         const uint64_t q0 = (uint64_t)t * kScanTile;
@@ -784,7 +777,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         if (next) fetch_plain(t + 1, On, A);
         uint2 pe = make_uint2(0, 0);
         uint4 pba, pbb;
-        const bool pv = DIAG != 3 && lane < prev_n;
+        const bool pv = lane < prev_n;
         if (pv) {
             pe = queue[wave][qh ^ 1][lane];
             pe.y = unraw(pe.y);
@@ -903,31 +896,17 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
             Ox[k] = O[k] ^ 0x80808080u;
             Sx[k] = S[k] ^ 0x80808080u;
         }
-        // pair steps per group: 2 G filter reads in flight (MASK_G8: 8)
-        constexpr int G = (MASK && MASK_G8) ? 8 : 4;
-        constexpr int SG = 4;          // MASK: snapshot every SG pairs
-        uint32_t hmask = 0;            // MASK: bit j = a hit at the lane's offset j
-        u16x2 sn1[H / SG], sn2[H / SG];  // MASK: (P1, P2) at pairs 0, SG, 2 SG, ...
+        constexpr int G = 4;  // pair steps per group: 8 filter reads in flight
 #pragma unroll
         for (int g0 = 0; g0 < H; g0 += G) {
             u16x2 p1[G], p2[G], wd[G];
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
                 const int j = g0 + jj;
-                if (MASK && j % SG == 0) {
-                    sn1[j / SG] = P1;
-                    sn2[j / SG] = P2;
-                }
                 p1[jj] = P1;
                 p2[jj] = P2;
                 const u16x2 X = P1 ^ P2;  // the word index of both windows
-                if constexpr (DIAG == 2) {
-                    uint32_t zw;
-                    asm volatile("v_and_b32 %0, 0, %1" : "=v"(zw) : "v"(as_u32(X)));
-                    wd[jj] = as_u16x2(zw);
-                } else {
-                    wd[jj] = u16x2{filt[X.x], filt[X.y]};
-                }
+                wd[jj] = u16x2{filt[X.x], filt[X.y]};
                 const u16x2 uo = pair_bytes(Ox[j >> 2], Ox[(j >> 2) + OW / 2], j & 3);
                 const u16x2 ui = pair_bytes(Sx[j >> 2], Sx[(j >> 2) + OW / 2], j & 3);
                 P1 = P1 + ui - uo;
@@ -943,59 +922,10 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 uint32_t z = as_u32(xy) & 0x00010001u;
                 asm("" : "+v"(z));
                 const uint32_t r1 = as_u32(p1[jj]), r2 = as_u32(p2[jj]);
-                if constexpr (DIAG == 1) {
-                    dsink |= z ^ r1 ^ r2;
-                } else if constexpr (MASK) {
-                    hmask |= z << j;  // stream a's offset j -> bit j, stream b's -> bit 16 + j
-                } else {
-                    park((z & 0xffffu) != 0, (uint32_t)j, __builtin_amdgcn_perm(r2, r1, 0x05040100u));
-                    park(z > 0xffffu, (uint32_t)(H + j), __builtin_amdgcn_perm(r2, r1, 0x07060302u));
-                }
+                park((z & 0xffffu) != 0, (uint32_t)j, __builtin_amdgcn_perm(r2, r1, 0x05040100u));
+                park(z > 0xffffu, (uint32_t)(H + j), __builtin_amdgcn_perm(r2, r1, 0x07060302u));
             }
             __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (MASK) {
-            // Park the tile's hits, one per lane per round.  Hit b = offset
-            // j = b & 15 of stream b >> 4: (P1, P2) re-rolled from the
-            // snapshot at pair 4 (j >> 2), j & 3 steps, with that group's
-            // bytes (word j >> 2 of each stream).
-#pragma unroll 1
-            for (;;) {
-                const bool hit = hmask != 0;
-                if (!__ballot(hit)) break;
-                uint32_t b = 0, raw = 0;
-                if (hit) {
-                    b = (uint32_t)__builtin_ctz(hmask);
-                    hmask &= hmask - 1u;
-                    const uint32_t j = b & 15u, g = j >> 2, r = j & 3u;
-                    // register selects as bit masks (v_bfi): a ?: tree over
-                    // the arrays becomes a scratch-indexed load otherwise
-                    uint32_t m1 = 0u - (g & 1u), m2 = 0u - ((g >> 1) & 1u);
-                    asm("" : "+v"(m1), "+v"(m2));
-                    auto sel4 = [&](uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
-                        const uint32_t lo = (w1 & m1) | (w0 & ~m1), hi = (w3 & m1) | (w2 & ~m1);
-                        return (hi & m2) | (lo & ~m2);
-                    };
-                    const uint32_t oa = sel4(Ox[0], Ox[1], Ox[2], Ox[3]);
-                    const uint32_t ob = sel4(Ox[OW / 2], Ox[OW / 2 + 1], Ox[OW / 2 + 2], Ox[OW / 2 + 3]);
-                    const uint32_t sa = sel4(Sx[0], Sx[1], Sx[2], Sx[3]);
-                    const uint32_t sb = sel4(Sx[OW / 2], Sx[OW / 2 + 1], Sx[OW / 2 + 2], Sx[OW / 2 + 3]);
-                    u16x2 q1 = as_u16x2(sel4(as_u32(sn1[0]), as_u32(sn1[1]), as_u32(sn1[2]), as_u32(sn1[3])));
-                    u16x2 q2 = as_u16x2(sel4(as_u32(sn2[0]), as_u32(sn2[1]), as_u32(sn2[2]), as_u32(sn2[3])));
-#pragma unroll
-                    for (int p = 0; p < SG - 1; p++) {
-                        const u16x2 uo = pair_bytes(oa, ob, p), ui = pair_bytes(sa, sb, p);
-                        const u16x2 n1 = q1 + ui - uo;
-                        const u16x2 n2 = q2 + uo * negB + n1;
-                        if ((uint32_t)p < r) {
-                            q1 = n1;
-                            q2 = n2;
-                        }
-                    }
-                    raw = __builtin_amdgcn_perm(as_u32(q2), as_u32(q1), (b >> 4) ? 0x07060302u : 0x05040100u);
-                }
-                park(hit, b, raw);
-            }
         }
         // the tile's last lane ends at the next tile's first window
         if (threadIdx.x == kRollThreads - 1) {
@@ -1004,7 +934,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         }
         }  // interior tile
         if (pv) probe(prev_q0 + pe.x, table_has(pba, pbb, pe.y));
-        if (DIAG != 3 && prev_n > 64) drain_rest(qh ^ 1, prev_q0, 64, prev_n);
+        if (prev_n > 64) drain_rest(qh ^ 1, prev_q0, 64, prev_n);
         prev_n = nq;
         prev_q0 = q0;
         qh ^= 1u;
@@ -1014,8 +944,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         }
         have = next;
     }
-    if (DIAG != 3) drain_rest(qh ^ 1, prev_q0, 0, prev_n);
-    if (DIAG == 1 && dsink == 0x9e3779b9u) cand[0] = dsink;  // keeps the diagnostic's checks alive
+    drain_rest(qh ^ 1, prev_q0, 0, prev_n);
 }
 
 // --------------------------------------------------------------- confirm plan
@@ -1113,30 +1042,6 @@ static bool roll_edge_inside() {
     return v;
 }
 
-bool roll_mask() {  // A/B switch: RSG_ROLL_MASK=1 parks hits per tile (roll_packed_kernel MASK)
-    static const bool v = [] {
-        const char *e = getenv("RSG_ROLL_MASK");
-        return e && e[0] == '1';
-    }();
-    return v;
-}
-
-bool roll_mask_g8() {  // A/B switch: RSG_ROLL_MASK=8: MASK with 8-pair groups
-    static const bool v = [] {
-        const char *e = getenv("RSG_ROLL_MASK");
-        return e && e[0] == '8';
-    }();
-    return v;
-}
-
-int roll_diag() {  // timing diagnostics only (roll_packed_kernel DIAG)
-    static const int v = [] {
-        const char *e = getenv("RSG_ROLL_DIAG");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-
 int roll_filter_bits() {
     static const int v = [] {
         // A/B switch: 2 = bits S2[0..3], S2[4..7] only; default 3 adds S2[8..11]
@@ -1177,11 +1082,6 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                 // the whole range: the packed kernel rolls its edge tiles itself
                 const uint32_t ga = min(grid, tile_hi - tile_lo);
                 auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, true> : roll_packed_kernel<2, true>;
-                if (roll_mask()) kern = roll_packed_kernel<3, true, 0, true>;
-                if (roll_mask_g8()) kern = roll_packed_kernel<3, true, 0, true, true>;
-                if (roll_diag() == 1) kern = roll_packed_kernel<3, true, 1>;
-                if (roll_diag() == 2) kern = roll_packed_kernel<3, true, 2>;
-                if (roll_diag() == 3) kern = roll_mask() ? roll_packed_kernel<3, true, 3, true> : roll_packed_kernel<3, true, 3>;
                 hipLaunchKernelGGL(kern, dim3(ga), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
                                    t_int, tile_hi, filter16, table_keys, bmask, cand, cap, count);
                 return hipGetLastError();

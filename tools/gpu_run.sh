@@ -25,12 +25,6 @@ for S in "$@"; do
     receive) timeout -k 10 300 python bench.py --workload receive > gpurun_out/${TAG}_receive.json 2> gpurun_out/${TAG}_receive.err || exit 1 ;;
     prof_cfg2) bash tools/profile_kernel.sh ${TAG}_cfg2 block_sums --steps 20 --warmup 5 --no-cpu --no-host-path --no-delivery || exit 1 ;;
     prof_cfg3) PASSES="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE;SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE;FETCH_SIZE" bash tools/profile_kernel.sh ${TAG}_cfg3 roll --workload cfg3 --steps 2 --warmup 1 --cfg3-files 4 --no-cpu --no-host-path || exit 1 ;;
-    rolldiag) for D in 0 1 2 0 1 2; do RSG_ROLL_DIAG=$D timeout -k 10 200 python bench.py --workload cfg3 --cfg3-files 4 --steps 3 --no-cpu --no-host-path > gpurun_out/${TAG}_rolldiag$D.json 2>> gpurun_out/${TAG}_rolldiag.err && cat gpurun_out/${TAG}_rolldiag$D.json >> gpurun_out/${TAG}_rolldiag.jsonl || exit 1; done ;;
-    rollmask) RSG_ROLL_MASK=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_match.py tests/test_gpu_sender_fd.py -m gpu -x -q $T > gpurun_out/${TAG}_rollmask_tests.log 2>&1 || { tail -30 gpurun_out/${TAG}_rollmask_tests.log; exit 1; }
-      for M in 0 1 0 1; do RSG_ROLL_MASK=$M timeout -k 10 200 python bench.py --workload cfg3 --cfg3-files 4 --steps 3 --no-host-path > gpurun_out/${TAG}_rollmask$M.json 2>> gpurun_out/${TAG}_rollmask.err && cat gpurun_out/${TAG}_rollmask$M.json >> gpurun_out/${TAG}_rollmask.jsonl || exit 1; done ;;
-    rolldiag3) for C in "0 0" "1 0" "0 3" "1 3" "0 0" "1 0" "0 3" "1 3"; do set -- $C; RSG_ROLL_MASK=$1 RSG_ROLL_DIAG=$2 timeout -k 10 200 python bench.py --workload cfg3 --cfg3-files 4 --steps 3 --no-cpu --no-host-path > gpurun_out/${TAG}_rd.json 2>> gpurun_out/${TAG}_rolldiag3.err && { echo "mask=$1 diag=$2"; cat gpurun_out/${TAG}_rd.json; } >> gpurun_out/${TAG}_rolldiag3.txt || exit 1; done ;;
-    rollab) RSG_ROLL_MASK=8 timeout -k 10 400 python -u -m pytest tests/test_gpu_match.py tests/test_gpu_sender_fd.py -m gpu -x -q $T > gpurun_out/${TAG}_rollab_tests.log 2>&1 || { tail -30 gpurun_out/${TAG}_rollab_tests.log; exit 1; }
-      for M in 0 1 8 0 1 8 0 1 8; do RSG_ROLL_MASK=$M timeout -k 10 200 python bench.py --workload cfg3 --steps 3 --no-cpu --no-host-path > gpurun_out/${TAG}_ra.json 2>> gpurun_out/${TAG}_rollab.err && { echo "mask=$M"; cat gpurun_out/${TAG}_ra.json; } >> gpurun_out/${TAG}_rollab.txt || exit 1; done ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
 done
