@@ -562,8 +562,11 @@ def bench_sender(args, rank, world, local):
     eng.kernel_times(reset=True)
     t0 = time.perf_counter()
     nm = 0
+    call_ms = []
     for _ in range(steps):
+        c0 = time.perf_counter()
         res = eng.hash_search_batch(jobs, SEED, as_arrays=True)
+        call_ms.append(round((time.perf_counter() - c0) * 1e3, 3))
         nm += sum(len(m) for m in res)
     dt = time.perf_counter() - t0
     kt = eng.kernel_times(reset=True)  # HIP events around every roll / confirmation on their own streams
@@ -619,7 +622,7 @@ def bench_sender(args, rank, world, local):
                           "config": {"workload": "cfg3: 10 x 1 GiB sources vs 50%-modified bases, B=32768",
                                      "files": args.cfg3_files, "matches_per_pass": nm // steps,
                                      "call": "rsg_hash_search_batch_device, one call per pass"},
-                          "ms_per_file": round(dt * 1e3 / (steps * len(metas)), 3),
+                          "ms_per_file": round(dt * 1e3 / (steps * len(metas)), 3), "call_ms": call_ms,
                           "single_file_calls_gib_s": single_gib_s,
                           "roofline": {"bound": "hbm", "kernel": "roll_packed_kernel (edge tiles included)",
                                        "note": "the roll is VALU-issue-bound (integer ops at 4 cycles per wave64, "

@@ -108,7 +108,10 @@ struct Search {
     std::function<bool()> hook_ready;        // hook() would not wait
     std::function<rsg_status()> tail;        // set by finish(): the rest of the job (wait + walk), any thread
     // device tables inside the slot's blob
-    uint64_t off_hi16 = 0, off_sum2 = 0, off_filter = 0, off_filter16 = 0, off_table = 0, off_keys = 0, blob_bytes = 0;
+    uint64_t off_filter = 0, off_filter16 = 0, off_table = 0, off_keys = 0, blob_a_bytes = 0;  // part A
+    uint64_t off_groups = 0, off_hi16 = 0, off_sum2 = 0, blob_bytes = 0;                       // part B
+    std::future<rsg_status> part_b;  // part B's build (a worker's), if not done inline
+    bool part_b_up = false;          // part B's upload is queued
     const uint2 *d_groups = nullptr;
     const uint32_t *d_hi16 = nullptr, *d_filter = nullptr;
     const uint16_t *d_filter16 = nullptr;  // packed roll (nullptr: not built)
@@ -175,6 +178,20 @@ rsg_status run_hook(Search &S, bool block) {
     return h();
 }
 
+// Part B on the device before the first resolve of this search: waits for its
+// build (a worker's) and queues its upload on the confirmation stream.
+rsg_status need_resolve_tables(Search &S) {
+    if (S.part_b_up) return RSG_OK;
+    if (S.part_b.valid()) {
+        const rsg_status s = S.part_b.get();
+        if (s != RSG_OK) return s;
+    }
+    RSG_HIP(S.ctx, hipMemcpyAsync((uint8_t *)S.sl->blob.p + S.off_groups, (uint8_t *)S.sl->stage.p + S.off_groups,
+                                  S.blob_bytes - S.off_groups, hipMemcpyHostToDevice, S.cst));
+    S.part_b_up = true;
+    return RSG_OK;
+}
+
 // Confirm a batch of candidates (indices into C): Checksum1 + MD4(window ||
 // seed) on the GPU, then the first block in targets order whose sums and
 // length agree.  res[i]: -2 unknown, -1 no match, else the block index.
@@ -203,6 +220,7 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
     for (uint32_t w = 0; w <= plan.nwg; w++)
         plan.wg_file[w] = (uint32_t)std::min<uint64_t>((uint64_t)w * rsg::kBlockSumThreads, idx.size() - 1);
     rsg_status s;
+    if ((s = need_resolve_tables(S)) != RSG_OK) return s;
     S.pt.mark("v.plan");
     if ((s = ensure_dev(ctx, ctx->d_files, plan.files.size() * sizeof(DevFile) + 32)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, ctx->d_wg, plan.wg_file.size() * sizeof(uint32_t) + 4)) != RSG_OK) return s;
@@ -393,6 +411,7 @@ rsg_status confirm_all(Search &S, uint32_t n, std::vector<uint64_t> &key) {
     plan.max_blen = (uint32_t)S.head.block_len;  // windows are at most B long
     plan.lds_reserve = S.confirm_lds;
     rsg_status s;
+    if ((s = need_resolve_tables(S)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, ctx->d_files, (uint64_t)n * sizeof(DevFile) + 32)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, ctx->d_wg, ((uint64_t)plan.nwg + 1) * sizeof(uint32_t) + 4)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, ctx->d_out[0], (uint64_t)n * kRecordBytes)) != RSG_OK) return s;
@@ -451,10 +470,15 @@ rsg_status confirm_all_tail(Search &S, const std::vector<uint64_t> &key, uint64_
 }
 
 // Stage 1 of a search, host part: the basis tables, packed into the slot's
-// pinned staging blob.  Basis sums grouped by Sum1 in targets order (resolve
-// tables); Bloom filter of every Sum1 + a 2-choice bucketed table {Sum1,
-// flags: bit1 = a block of length B, bit2 = the remainder block}.
-rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets) {
+// pinned staging blob in two parts.  Part A is what the roll reads: Bloom
+// filter of every Sum1 + the packed roll's 16-bit filter + a 2-choice bucketed
+// table {Sum1, flags: bit1 = a block of length B, bit2 = the remainder block}
+// (and its key-only copy), built straight from the sums (no sort), so the
+// roll can start before part B exists.  Part B is what the confirmation's
+// resolve reads: basis sums grouped by Sum1 in targets order, their sum2s.
+// Blob layout: filter | filter16 | table | keys | groups | hi16 | sum2.
+rsg_status tables_roll(Search &S, const uint32_t *sum1, const int32_t *targets) {
+    (void)targets;
     rsg_ctx *ctx = S.ctx;
     SearchSlot &sl = *S.sl;
     TableScratch &T = sl.hs;
@@ -465,6 +489,99 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
     const uint64_t ntiles64 = (S.size + kScanTile - 1) / kScanTile;
     if (ntiles64 >= 0xFFFFFFF0ull) return fail(ctx, RSG_ERR_INVALID, "source too large");
     S.ntiles = (uint32_t)ntiles64;
+    // distinct Sum1 -> flags, inserted into the bucket table directly (an
+    // existing key ORs its flags: match.go:108's candidates are every block
+    // with that Sum1)
+    uint32_t nb = 16;
+    while (nb < (uint32_t)count / 2) nb <<= 1;
+    auto &table = T.table;
+    auto &fill = T.fill;
+    constexpr uint32_t W = rsg::kBucketWays;
+    uint32_t first_key = 0;
+    for (;;) {
+        table.assign((size_t)nb * W, 0);
+        fill.assign(nb, 0);
+        bool ok = true;
+        for (int32_t k = 0; k < count && ok; k++) {
+            const uint32_t v = sum1[k];
+            const uint32_t f = 1u | ((S.len_of(k) == B) ? 2u : 4u);
+            if (k == 0) first_key = v;
+            const uint32_t h1 = rsg::bucket_hash1(v) & (nb - 1), h2 = rsg::bucket_hash2(v) & (nb - 1);
+            bool found = false;
+            for (uint32_t hh : {h1, h2}) {
+                for (uint32_t w = 0; w < fill[hh] && !found; w++) {
+                    uint64_t &e = table[(size_t)hh * W + w];
+                    if ((uint32_t)(e >> 32) == v) {
+                        e |= f;
+                        found = true;
+                    }
+                }
+                if (found || h2 == h1) break;
+            }
+            if (found) continue;
+            const uint32_t h = fill[h2] < fill[h1] ? h2 : h1;
+            if (fill[h] == W) {
+                ok = false;
+                break;
+            }
+            table[(size_t)h * W + fill[h]++] = ((uint64_t)v << 32) | f;
+        }
+        if (ok) break;
+        nb <<= 1;
+    }
+    S.bmask = nb - 1;
+    auto &bitmap = T.bitmap;
+    bitmap.assign(rsg::kFilterBits / 32, 0);
+    const bool sel = rsg::roll_filter_sel();
+    auto &filter16 = T.filter16;  // the packed roll's filter (interior tiles of the fused mode)
+    filter16.clear();
+    const bool packed = (uint32_t)B <= rsg::kFusedMaxB && rsg::roll_packed();
+    if (packed) filter16.assign(rsg::kFilter16Words, 0);
+    const int nbits = rsg::roll_filter_bits();
+    auto &tkeys = T.table_keys;  // the packed roll's key-only copy
+    tkeys.resize(table.size());
+    for (size_t i = 0; i < table.size(); i++) {
+        const uint64_t e = table[i];
+        const uint32_t key = (uint32_t)(e >> 32);
+        tkeys[i] = (uint32_t)e != 0 ? key : first_key;  // empty slots: a key that exists
+        if ((uint32_t)e == 0) continue;
+        if (sel) {
+            bitmap[rsg::sel_word(key)] |= rsg::sel_mask(key);
+        } else {
+            const uint32_t h = rsg::filter_hash(key);
+            bitmap[rsg::filter_word(h)] |= rsg::filter_mask(h);
+        }
+        if (packed) filter16[rsg::f16_word(key, (uint32_t)B)] |= (uint16_t)rsg::f16_mask(key, nbits);
+    }
+    // blob layout, 256-byte aligned parts; the whole blob is sized here so
+    // part B never regrows the stage under part A's upload
+    auto up = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
+    const uint64_t n_filter = bitmap.size() * 4, n_table = table.size() * 8, n_filter16 = filter16.size() * 2;
+    const uint64_t n_groups = (uint64_t)count * 8, n_hi16 = 65537ull * 4, n_sum2 = (uint64_t)count * 16;
+    S.off_filter = 0;
+    S.off_filter16 = up(n_filter);
+    S.off_table = S.off_filter16 + up(n_filter16);
+    S.off_keys = S.off_table + up(n_table);
+    S.blob_a_bytes = S.off_keys + up(tkeys.size() * 4);
+    S.off_groups = S.blob_a_bytes;
+    S.off_hi16 = S.off_groups + up(n_groups);
+    S.off_sum2 = S.off_hi16 + up(n_hi16);
+    S.blob_bytes = S.off_sum2 + up(n_sum2);
+    rsg_status s;
+    if ((s = ensure_pin(ctx, sl.stage, S.blob_bytes)) != RSG_OK) return s;
+    uint8_t *st = (uint8_t *)sl.stage.p;
+    memcpy(st + S.off_filter, bitmap.data(), n_filter);
+    if (n_filter16) memcpy(st + S.off_filter16, filter16.data(), n_filter16);
+    memcpy(st + S.off_table, table.data(), n_table);
+    memcpy(st + S.off_keys, tkeys.data(), tkeys.size() * 4);
+    S.pt.mark("tables");
+    return RSG_OK;
+}
+
+// Part B (after tables_roll, which sized the blob).
+rsg_status tables_resolve(Search &S, const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets) {
+    TableScratch &T = S.sl->hs;
+    const int32_t count = S.head.count;
     // (sum1, block) in targets order, stably sorted by sum1: each sum's blocks
     // are one run, in targets order (match.go:108 walks targets in that
     // order); hi16[h] = index of the first sum with high half h.
@@ -491,80 +608,18 @@ rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const in
         for (auto &e : groups) hi16[(e.first >> 16) + 1]++;
         for (size_t h = 1; h < hi16.size(); h++) hi16[h] += hi16[h - 1];
     }
-    S.pt.mark("groups");
-    auto &keys = T.keys;
-    keys.clear();
-    for (size_t i = 0; i < groups.size(); i++) {
-        const uint32_t f = 1u | ((S.len_of(groups[i].second) == B) ? 2u : 4u);
-        if (!keys.empty() && keys.back().first == groups[i].first) keys.back().second |= f;
-        else keys.push_back({groups[i].first, f});
-    }
-    auto &bitmap = T.bitmap;
-    bitmap.assign(rsg::kFilterBits / 32, 0);
-    const bool sel = rsg::roll_filter_sel();
-    for (auto &kv : keys) {
-        if (sel) {
-            bitmap[rsg::sel_word(kv.first)] |= rsg::sel_mask(kv.first);
-        } else {
-            const uint32_t h = rsg::filter_hash(kv.first);
-            bitmap[rsg::filter_word(h)] |= rsg::filter_mask(h);
-        }
-    }
-    // the packed roll's filter (interior tiles of the fused mode)
-    auto &filter16 = T.filter16;
-    filter16.clear();
-    if ((uint32_t)B <= rsg::kFusedMaxB && rsg::roll_packed()) {
-        filter16.assign(rsg::kFilter16Words, 0);
-        const int nbits = rsg::roll_filter_bits();
-        for (auto &kv : keys)
-            filter16[rsg::f16_word(kv.first, (uint32_t)B)] |= (uint16_t)rsg::f16_mask(kv.first, nbits);
-    }
-    uint32_t nb = 16;
-    while (nb < keys.size() / 2) nb <<= 1;
-    auto &table = T.table;
-    auto &fill = T.fill;
-    for (;;) {
-        table.assign((size_t)nb * rsg::kBucketWays, 0);
-        fill.assign(nb, 0);
-        bool ok = true;
-        for (auto &kv : keys) {
-            const uint32_t h1 = rsg::bucket_hash1(kv.first) & (nb - 1), h2 = rsg::bucket_hash2(kv.first) & (nb - 1);
-            const uint32_t h = fill[h2] < fill[h1] ? h2 : h1;
-            if (fill[h] == rsg::kBucketWays) { ok = false; break; }
-            table[(size_t)h * rsg::kBucketWays + fill[h]++] = ((uint64_t)kv.first << 32) | kv.second;
-        }
-        if (ok) break;
-        nb <<= 1;
-    }
-    S.bmask = nb - 1;
-    auto &tkeys = T.table_keys;  // the packed roll's key-only copy
-    tkeys.resize(table.size());
-    for (size_t i = 0; i < table.size(); i++)
-        tkeys[i] = (uint32_t)table[i] != 0 ? (uint32_t)(table[i] >> 32) : (keys.empty() ? 0u : keys[0].first);
-    // blob layout, 256-byte aligned parts
     static_assert(sizeof(groups[0]) == 8, "(sum1, block) pair must be 8 bytes");
-    auto up = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
-    const uint64_t n_groups = groups.size() * 8, n_hi16 = hi16.size() * 4, n_sum2 = (uint64_t)count * 16;
-    const uint64_t n_filter = bitmap.size() * 4, n_table = table.size() * 8, n_filter16 = filter16.size() * 2;
-    S.off_hi16 = up(n_groups);
-    S.off_sum2 = S.off_hi16 + up(n_hi16);
-    S.off_filter = S.off_sum2 + up(n_sum2);
-    S.off_filter16 = S.off_filter + up(n_filter);
-    S.off_table = S.off_filter16 + up(n_filter16);
-    S.off_keys = S.off_table + up(n_table);
-    S.blob_bytes = S.off_keys + up(tkeys.size() * 4);
-    rsg_status s;
-    if ((s = ensure_pin(ctx, sl.stage, S.blob_bytes)) != RSG_OK) return s;
-    uint8_t *st = (uint8_t *)sl.stage.p;
-    if (n_groups) memcpy(st, groups.data(), n_groups);
-    memcpy(st + S.off_hi16, hi16.data(), n_hi16);
-    if (n_sum2) memcpy(st + S.off_sum2, sum2, n_sum2);
-    memcpy(st + S.off_filter, bitmap.data(), n_filter);
-    if (n_filter16) memcpy(st + S.off_filter16, filter16.data(), n_filter16);
-    memcpy(st + S.off_table, table.data(), n_table);
-    memcpy(st + S.off_keys, tkeys.data(), tkeys.size() * 4);
-    S.pt.mark("tables");
-    return RSG_OK;
+    uint8_t *st = (uint8_t *)S.sl->stage.p;
+    if (count) memcpy(st + S.off_groups, groups.data(), (size_t)count * 8);
+    memcpy(st + S.off_hi16, hi16.data(), hi16.size() * 4);
+    if (count) memcpy(st + S.off_sum2, sum2, (size_t)count * 16);
+    return RSG_OK;  // (no S.pt mark: this may run on a worker beside the job's own thread)
+}
+
+// Both parts, in order (callers that need the whole blob at once).
+rsg_status tables(Search &S, const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets) {
+    rsg_status s = tables_roll(S, sum1, targets);
+    return s != RSG_OK ? s : tables_resolve(S, sum1, sum2, targets);
 }
 
 // Stage 1, GPU part.  Side stream: (realigning copy,) prefix pass, blob
@@ -600,10 +655,10 @@ rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
     // The tables' upload (~1.7 MB for a 32 768-block basis) goes on the side
     // stream too: on the compute stream it sat between two files' rolls
     // (≈ 50 µs of PCIe per file in the batch timeline).
-    RSG_HIP(ctx, hipMemcpyAsync(sl.blob.p, sl.stage.p, S.blob_bytes, hipMemcpyHostToDevice, S.side));
+    RSG_HIP(ctx, hipMemcpyAsync(sl.blob.p, sl.stage.p, S.blob_a_bytes, hipMemcpyHostToDevice, S.side));
     RSG_HIP(ctx, hipEventRecord(sl.scanned, S.side));  // also orders the realigning copy and the upload
     const uint8_t *blob = (const uint8_t *)sl.blob.p;
-    S.d_groups = (const uint2 *)blob;
+    S.d_groups = (const uint2 *)(blob + S.off_groups);
     S.d_hi16 = (const uint32_t *)(blob + S.off_hi16);
     S.d_sum2 = blob + S.off_sum2;
     S.d_filter = (const uint32_t *)(blob + S.off_filter);
@@ -749,6 +804,7 @@ bool job_local(rsg_status s) { return s == RSG_ERR_INVALID || s == RSG_ERR_TRUNC
 // lanes, serial MD4 chains) beside a roll kernel ran 3x slower.
 rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed, bool host_src) {
     if (njobs && !jobs) return fail(ctx, RSG_ERR_INVALID, "NULL jobs");
+    PhaseTimer bt;  // RSG_TIMING: the call's start-up and drain
     for (uint64_t i = 0; i < njobs; i++) {
         jobs[i].n_matches = 0;
         jobs[i].status = RSG_OK;
@@ -850,7 +906,16 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
         S->seed = seed;
         Search *raw = S.get();
         Pending &pend = pends[i & 1];
-        pend.tab = std::async(std::launch::async, [raw, &j] { return tables(*raw, j.sum1, j.sum2, j.targets); });
+        // part A (the roll's tables) is what issue() waits for; part B (the
+        // resolve's) follows on the same worker and is waited for at the
+        // job's first confirmation
+        auto part_a = std::make_shared<std::promise<rsg_status>>();
+        pend.tab = part_a->get_future();
+        raw->part_b = std::async(std::launch::async, [raw, &j, part_a] {
+            const rsg_status sa = tables_roll(*raw, j.sum1, j.targets);
+            part_a->set_value(sa);
+            return sa != RSG_OK ? sa : tables_resolve(*raw, j.sum1, j.sum2, j.targets);
+        });
         pend.S = std::move(S);
         pend.i = i;
         pend.valid = true;
@@ -887,6 +952,7 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
         for (uint64_t k = 0; k < std::min<uint64_t>(njobs, 2) && fatal == RSG_OK; k++) fatal = prepare(k);
         for (uint64_t k = 0; k < std::min<uint64_t>(njobs, 2) && fatal == RSG_OK; k++) fatal = issue(k);
     }
+    bt.mark("b.issued");
     for (; fatal == RSG_OK && i < njobs; i++) {
         const uint64_t ahead = overlap ? i + 2 : i + 1;
         // job i+2 takes job i-2's slot: that job's walk (a worker) is done by
@@ -927,6 +993,7 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
         }
         if (!overlap) live[slot].reset();
     }
+    bt.mark("b.loop");
     // the last jobs' walks (and, after a fatal error, any still running)
     for (uint64_t k = i >= kSearchSlots ? i - kSearchSlots : 0; k < i; k++) {
         const rsg_status f = join(k);
@@ -947,6 +1014,7 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
     (void)hipStreamSynchronize(ctx->confirm);
     (void)hipStreamSynchronize(ctx->stream);
     if (first != RSG_OK) ctx->err = first_err;
+    bt.mark("b.drain");
     return first;
 }
 
@@ -1096,13 +1164,15 @@ rsg_status search_fd(rsg_ctx *ctx, int32_t fd, int64_t off0, uint64_t size, cons
             S.size = nread;
             S.ntiles = (uint32_t)((nread + kScanTile - 1) / kScanTile);
             S.end = std::min<int64_t>((int64_t)W, end_global - (int64_t)a);
-            S.off_hi16 = T->off_hi16;
-            S.off_sum2 = T->off_sum2;
             S.off_filter = T->off_filter;
             S.off_filter16 = T->off_filter16;
             S.off_table = T->off_table;
             S.off_keys = T->off_keys;
-            S.blob_bytes = T->blob_bytes;
+            S.blob_a_bytes = T->blob_a_bytes;
+            S.off_groups = T->off_groups;
+            S.off_hi16 = T->off_hi16;
+            S.off_sum2 = T->off_sum2;
+            S.blob_bytes = T->blob_bytes;  // part B is uploaded again per window (need_resolve_tables)
             S.bmask = T->bmask;
             S.pos0 = pos > a ? pos - a : 0;
             if ((s = enqueue_scan(S, (const uint8_t *)ctx->d_in[slot].p, false)) != RSG_OK) return s;
