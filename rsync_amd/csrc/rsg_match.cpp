@@ -489,6 +489,28 @@ rsg_status tables_roll(Search &S, const uint32_t *sum1, const int32_t *targets) 
     const uint64_t ntiles64 = (S.size + kScanTile - 1) / kScanTile;
     if (ntiles64 >= 0xFFFFFFF0ull) return fail(ctx, RSG_ERR_INVALID, "source too large");
     S.ntiles = (uint32_t)ntiles64;
+    // the filters on a second thread (they need only the sums; bits set per
+    // block, a repeated Sum1 sets the same bits)
+    auto &bitmap = T.bitmap;
+    auto &filter16 = T.filter16;  // the packed roll's filter (interior tiles of the fused mode)
+    const bool packed = (uint32_t)B <= rsg::kFusedMaxB && rsg::roll_packed();
+    std::thread filters([&] {
+        bitmap.assign(rsg::kFilterBits / 32, 0);
+        filter16.clear();
+        if (packed) filter16.assign(rsg::kFilter16Words, 0);
+        const bool sel = rsg::roll_filter_sel();
+        const int nbits = rsg::roll_filter_bits();
+        for (int32_t k = 0; k < count; k++) {
+            const uint32_t key = sum1[k];
+            if (sel) {
+                bitmap[rsg::sel_word(key)] |= rsg::sel_mask(key);
+            } else {
+                const uint32_t h = rsg::filter_hash(key);
+                bitmap[rsg::filter_word(h)] |= rsg::filter_mask(h);
+            }
+            if (packed) filter16[rsg::f16_word(key, (uint32_t)B)] |= (uint16_t)rsg::f16_mask(key, nbits);
+        }
+    });
     // distinct Sum1 -> flags, inserted into the bucket table directly (an
     // existing key ORs its flags: match.go:108's candidates are every block
     // with that Sum1)
@@ -530,29 +552,13 @@ rsg_status tables_roll(Search &S, const uint32_t *sum1, const int32_t *targets) 
         nb <<= 1;
     }
     S.bmask = nb - 1;
-    auto &bitmap = T.bitmap;
-    bitmap.assign(rsg::kFilterBits / 32, 0);
-    const bool sel = rsg::roll_filter_sel();
-    auto &filter16 = T.filter16;  // the packed roll's filter (interior tiles of the fused mode)
-    filter16.clear();
-    const bool packed = (uint32_t)B <= rsg::kFusedMaxB && rsg::roll_packed();
-    if (packed) filter16.assign(rsg::kFilter16Words, 0);
-    const int nbits = rsg::roll_filter_bits();
     auto &tkeys = T.table_keys;  // the packed roll's key-only copy
     tkeys.resize(table.size());
     for (size_t i = 0; i < table.size(); i++) {
         const uint64_t e = table[i];
-        const uint32_t key = (uint32_t)(e >> 32);
-        tkeys[i] = (uint32_t)e != 0 ? key : first_key;  // empty slots: a key that exists
-        if ((uint32_t)e == 0) continue;
-        if (sel) {
-            bitmap[rsg::sel_word(key)] |= rsg::sel_mask(key);
-        } else {
-            const uint32_t h = rsg::filter_hash(key);
-            bitmap[rsg::filter_word(h)] |= rsg::filter_mask(h);
-        }
-        if (packed) filter16[rsg::f16_word(key, (uint32_t)B)] |= (uint16_t)rsg::f16_mask(key, nbits);
+        tkeys[i] = (uint32_t)e != 0 ? (uint32_t)(e >> 32) : first_key;  // empty slots: a key that exists
     }
+    filters.join();
     // blob layout, 256-byte aligned parts; the whole blob is sized here so
     // part B never regrows the stage under part A's upload
     auto up = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
