@@ -40,8 +40,14 @@ rsg_status hip_fail(rsg_ctx *ctx, hipError_t e, const char *what) {
                 hipGetErrorString(e), (int)e);
 }
 
+static bool alloc_trace() {  // RSG_TIMING: report every (re)allocation of scratch
+    static const bool on = getenv("RSG_TIMING") != nullptr;
+    return on;
+}
+
 rsg_status ensure_dev(rsg_ctx *ctx, DevBuf &b, uint64_t bytes) {
     if (bytes <= b.cap) return RSG_OK;
+    if (alloc_trace()) fprintf(stderr, "[rsg] alloc dev %llu -> %llu\n", (unsigned long long)b.cap, (unsigned long long)bytes);
     if (b.p) {
         RSG_HIP(ctx, hipStreamSynchronize(ctx->stream));
         hipFree(b.p);
@@ -59,6 +65,7 @@ rsg_status ensure_dev(rsg_ctx *ctx, DevBuf &b, uint64_t bytes) {
 
 rsg_status ensure_pin(rsg_ctx *ctx, PinBuf &b, uint64_t bytes) {
     if (bytes <= b.cap) return RSG_OK;
+    if (alloc_trace()) fprintf(stderr, "[rsg] alloc pin %llu -> %llu\n", (unsigned long long)b.cap, (unsigned long long)bytes);
     if (b.p) {
         hipHostFree(b.p);
         b.p = nullptr;
@@ -280,6 +287,7 @@ void rsg_ctx_destroy(rsg_ctx *c) {
         if (sl.stage.p) hipHostFree(sl.stage.p);
         if (sl.hres.p) hipHostFree(sl.hres.p);
         if (sl.scanned) hipEventDestroy(sl.scanned);
+        if (sl.tables_b) hipEventDestroy(sl.tables_b);
         if (sl.rolled) hipEventDestroy(sl.rolled);
         if (sl.confirmed) hipEventDestroy(sl.confirmed);
     }

@@ -51,6 +51,7 @@ struct SearchSlot {
     DevBuf res;                        // confirmation results (block index per window)
     PinBuf hres;                       // ... read back; the job's walk reads them on a worker thread
     hipEvent_t scanned = nullptr;      // prefix pass done (side stream)
+    hipEvent_t tables_b = nullptr;     // the resolve tables' upload done (side stream)
     hipEvent_t rolled = nullptr;       // roll kernel + count read-back done
     hipEvent_t confirmed = nullptr;    // confirmation batch + result read-back done
 };
