@@ -654,7 +654,9 @@ __device__ __forceinline__ u16x2 pair_bytes(uint32_t wa, uint32_t wb, int p) {
 // NBITS: filter bits per sum, S2[0..3], S2[4..7] (and S2[8..11]); EDGE: the
 // kernel rolls the range's edge tiles itself (else the host leaves them to
 // roll_kernel and passes t_int = tile_hi).
-template <int NBITS, bool EDGE>
+// D16 (A/B, RSG_ROLL_D16=1): a pair's two filter words land in the two halves
+// of one VGPR (ds_read_u16_d16 / _d16_hi) instead of two loads and a v_perm.
+template <int NBITS, bool EDGE, bool D16 = false>
 __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
     uint32_t t_int, uint32_t tile_hi, const uint16_t *__restrict__ filter_g, const uint32_t *__restrict__ keys,
@@ -897,6 +899,8 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
             Sx[k] = S[k] ^ 0x80808080u;
         }
         constexpr int G = 4;  // pair steps per group: 8 filter reads in flight
+        uint32_t one16 = 1;  // D16: the SDWA shift count (a VGPR operand)
+        asm("" : "+v"(one16));
 #pragma unroll
         for (int g0 = 0; g0 < H; g0 += G) {
             u16x2 p1[G], p2[G], wd[G];
@@ -906,12 +910,29 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 p1[jj] = P1;
                 p2[jj] = P2;
                 const u16x2 X = P1 ^ P2;  // the word index of both windows
-                wd[jj] = u16x2{filt[X.x], filt[X.y]};
+                if constexpr (D16) {
+                    // byte addresses 2 X.x, 2 X.y: one SDWA shift each, plus the
+                    // filter's LDS base (0 in practice: the add folds away)
+                    const uint32_t fb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint16_t *)filt;
+                    const uint32_t xa = as_u32(X);
+                    uint32_t alo, ahi, w;
+                    asm("v_lshlrev_b32_sdwa %0, %3, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+                        "v_lshlrev_b32_sdwa %1, %3, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+                        : "=&v"(alo), "=&v"(ahi) : "v"(xa), "v"(one16));
+                    alo += fb;
+                    ahi += fb;
+                    asm volatile("ds_read_u16_d16 %0, %1\n\tds_read_u16_d16_hi %0, %2"
+                                 : "=&v"(w) : "v"(alo), "v"(ahi) : "memory");
+                    wd[jj] = as_u16x2(w);
+                } else {
+                    wd[jj] = u16x2{filt[X.x], filt[X.y]};
+                }
                 const u16x2 uo = pair_bytes(Ox[j >> 2], Ox[(j >> 2) + OW / 2], j & 3);
                 const u16x2 ui = pair_bytes(Sx[j >> 2], Sx[(j >> 2) + OW / 2], j & 3);
                 P1 = P1 + ui - uo;
                 P2 = P2 + uo * negB + P1;
             }
+            if constexpr (D16) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm loads above
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
                 const int j = g0 + jj;
@@ -1042,6 +1063,14 @@ static bool roll_edge_inside() {
     return v;
 }
 
+static bool roll_d16() {  // A/B switch (roll_packed_kernel D16)
+    static const bool v = [] {
+        const char *e = getenv("RSG_ROLL_D16");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 int roll_filter_bits() {
     static const int v = [] {
         // A/B switch: 2 = bits S2[0..3], S2[4..7] only; default 3 adds S2[8..11]
@@ -1082,6 +1111,7 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                 // the whole range: the packed kernel rolls its edge tiles itself
                 const uint32_t ga = min(grid, tile_hi - tile_lo);
                 auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, true> : roll_packed_kernel<2, true>;
+                if (roll_d16()) kern = roll_packed_kernel<3, true, true>;
                 hipLaunchKernelGGL(kern, dim3(ga), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
                                    t_int, tile_hi, filter16, table_keys, bmask, cand, cap, count);
                 return hipGetLastError();
