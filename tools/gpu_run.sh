@@ -13,7 +13,7 @@ for S in "$@"; do
     tests) timeout -k 10 600 python -u -m pytest tests -m gpu -x -v $T > gpurun_out/${TAG}_pytest.log 2>&1 || { tail -30 gpurun_out/${TAG}_pytest.log; exit 1; } ;;
     newtests) timeout -k 10 400 python -u -m pytest tests/test_shard_plan.py tests/test_gpu_sender_fd.py -m gpu -x -v $T > gpurun_out/${TAG}_newtests.log 2>&1 || { tail -30 gpurun_out/${TAG}_newtests.log; exit 1; } ;;
     smoke) timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || exit 1 ;;
-    sweep) SWEEP_SHAPES=1,2,0 SWEEP_ROUNDS=2 timeout -k 10 300 python tools/blocklen_sweep.py > gpurun_out/${TAG}_sweep.jsonl 2> gpurun_out/${TAG}_sweep.err || exit 1 ;;
+    sweep) SWEEP_SHAPES=${SWEEP_SHAPES:-1,4,2,0} SWEEP_ROUNDS=2 timeout -k 10 300 python tools/blocklen_sweep.py > gpurun_out/${TAG}_sweep.jsonl 2> gpurun_out/${TAG}_sweep.err || exit 1 ;;
     variants) timeout -k 10 300 python -u -m pytest tests/test_gpu_blocksums.py -m gpu -x -q $T -k "variants or per_context or cfg2_full" > gpurun_out/${TAG}_variants.log 2>&1 || { tail -30 gpurun_out/${TAG}_variants.log; exit 1; } ;;
     ab8) AB_ROUNDS=8 timeout -k 10 300 python bench.py --ab --steps 30 --no-cpu --no-host-path --no-delivery > gpurun_out/${TAG}_ab8.json 2> gpurun_out/${TAG}_ab8.err || exit 1 ;;
     ab) timeout -k 10 200 python bench.py --ab --steps 30 --no-cpu --no-host-path --no-delivery > gpurun_out/${TAG}_ab.json 2> gpurun_out/${TAG}_ab.err || exit 1 ;;
