@@ -572,9 +572,6 @@ struct PkDesc {
     uint32_t n;    // per lane
 };
 
-// SEG (segpark): blocks of any length, read whole in 704-byte segments: a
-// block's reads reach its length rounded up to 16 bytes, not 704 bytes.
-template <bool SEG = false>
 __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, const DevFile *__restrict__ files,
                                           const uint32_t *__restrict__ wg_file, uint32_t nwg256,
                                           uint64_t total_blocks, uint64_t arena_bytes) {
@@ -597,8 +594,8 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
         d.nl = (uint32_t)(F0.len - (uint64_t)(F0.nblocks - 1) * F0.blen);
         d.n = lane == d.jl ? d.nl : d.B;
         d.off = d.base + (uint64_t)d.B * lane;
-        const uint64_t top = d.base + (uint64_t)d.B * 63 + (SEG ? (uint64_t)((d.B + 15u) & ~15u) : 704u);
-        d.staged = (SEG || d.B <= kRegMaxBytes) && top <= arena_bytes && top - d.base <= 0x7FFFFFFFull;
+        const uint64_t top = d.base + (uint64_t)d.B * 63 + 704u;
+        d.staged = d.B <= kRegMaxBytes && top <= arena_bytes && top - d.base <= 0x7FFFFFFFull;
         return;
     }
     const uint64_t gend = min(g0 + 64, total_blocks);
@@ -633,7 +630,7 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
             if (fe > fb && fe > g0 && fb < gend) {  // the file has blocks in this tile
                 const uint64_t b_first = (g0 > fb ? g0 : fb) - fb, b_last = (gend < fe ? gend : fe) - 1 - fb;
                 const uint64_t o_first = F[i].offset + b_first * F[i].blen;
-                const uint64_t o_top = F[i].offset + b_last * F[i].blen + (SEG ? (uint64_t)((F[i].blen + 15u) & ~15u) : 704u);
+                const uint64_t o_top = F[i].offset + b_last * F[i].blen + 704u;
                 lo_off = o_first < lo_off ? o_first : lo_off;
                 top = o_top > top ? o_top : top;
                 bmax = F[i].blen > bmax ? F[i].blen : bmax;
@@ -644,7 +641,7 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
     d.base = rfl64(lo_off);
     top = rfl64(top);
     bmax = rfl32(bmax);
-    d.staged = (g0 + 64 <= total_blocks) && (SEG || bmax <= kRegMaxBytes) && top <= arena_bytes &&
+    d.staged = (g0 + 64 <= total_blocks) && bmax <= kRegMaxBytes && top <= arena_bytes &&
                top - d.base <= 0x7FFFFFFFull;
     d.off = off;
     d.n = n;
@@ -658,11 +655,9 @@ __device__ __forceinline__ void pk_locate(uint64_t t, PkDesc &d, uint32_t lane, 
 // jj/uu: per-lane block index and byte offset (0x40000000 for the pad) of
 // each instruction, precomputed by the loader (UNROLL); otherwise computed on
 // the fly (a caller short of VGPRs).
-// so (segpark): the tile is bytes [so, so + 704) of every block.
 template <int AUX, bool UNROLL, bool ALN = false>
 __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, const PkDesc &d, uint32_t lane,
-                                         const uint32_t *jj = nullptr, const uint32_t *uu = nullptr,
-                                         uint32_t so = 0) {
+                                         const uint32_t *jj = nullptr, const uint32_t *uu = nullptr) {
     // ALN (timing diagnostic only): every quad request rounded down to a
     // 16-byte boundary of the arena -- the same bytes per tile, naturally
     // aligned, to price the misaligned quads of blocks at a 700-byte stride
@@ -685,11 +680,11 @@ __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, con
         uint32_t vo_;                                                                                           \
         if (REG) {                                                                                              \
             const uint32_t nj_ = j_ == d.jl ? d.nl : d.B;                                                       \
-            vo_ = u16_ + so < nj_ ? (ALN ? ((d.B * j_ + u16_ + amis) & ~15u) : d.B * j_ + so + u16_) : 0x80000000u; \
+            vo_ = u16_ < nj_ ? (ALN ? ((d.B * j_ + u16_ + amis) & ~15u) : d.B * j_ + u16_) : 0x80000000u;     \
         } else {                                                                                                \
             const uint32_t rj_ = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * j_), rel);                  \
             const uint32_t nj_ = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * j_), (int)d.n);             \
-            vo_ = u16_ + so < nj_ ? rj_ + so + u16_ : 0x80000000u;                                              \
+            vo_ = u16_ < nj_ ? rj_ + u16_ : 0x80000000u;                                                        \
         }                                                                                                       \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * (I_)), \
                                                  16, vo_, 0, 0, AUX);                                           \
@@ -725,8 +720,7 @@ __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, con
 #pragma unroll
                 for (uint32_t k = 0; k < kBatch; k++) {
                     const uint32_t u16 = uu[i0 + k];
-                    const uint32_t vo =
-                        u16 + so < nj[k] ? (ALN ? ((rj[k] + u16 + amis) & ~15u) : rj[k] + so + u16) : 0x80000000u;
+                    const uint32_t vo = u16 < nj[k] ? (ALN ? ((rj[k] + u16 + amis) & ~15u) : rj[k] + u16) : 0x80000000u;
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(
                         rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * (i0 + k)), 16, vo, 0, 0, AUX);
                 }
@@ -923,150 +917,6 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     }
 }
 
-// ------------------------------------------------------------ segment park
-// park for blocks longer than 703 bytes (the reference's sqrt sizing: B =
-// 1024..4096 for 1-16 MiB files).  A group = 64 consecutive blocks; its
-// blocks are read in S segments of 704 bytes (segment s = bytes [704 s,
-// 704 s + 704) of every block: 64 pieces at stride B, each a 704-byte run,
-// against the staged kernel's 128/256-byte pieces).  Each segment is one
-// tile of park's 3-slot ring; the hasher that owns the group parks segment
-// after segment in the same 176 VGPRs, carrying the MD4 state and the weak
-// sums between them, and stores the records after the last.
-// Schedule (static, so loaders need no feedback): hasher h (of NH = 5) owns
-// the groups i = 5 q + h of this workgroup; super-round q's tickets are
-// (s, h) in s-major order, k = q 5 S + 5 s + h; slot k % 3, loader k % 3.
-// S is uniform (the batch's longest block); shorter blocks' extra segments
-// are empty tiles (no memory requests).  Tickets of groups past the end are
-// freed by their loader; direct groups (see park) hash at segment 0.
-__global__ __launch_bounds__(kPkThreads) void block_sums_segpark(
-    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
-    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
-    uint8_t *__restrict__ out, uint32_t S) {
-    constexpr uint32_t NL = kPkSlots, NH = kPkWaves - NL;  // one loader per slot
-    __shared__ __attribute__((aligned(16))) PkShared sh;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (threadIdx.x < kPkSlots) {
-        sh.full[threadIdx.x] = ~0u;
-        sh.freeq[threadIdx.x] = threadIdx.x;
-    }
-    __syncthreads();
-    const uint64_t ngroups = (total_blocks + 63) / 64;
-    const uint32_t G = gridDim.x;
-    const uint64_t mine = ngroups > blockIdx.x ? (ngroups - blockIdx.x + G - 1) / G : 0;  // this WG's groups
-    const uint32_t per_round = NH * S;
-
-    if (wave < NL) {
-        __builtin_amdgcn_s_setprio(3);
-        uint32_t jj[kPkDma], uu[kPkDma];
-#pragma unroll
-        for (uint32_t i = 0; i < kPkDma; i++) {
-            const uint32_t idx = 64u * i + lane;
-            jj[i] = idx / 45u;
-            const uint32_t u = idx - 45u * jj[i];
-            uu[i] = u < 44u ? 16u * u : 0x40000000u;
-        }
-        // this loader's tickets k = wave, wave + 3, ...: k -> super-round q,
-        // segment sg, hasher h, group i = 5 q + h (absent past `mine`); the
-        // next ticket's descriptor is located while this ticket's DMA flies
-        const uint32_t kend = (uint32_t)(((mine + NH - 1) / NH) * per_round);
-        auto info = [&](uint32_t kk, uint64_t &i, uint32_t &sg) {
-            const uint32_t q = kk / per_round, r = kk - q * per_round;
-            sg = r / NH;
-            i = (uint64_t)q * NH + (r - sg * NH);
-        };
-        PkDesc cur;
-        uint32_t k = wave;
-        if (k < kend) {
-            uint64_t i;
-            uint32_t sg;
-            info(k, i, sg);
-            if (i < mine) pk_locate<true>(blockIdx.x + i * G, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
-        }
-#pragma unroll 1
-        while (k < kend) {
-            uint64_t i;
-            uint32_t sg;
-            info(k, i, sg);
-            const uint32_t slot = wave;
-            while (pk_load(&sh.freeq[slot]) != k) __builtin_amdgcn_s_sleep(1);
-            const bool present = i < mine;
-            const bool staged = present && cur.staged;
-            if (!present) {
-                if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);  // no such group: the slot goes on
-            } else {
-                sh.n[slot][lane] = cur.n;
-                if (lane == 0) sh.kind[slot] = staged ? 1u : 0u;
-                if (staged) pk_issue<2, true>(arena, &sh.tile[slot][0], cur, lane, jj, uu, 704u * sg);
-            }
-            const uint32_t kn = k + kPkSlots;
-            if (kn < kend) {
-                uint64_t in;
-                uint32_t sgn;
-                info(kn, in, sgn);
-                if (in < mine)
-                    pk_locate<true>(blockIdx.x + in * G, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
-            }
-            if (present) {
-                if (staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) pk_store(&sh.full[slot], k);
-            }
-            k = kn;
-        }
-        return;
-    }
-
-    // ---------------------------------------------------------------- hashers
-    const uint32_t hw = wave - NL;
-#pragma unroll 1
-    for (uint64_t q = 0; q * NH + hw < mine; q++) {
-        const uint64_t grp = blockIdx.x + (q * NH + hw) * G;
-        const uint64_t g = grp * 64 + lane;
-        const uint32_t k0 = (uint32_t)(q * per_round) + hw;
-        uint32_t h[4];
-        md4_init(h);
-        int32_t s1 = 0;
-        uint32_t tw = 0, n = 0, kind = 0;
-#pragma unroll 1
-        for (uint32_t sg = 0; sg < S; sg++) {
-            const uint32_t k = k0 + NH * sg, slot = k % kPkSlots;
-            while (pk_load(&sh.full[slot]) != k) __builtin_amdgcn_s_sleep(1);
-            __builtin_amdgcn_s_setprio(3);
-            if (sg == 0) {
-                n = sh.n[slot][lane];
-                kind = __builtin_amdgcn_readfirstlane(sh.kind[slot]);
-            }
-            if (kind) {
-                uint32_t R[16 * kRegChunks];
-                const uint8_t *src = &sh.tile[slot][0] + lane * kPkPiece;
-#pragma unroll
-                for (uint32_t qd = 0; qd < 4 * kRegChunks; qd++) {
-                    const uint4 v = *reinterpret_cast<const uint4 *>(src + 16 * qd);
-                    R[4 * qd + 0] = v.x; R[4 * qd + 1] = v.y; R[4 * qd + 2] = v.z; R[4 * qd + 3] = v.w;
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);
-                __builtin_amdgcn_s_setprio(0);
-                const uint32_t nfull = n >> 6, c0 = kRegChunks * sg;
-#pragma unroll
-                for (uint32_t c = 0; c < kRegChunks; c++) {
-                    const uint32_t cc = c0 + c;
-                    if (cc < nfull) hash_chunk<true>(R + 16 * c, 0u, 0u, cc, h, s1, tw);
-                    else if (cc == nfull) hash_tail<true>(R + 16 * c, 0u, 0u, n, seed, h, s1, tw);
-                }
-            } else {
-                if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);
-                __builtin_amdgcn_s_setprio(0);
-                if (sg == 0) {
-                    if (lane == 0 && grp * 64 + 64 <= total_blocks) count_fallback(1);
-                    if (g < total_blocks) pk_direct(arena, arena_bytes, files, wg_file, nwg256, g, seed, out);
-                }
-            }
-        }
-        if (kind) store_record(out, g, n, s1, tw, h);
-    }
-}
-
 // Kernel variants (rsg_set_block_sums_kernel; identical results, only speed
 // differs): -1 = automatic, 0 = direct per-lane loads, 1 = staged LDS-DMA
 // slabs (256-byte segments), 2 = park (three loader waves + five hashers with
@@ -1162,7 +1012,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v == 7)) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
     if (v == 2 && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
@@ -1174,12 +1024,6 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                files, wg_file, nwg, total_blocks, seed, out);
             break;
-        case 7: {  // segment park (aligned batches, blocks of any length)
-            const uint32_t S = (max_blen >> 6) / kRegChunks + 1;
-            hipLaunchKernelGGL(block_sums_segpark, pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file, nwg,
-                               total_blocks, seed, out, S);
-            break;
-        }
         case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel
             if (aligned)
                 hipLaunchKernelGGL((block_sums_staged<0>), grid, block, lds_reserve, stream, arena, arena_bytes, files,

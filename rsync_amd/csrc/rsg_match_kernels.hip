@@ -932,7 +932,14 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 P1 = P1 + ui - uo;
                 P2 = P2 + uo * negB + P1;
             }
-            if constexpr (D16) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm loads above
+            if constexpr (D16) {
+                // the asm loads above: the wait carries the words as operands so
+                // no use of them is scheduled before it
+                static_assert(G == 4, "four words");
+                uint32_t w0 = as_u32(wd[0]), w1 = as_u32(wd[1]), w2 = as_u32(wd[2]), w3 = as_u32(wd[3]);
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3) : : "memory");
+                wd[0] = as_u16x2(w0); wd[1] = as_u16x2(w1); wd[2] = as_u16x2(w2); wd[3] = as_u16x2(w3);
+            }
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
                 const int j = g0 + jj;

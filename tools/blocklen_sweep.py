@@ -29,7 +29,7 @@ SHAPES = [  # (files, file bytes, block length, arenas)
     (1, 32 << 30, 131072, 1),     # cfg5's per-GPU share: one 32 GiB file
     (512, 2 << 20, 2048, 2),      # 2 MiB files (B = 2048)
 ]
-VARIANTS = {1: "staged", 4: "staged_seg128", 5: "staged_seg512", 7: "segpark", 2: "park", 3: "long_deep_prefetch"}
+VARIANTS = {1: "staged", 4: "staged_seg128", 5: "staged_seg512", 2: "park", 3: "long_deep_prefetch"}
 DIAGS = {1: "diag_staged_memory_only", 2: "diag_staged_hash_only", 6: "diag_linear_read_ldsdma"}
 
 
