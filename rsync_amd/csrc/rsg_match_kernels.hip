@@ -904,6 +904,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
 #pragma unroll
         for (int g0 = 0; g0 < H; g0 += G) {
             u16x2 p1[G], p2[G], wd[G];
+            uint32_t alo[G], ahi[G];  // D16: the filter words' byte addresses
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
                 const int j = g0 + jj;
@@ -912,18 +913,15 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 const u16x2 X = P1 ^ P2;  // the word index of both windows
                 if constexpr (D16) {
                     // byte addresses 2 X.x, 2 X.y: one SDWA shift each, plus the
-                    // filter's LDS base (0 in practice: the add folds away)
+                    // filter's LDS base (0 in practice: the add folds away);
+                    // the loads are issued below, after the group's last pair
                     const uint32_t fb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint16_t *)filt;
                     const uint32_t xa = as_u32(X);
-                    uint32_t alo, ahi, w;
                     asm("v_lshlrev_b32_sdwa %0, %3, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
                         "v_lshlrev_b32_sdwa %1, %3, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
-                        : "=&v"(alo), "=&v"(ahi) : "v"(xa), "v"(one16));
-                    alo += fb;
-                    ahi += fb;
-                    asm volatile("ds_read_u16_d16 %0, %1\n\tds_read_u16_d16_hi %0, %2"
-                                 : "=&v"(w) : "v"(alo), "v"(ahi) : "memory");
-                    wd[jj] = as_u16x2(w);
+                        : "=&v"(alo[jj]), "=&v"(ahi[jj]) : "v"(xa), "v"(one16));
+                    alo[jj] += fb;
+                    ahi[jj] += fb;
                 } else {
                     wd[jj] = u16x2{filt[X.x], filt[X.y]};
                 }
@@ -933,11 +931,21 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 P2 = P2 + uo * negB + P1;
             }
             if constexpr (D16) {
-                // the asm loads above: the wait carries the words as operands so
-                // no use of them is scheduled before it
+                // the group's 8 filter words in one asm: loads into the halves
+                // of 4 VGPRs, then the wait (in the same statement, so no copy
+                // of a destination can be scheduled before the data lands)
                 static_assert(G == 4, "four words");
-                uint32_t w0 = as_u32(wd[0]), w1 = as_u32(wd[1]), w2 = as_u32(wd[2]), w3 = as_u32(wd[3]);
-                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3) : : "memory");
+                uint32_t w0, w1, w2, w3;
+                asm volatile(
+                    "ds_read_u16_d16 %0, %4\n\tds_read_u16_d16_hi %0, %5\n\t"
+                    "ds_read_u16_d16 %1, %6\n\tds_read_u16_d16_hi %1, %7\n\t"
+                    "ds_read_u16_d16 %2, %8\n\tds_read_u16_d16_hi %2, %9\n\t"
+                    "ds_read_u16_d16 %3, %10\n\tds_read_u16_d16_hi %3, %11\n\t"
+                    "s_waitcnt lgkmcnt(0)"
+                    : "=&v"(w0), "=&v"(w1), "=&v"(w2), "=&v"(w3)
+                    : "v"(alo[0]), "v"(ahi[0]), "v"(alo[1]), "v"(ahi[1]), "v"(alo[2]), "v"(ahi[2]), "v"(alo[3]),
+                      "v"(ahi[3])
+                    : "memory");
                 wd[0] = as_u16x2(w0); wd[1] = as_u16x2(w1); wd[2] = as_u16x2(w2); wd[3] = as_u16x2(w3);
             }
 #pragma unroll
