@@ -654,8 +654,10 @@ __device__ __forceinline__ u16x2 pair_bytes(uint32_t wa, uint32_t wb, int p) {
 // NBITS: filter bits per sum, S2[0..3], S2[4..7] (and S2[8..11]); EDGE: the
 // kernel rolls the range's edge tiles itself (else the host leaves them to
 // roll_kernel and passes t_int = tile_hi).
-// D16 (A/B, RSG_ROLL_D16=1): a pair's two filter words land in the two halves
-// of one VGPR (ds_read_u16_d16 / _d16_hi) instead of two loads and a v_perm.
+// D16 (A/B, RSG_ROLL_D16=1): the filter words' LDS addresses by two SDWA
+// shifts of P1 ^ P2 (the compiler's form takes three VALU for the pair).
+// (d16 loads into the two halves of one VGPR would save the v_perm too, but
+// with SRAM ECC on gfx950 a d16 load zeroes the other half.)
 template <int NBITS, bool EDGE, bool D16 = false>
 __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
@@ -913,15 +915,14 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 const u16x2 X = P1 ^ P2;  // the word index of both windows
                 if constexpr (D16) {
                     // byte addresses 2 X.x, 2 X.y: one SDWA shift each, plus the
-                    // filter's LDS base (0 in practice: the add folds away);
-                    // the loads are issued below, after the group's last pair
+                    // filter's LDS base (0 in practice: the add folds away)
                     const uint32_t fb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint16_t *)filt;
                     const uint32_t xa = as_u32(X);
                     asm("v_lshlrev_b32_sdwa %0, %3, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
                         "v_lshlrev_b32_sdwa %1, %3, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
                         : "=&v"(alo[jj]), "=&v"(ahi[jj]) : "v"(xa), "v"(one16));
-                    alo[jj] += fb;
-                    ahi[jj] += fb;
+                    typedef __attribute__((address_space(3))) const uint16_t lds16;
+                    wd[jj] = u16x2{*(lds16 *)(uintptr_t)(alo[jj] + fb), *(lds16 *)(uintptr_t)(ahi[jj] + fb)};
                 } else {
                     wd[jj] = u16x2{filt[X.x], filt[X.y]};
                 }
@@ -929,24 +930,6 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 const u16x2 ui = pair_bytes(Sx[j >> 2], Sx[(j >> 2) + OW / 2], j & 3);
                 P1 = P1 + ui - uo;
                 P2 = P2 + uo * negB + P1;
-            }
-            if constexpr (D16) {
-                // the group's 8 filter words in one asm: loads into the halves
-                // of 4 VGPRs, then the wait (in the same statement, so no copy
-                // of a destination can be scheduled before the data lands)
-                static_assert(G == 4, "four words");
-                uint32_t w0, w1, w2, w3;
-                asm volatile(
-                    "ds_read_u16_d16 %0, %4\n\tds_read_u16_d16_hi %0, %5\n\t"
-                    "ds_read_u16_d16 %1, %6\n\tds_read_u16_d16_hi %1, %7\n\t"
-                    "ds_read_u16_d16 %2, %8\n\tds_read_u16_d16_hi %2, %9\n\t"
-                    "ds_read_u16_d16 %3, %10\n\tds_read_u16_d16_hi %3, %11\n\t"
-                    "s_waitcnt lgkmcnt(0)"
-                    : "=&v"(w0), "=&v"(w1), "=&v"(w2), "=&v"(w3)
-                    : "v"(alo[0]), "v"(ahi[0]), "v"(alo[1]), "v"(ahi[1]), "v"(alo[2]), "v"(ahi[2]), "v"(alo[3]),
-                      "v"(ahi[3])
-                    : "memory");
-                wd[0] = as_u16x2(w0); wd[1] = as_u16x2(w1); wd[2] = as_u16x2(w2); wd[3] = as_u16x2(w3);
             }
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
