@@ -654,11 +654,7 @@ __device__ __forceinline__ u16x2 pair_bytes(uint32_t wa, uint32_t wb, int p) {
 // NBITS: filter bits per sum, S2[0..3], S2[4..7] (and S2[8..11]); EDGE: the
 // kernel rolls the range's edge tiles itself (else the host leaves them to
 // roll_kernel and passes t_int = tile_hi).
-// D16 (A/B, RSG_ROLL_D16=1): the filter words' LDS addresses by two SDWA
-// shifts of P1 ^ P2 (the compiler's form takes three VALU for the pair).
-// (d16 loads into the two halves of one VGPR would save the v_perm too, but
-// with SRAM ECC on gfx950 a d16 load zeroes the other half.)
-template <int NBITS, bool EDGE, bool D16 = false>
+template <int NBITS, bool EDGE>
 __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
     uint32_t t_int, uint32_t tile_hi, const uint16_t *__restrict__ filter_g, const uint32_t *__restrict__ keys,
@@ -901,30 +897,32 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
             Sx[k] = S[k] ^ 0x80808080u;
         }
         constexpr int G = 4;  // pair steps per group: 8 filter reads in flight
-        uint32_t one16 = 1;  // D16: the SDWA shift count (a VGPR operand)
+        uint32_t one16 = 1;  // the SDWA shift count of the filter addresses (a VGPR operand)
         asm("" : "+v"(one16));
 #pragma unroll
         for (int g0 = 0; g0 < H; g0 += G) {
             u16x2 p1[G], p2[G], wd[G];
-            uint32_t alo[G], ahi[G];  // D16: the filter words' byte addresses
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
                 const int j = g0 + jj;
                 p1[jj] = P1;
                 p2[jj] = P2;
                 const u16x2 X = P1 ^ P2;  // the word index of both windows
-                if constexpr (D16) {
-                    // byte addresses 2 X.x, 2 X.y: one SDWA shift each, plus the
-                    // filter's LDS base (0 in practice: the add folds away)
+                {
+                    // the filter words' LDS byte addresses 2 X.x, 2 X.y: one SDWA
+                    // shift each (the compiler's form takes three VALU for the
+                    // pair), plus the filter's LDS base (0: the add folds away).
+                    // (d16 loads into the two halves of one VGPR would save the
+                    // v_perm too, but with SRAM ECC on gfx950 a d16 load zeroes
+                    // the other half: measured, the parity tests failed.)
                     const uint32_t fb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint16_t *)filt;
                     const uint32_t xa = as_u32(X);
+                    uint32_t alo, ahi;
                     asm("v_lshlrev_b32_sdwa %0, %3, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
                         "v_lshlrev_b32_sdwa %1, %3, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
-                        : "=&v"(alo[jj]), "=&v"(ahi[jj]) : "v"(xa), "v"(one16));
+                        : "=&v"(alo), "=&v"(ahi) : "v"(xa), "v"(one16));
                     typedef __attribute__((address_space(3))) const uint16_t lds16;
-                    wd[jj] = u16x2{*(lds16 *)(uintptr_t)(alo[jj] + fb), *(lds16 *)(uintptr_t)(ahi[jj] + fb)};
-                } else {
-                    wd[jj] = u16x2{filt[X.x], filt[X.y]};
+                    wd[jj] = u16x2{*(lds16 *)(uintptr_t)(alo + fb), *(lds16 *)(uintptr_t)(ahi + fb)};
                 }
                 const u16x2 uo = pair_bytes(Ox[j >> 2], Ox[(j >> 2) + OW / 2], j & 3);
                 const u16x2 ui = pair_bytes(Sx[j >> 2], Sx[(j >> 2) + OW / 2], j & 3);
@@ -1061,14 +1059,6 @@ static bool roll_edge_inside() {
     return v;
 }
 
-static bool roll_d16() {  // A/B switch (roll_packed_kernel D16)
-    static const bool v = [] {
-        const char *e = getenv("RSG_ROLL_D16");
-        return e && e[0] == '1';
-    }();
-    return v;
-}
-
 int roll_filter_bits() {
     static const int v = [] {
         // A/B switch: 2 = bits S2[0..3], S2[4..7] only; default 3 adds S2[8..11]
@@ -1109,7 +1099,6 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                 // the whole range: the packed kernel rolls its edge tiles itself
                 const uint32_t ga = min(grid, tile_hi - tile_lo);
                 auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, true> : roll_packed_kernel<2, true>;
-                if (roll_d16()) kern = roll_packed_kernel<3, true, true>;
                 hipLaunchKernelGGL(kern, dim3(ga), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
                                    t_int, tile_hi, filter16, table_keys, bmask, cand, cap, count);
                 return hipGetLastError();
