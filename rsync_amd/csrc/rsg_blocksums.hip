@@ -924,7 +924,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
 // per-lane prefetch, 4 / 5 = staged with 128- / 512-byte segments, 6 = staged
 // for blocks at any byte offset (funnel-shifted pieces).
 // Automatic (launch_block_sums below): aligned batches take park when
-// 512 <= max block <= 703, 4 when the max block is 704..1536, else 1;
+// 512 <= max block <= 703, 4 when the max block is 704..4096, else 1;
 // unaligned batches take 6 (3 for blocks >= 8 KiB, else 0, when the arena
 // itself is not 4-byte aligned).
 //
@@ -1001,14 +1001,15 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         return hipGetLastError();
     }
     int v = variant;
-    // Aligned: park for 512..703-byte blocks, 128-byte segments up to 1536
+    // Aligned: park for 512..703-byte blocks, 128-byte segments up to 4096
     // (B = 1024: 0.197-0.204 ms against 0.207-0.224 for 256-byte segments in
-    // three sweeps), 256-byte segments beyond (equal at 4 KiB, 12 % better at
-    // 128 KiB).  Unaligned: the staged kernel wins at every block length
-    // measured.
+    // three sweeps; B = 2048 0.186 against 0.197, B = 4096 equal,
+    // profiles/r04x_blocklen_sweep.jsonl), 256-byte segments beyond (12 %
+    // better at 128 KiB).  Unaligned: the staged kernel wins at every block
+    // length measured.
     if (v == -1)
         v = aligned ? ((max_blen <= kRegMaxBytes && max_blen >= kParkMinBytes) ? 2
-                                                                               : (max_blen > kRegMaxBytes && max_blen <= 1536 ? 4 : 1))
+                                                                               : (max_blen > kRegMaxBytes && max_blen <= 4096 ? 4 : 1))
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena

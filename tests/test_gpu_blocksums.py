@@ -257,7 +257,7 @@ def test_variants_device_aligned_arena(eng, variant):
     waves and tiles, a file ending exactly at the arena end (park's direct
     tiles), blocks of 700/64/703 bytes (64: park with tiny blocks, ragged
     tails hashed by the predicated path) and the automatic choice's
-    boundaries (-1: 703 park, 704..1536 128-byte segments, 1537 and up
+    boundaries (-1: 703 park, 704..4096 128-byte segments, 4097 and up
     256-byte segments)."""
     from rsync_amd import _lib
     lens = [1 << 20, 700 * 64 * 3 + 5, 12344, 64, 4, 0, 300_000, 70_000 * 3]
@@ -274,7 +274,7 @@ def test_variants_device_aligned_arena(eng, variant):
         datas.append(d)
     arena = eng.alloc(arena_bytes)
     arena.upload(host)
-    for blen in (700, 64, 703, 704, 1024, 1536, 1537, 4096):
+    for blen in (700, 64, 703, 704, 1024, 1536, 1537, 4096, 4097):
         want = b"".join(orc.block_sums(d, blen, cases.SEED) for d in datas)
         try:
             eng.set_block_sums_kernel(variant)
