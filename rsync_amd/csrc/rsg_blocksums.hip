@@ -549,7 +549,6 @@ struct PkShared {
     uint32_t full[kPkSlots];
     uint32_t freeq[kPkSlots];
     uint32_t kind[kPkSlots];   // 1 = staged in the slot, 0 = direct
-    uint32_t arrived[kPkSlots];  // SPLIT: loaders whose part of the slot's tile has landed
     uint32_t ticket;
 };
 
@@ -767,46 +766,6 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
     store_record(out, g, nn, s1, tw, h);
 }
 
-// SPLIT loaders: instructions [i0, i0 + NI) of a tile's 45 (loader L issues
-// i0 = 15 L), jj/uu as pk_issue's for those instructions.
-template <int AUX, uint32_t NI>
-__device__ __forceinline__ void pk_issue_part(const uint8_t *arena, uint8_t *dst, const PkDesc &d, uint32_t lane,
-                                              uint32_t i0, const uint32_t *jj, const uint32_t *uu) {
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(arena + d.base), (short)0, 0x7FFFFFFF, 0x00020000);
-    if (d.regular) {
-#pragma unroll
-        for (uint32_t i = 0; i < NI; i++) {
-            const uint32_t nj = jj[i] == d.jl ? d.nl : d.B;
-            const uint32_t vo = uu[i] < nj ? d.B * jj[i] + uu[i] : 0x80000000u;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * (i0 + i)),
-                                                     16, vo, 0, 0, AUX);
-        }
-    } else {
-        const int rel = (int)(uint32_t)(d.off - d.base);
-        constexpr uint32_t kB = 5;
-        static_assert(NI % kB == 0, "whole batches");
-#pragma unroll
-        for (uint32_t b0 = 0; b0 < NI; b0 += kB) {
-            uint32_t rj[kB], nj[kB];
-#pragma unroll
-            for (uint32_t k = 0; k < kB; k++) {
-                rj[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * jj[b0 + k]), rel);
-                nj[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * jj[b0 + k]), (int)d.n);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (uint32_t k = 0; k < kB; k++) {
-                const uint32_t u16 = uu[b0 + k];
-                const uint32_t vo = u16 < nj[k] ? rj[k] + u16 : 0x80000000u;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rsrc, (__attribute__((address_space(3))) void *)(dst + 1024u * (i0 + b0 + k)), 16, vo, 0, 0, AUX);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-}
-
 // MODE 0 = product; diagnostics: 1 = memory only (DMA + copy, no hashing),
 // 2 = hashing only (no DMA: the hashers hash whatever the slots hold),
 // 3 = memory only with every quad request 16-byte aligned (ALN above).
@@ -821,11 +780,7 @@ __device__ __forceinline__ void pk_issue_part(const uint8_t *arena, uint8_t *dst
 // none 0.1984 ms, loaders only 0.1962, copy-out at 2 0.1950, at 3 0.1942;
 // raising the hasher already while it waits for its slot: no gain,
 // profiles/r04g_ab_park_prio_ticket.json.)
-// SPLIT (A/B): the three loaders share every tile, loader L issuing its
-// instructions [15 L, 15 L + 15) (a tile's issue takes a third of the time),
-// each with up to three tiles' parts in flight; the third loader to see its
-// part land publishes the tile.
-template <int MODE, int NL, int AUX, int PRIO = 0, bool SPLIT = false>
+template <int MODE, int NL, int AUX, int PRIO = 0>
 __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
@@ -836,69 +791,11 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     if (threadIdx.x < kPkSlots) {
         sh.full[threadIdx.x] = ~0u;
         sh.freeq[threadIdx.x] = threadIdx.x;
-        sh.arrived[threadIdx.x] = 0;
     }
     if (threadIdx.x == 0) sh.ticket = 0;
     __syncthreads();
     const uint64_t ntiles = (total_blocks + 63) / 64;
     const uint32_t G = gridDim.x;  // one persistent workgroup per CU; tile t belongs to workgroup t % G
-
-    if (SPLIT && wave < NL) {
-        static_assert(!SPLIT || (NL == 3 && kPkDma == 45), "three loaders, 15 instructions each");
-        if (PRIO >= 3) __builtin_amdgcn_s_setprio(3);
-        constexpr uint32_t NI = kPkDma / 3;
-        const uint32_t i0 = NI * wave;
-        uint32_t jj[NI], uu[NI];
-#pragma unroll
-        for (uint32_t i = 0; i < NI; i++) {
-            const uint32_t idx = 64u * (i0 + i) + lane;
-            jj[i] = idx / 45u;
-            const uint32_t u = idx - 45u * jj[i];
-            uu[i] = u < 44u ? 16u * u : 0x40000000u;
-        }
-        const uint32_t nt = ntiles > blockIdx.x ? (uint32_t)((ntiles - blockIdx.x + G - 1) / G) : 0u;
-        uint32_t ki = 0, kd = 0;  // next tile to issue, oldest tile not yet landed
-        uint32_t stg = 0;         // bit k % 3: tile k's part issued DMAs
-        PkDesc cur;
-        if (nt) pk_locate(blockIdx.x, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
-#pragma unroll 1
-        for (;;) {
-            // issue while fewer than three tiles are in flight; the slot's
-            // previous tile (ki - 3) has landed for this loader already
-            while (ki < nt && ki - kd < kPkSlots) {
-                const uint32_t slot = ki % kPkSlots;
-                while (pk_load(&sh.freeq[slot]) != ki) __builtin_amdgcn_s_sleep(1);
-                if (wave == 0) {
-                    sh.n[slot][lane] = cur.n;
-                    if (lane == 0) sh.kind[slot] = cur.staged ? 1u : 0u;
-                }
-                const bool st = cur.staged && MODE != 2;
-                if (st) pk_issue_part<AUX, NI>(arena, &sh.tile[slot][0], cur, lane, i0, jj, uu);
-                stg = (stg & ~(1u << slot)) | (st ? 1u << slot : 0u);
-                ki++;
-                if (ki < nt)
-                    pk_locate(blockIdx.x + (uint64_t)ki * G, cur, lane, files, wg_file, nwg256, total_blocks,
-                              arena_bytes);
-            }
-            if (kd == ki) break;
-            // tile kd's part landed: the younger tiles' DMAs may stay in flight
-            uint32_t young = 0;
-            for (uint32_t y = kd + 1; y < ki; y++) young += (stg >> (y % kPkSlots)) & 1u;
-            if (young == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else if (young == 1) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
-            const uint32_t slot = kd % kPkSlots;
-            uint32_t prev = 0;
-            if (lane == 0) prev = __hip_atomic_fetch_add(&sh.arrived[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-            prev = __builtin_amdgcn_readfirstlane(prev);
-            if (prev == NL - 1 && lane == 0) {  // the last part: publish
-                __hip_atomic_store(&sh.arrived[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                pk_store(&sh.full[slot], kd);
-            }
-            kd++;
-        }
-        return;
-    }
 
     if (wave < NL) {
         if (PRIO >= 3) __builtin_amdgcn_s_setprio(3);
@@ -1100,11 +997,6 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     hipLaunchKernelGGL((block_sums_park<3, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                        files, wg_file, nwg, total_blocks, seed, out);
                 break;
-            case 9:
-                if (max_blen <= kRegMaxBytes)
-                    hipLaunchKernelGGL((block_sums_park<1, kParkLoaders, 2, 3, true>), pgrid, pblock, 0, stream, arena,
-                                       arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
-                break;
         }
         return hipGetLastError();
     }
@@ -1121,9 +1013,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v == 7)) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
-    if ((v == 2 || v == 7) && max_blen > kRegMaxBytes) v = 1;
+    if (v == 2 && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
             hipLaunchKernelGGL((block_sums_staged<0>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
@@ -1132,10 +1024,6 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                files, wg_file, nwg, total_blocks, seed, out);
-            break;
-        case 7:  // A/B: park with split loaders
-            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3, true>), pgrid, pblock, 0, stream, arena,
-                               arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
             break;
         case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel
             if (aligned)
