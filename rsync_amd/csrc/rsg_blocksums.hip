@@ -767,7 +767,6 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
 }
 
 // MODE 0 = product; diagnostics: 1 = memory only (DMA + copy, no hashing),
-// 4 = hashing only without the full chunks' weak sums (their cost),
 // 2 = hashing only (no DMA: the hashers hash whatever the slots hold),
 // 3 = memory only with every quad request 16-byte aligned (ALN above).
 // The tile DMA uses the nt cache policy (aux = 2): every byte is read once.
@@ -834,7 +833,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             sh.n[slot][lane] = cur.n;
             if (lane == 0) sh.kind[slot] = cur.staged ? 1u : 0u;
             const bool staged = cur.staged;
-            if (staged && MODE != 2 && MODE != 4) pk_issue<AUX, true, MODE == 3>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
+            if (staged && MODE != 2) pk_issue<AUX, true, MODE == 3>(arena, &sh.tile[slot][0], cur, lane, jj, uu);
             uint32_t kn = k + 1;
             while (!owned(kn)) kn++;
             const uint64_t tn = blockIdx.x + (uint64_t)kn * G;
@@ -902,12 +901,8 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             } else {
 #pragma unroll
                 for (uint32_t c = 0; c < kRegChunks; c++) {
-                    if (c < nfull) {
-                        if (MODE == 4) md4_compress(h, R + 16 * c);  // timing: no weak sums
-                        else hash_chunk<true>(R + 16 * c, 0u, 0u, c, h, s1, tw);
-                    } else if (c == nfull) {
-                        hash_tail<true>(R + 16 * c, 0u, 0u, n, seed, h, s1, tw);
-                    }
+                    if (c < nfull) hash_chunk<true>(R + 16 * c, 0u, 0u, c, h, s1, tw);
+                    else if (c == nfull) hash_tail<true>(R + 16 * c, 0u, 0u, n, seed, h, s1, tw);
                 }
             }
             store_record(out, g, n, s1, tw, h);
@@ -939,8 +934,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
 // 1 = staged memory only, 2 = staged hashing only, 3 = park memory only,
 // 4 = park hashing only, 5 = linear read with plain loads, 6 = linear read
 // with LDS DMA, 7 = the same with every request 4 bytes off a 16-byte
-// boundary, 8 = park memory only with 16-byte aligned quad requests, 9 = park hashing
-// only without the full chunks' weak sums.
+// boundary, 8 = park memory only with 16-byte aligned quad requests.
 constexpr int kParkLoaders = 3;  // 1 / 2 / 3 loaders measured
 int block_sums_variant_env() {
     static const int v = [] {
@@ -1001,11 +995,6 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             case 8:
                 if (max_blen <= kRegMaxBytes)
                     hipLaunchKernelGGL((block_sums_park<3, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
-                                       files, wg_file, nwg, total_blocks, seed, out);
-                break;
-            case 9:
-                if (max_blen <= kRegMaxBytes)
-                    hipLaunchKernelGGL((block_sums_park<4, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                        files, wg_file, nwg, total_blocks, seed, out);
                 break;
         }
