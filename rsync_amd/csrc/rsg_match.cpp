@@ -519,46 +519,46 @@ rsg_status tables_roll(Search &S, const uint32_t *sum1, const int32_t *targets) 
             if (packed) filter16[rsg::f16_word(key, (uint32_t)B)] |= (uint16_t)rsg::f16_mask(key, nbits);
         }
     });
-    // distinct Sum1 -> flags, inserted into the bucket table directly (an
-    // existing key ORs its flags: match.go:108's candidates are every block
-    // with that Sum1)
+    // Sum1 -> flags into the 2-choice bucket table, straight from the sums.
+    // First without looking for an equal key (a repeated Sum1 then sits in
+    // the table twice: the probes OR the flags of every equal entry, and the
+    // packed roll's key test only asks for presence); only if a bucket pair
+    // fills up -- many equal sums, e.g. periodic data -- again with equal
+    // keys merged (match.go:108's candidates are every block with that Sum1).
     uint32_t nb = 16;
     while (nb < (uint32_t)count / 2) nb <<= 1;
     auto &table = T.table;
     auto &fill = T.fill;
     constexpr uint32_t W = rsg::kBucketWays;
-    uint32_t first_key = 0;
-    for (;;) {
+    const uint32_t first_key = count ? sum1[0] : 0u;
+    auto build = [&](bool merge) -> bool {
         table.assign((size_t)nb * W, 0);
         fill.assign(nb, 0);
-        bool ok = true;
-        for (int32_t k = 0; k < count && ok; k++) {
+        for (int32_t k = 0; k < count; k++) {
             const uint32_t v = sum1[k];
             const uint32_t f = 1u | ((S.len_of(k) == B) ? 2u : 4u);
-            if (k == 0) first_key = v;
             const uint32_t h1 = rsg::bucket_hash1(v) & (nb - 1), h2 = rsg::bucket_hash2(v) & (nb - 1);
-            bool found = false;
-            for (uint32_t hh : {h1, h2}) {
-                for (uint32_t w = 0; w < fill[hh] && !found; w++) {
-                    uint64_t &e = table[(size_t)hh * W + w];
-                    if ((uint32_t)(e >> 32) == v) {
-                        e |= f;
-                        found = true;
+            if (merge) {
+                bool found = false;
+                for (uint32_t hh : {h1, h2}) {
+                    for (uint32_t w = 0; w < fill[hh] && !found; w++) {
+                        uint64_t &e = table[(size_t)hh * W + w];
+                        if ((uint32_t)(e >> 32) == v) {
+                            e |= f;
+                            found = true;
+                        }
                     }
+                    if (found || h2 == h1) break;
                 }
-                if (found || h2 == h1) break;
+                if (found) continue;
             }
-            if (found) continue;
             const uint32_t h = fill[h2] < fill[h1] ? h2 : h1;
-            if (fill[h] == W) {
-                ok = false;
-                break;
-            }
+            if (fill[h] == W) return false;
             table[(size_t)h * W + fill[h]++] = ((uint64_t)v << 32) | f;
         }
-        if (ok) break;
-        nb <<= 1;
-    }
+        return true;
+    };
+    while (!build(false) && !build(true)) nb <<= 1;
     S.bmask = nb - 1;
     auto &tkeys = T.table_keys;  // the packed roll's key-only copy
     tkeys.resize(table.size());
