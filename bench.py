@@ -176,7 +176,7 @@ def main():
     if args.ab:
         from rsync_amd import _lib
         # (product variant, diagnostic) pairs; diagnostics write meaningless records
-        names = {(2, 0): "park", (7, 0): "park_sleep0", (1, 3): "diag_park_memory_only", (1, 4): "diag_park_hash_only",
+        names = {(2, 0): "park", (1, 3): "diag_park_memory_only", (1, 4): "diag_park_hash_only",
                  (1, 6): "diag_linear_read_ldsdma", (1, 5): "diag_linear_read_plain",
                  (1, 7): "diag_linear_read_ldsdma_misaligned4", (1, 8): "diag_park_memory_only_aligned"}
         res = {v: [] for v in names}

@@ -780,8 +780,7 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
 // none 0.1984 ms, loaders only 0.1962, copy-out at 2 0.1950, at 3 0.1942;
 // raising the hasher already while it waits for its slot: no gain,
 // profiles/r04g_ab_park_prio_ticket.json.)
-// SLEEP (A/B): s_sleep argument of the slot polls (units of 64 cycles).
-template <int MODE, int NL, int AUX, int PRIO = 0, int SLEEP = 1>
+template <int MODE, int NL, int AUX, int PRIO = 0>
 __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
@@ -830,7 +829,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
         while (t < ntiles) {
             const uint32_t slot = k % kPkSlots;
             // the slot's previous tile must have been copied out by its hasher
-            while (pk_load(&sh.freeq[slot]) != k) __builtin_amdgcn_s_sleep(SLEEP);
+            while (pk_load(&sh.freeq[slot]) != k) __builtin_amdgcn_s_sleep(1);
             sh.n[slot][lane] = cur.n;
             if (lane == 0) sh.kind[slot] = cur.staged ? 1u : 0u;
             const bool staged = cur.staged;
@@ -875,7 +874,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
         const uint64_t t = blockIdx.x + (uint64_t)k * G;
         if (t >= ntiles) break;
         const uint32_t slot = k % kPkSlots;
-        while (pk_load(&sh.full[slot]) != k) __builtin_amdgcn_s_sleep(SLEEP);
+        while (pk_load(&sh.full[slot]) != k) __builtin_amdgcn_s_sleep(1);
         if (PRIO >= 3) __builtin_amdgcn_s_setprio(3);
         const uint32_t n = sh.n[slot][lane];
         const uint32_t kind = __builtin_amdgcn_readfirstlane(sh.kind[slot]);
@@ -1014,9 +1013,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v == 7)) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
-    if ((v == 2 || v == 7) && max_blen > kRegMaxBytes) v = 1;
+    if (v == 2 && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
             hipLaunchKernelGGL((block_sums_staged<0>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
@@ -1025,10 +1024,6 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                files, wg_file, nwg, total_blocks, seed, out);
-            break;
-        case 7:  // A/B: park polling with s_sleep 0
-            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3, 0>), pgrid, pblock, 0, stream, arena,
-                               arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
             break;
         case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel
             if (aligned)
