@@ -1014,7 +1014,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
     if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
-    if ((v == 6 || v == 7) && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
+    if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
     if (v == 2 && max_blen > kRegMaxBytes) v = 1;
     switch (v) {
         case 1:
@@ -1024,14 +1024,6 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                files, wg_file, nwg, total_blocks, seed, out);
-            break;
-        case 7:  // A/B: as 6 with 128-byte segments (the sender's confirmation: 3 workgroups per CU)
-            if (aligned)
-                hipLaunchKernelGGL((block_sums_staged<10>), grid, block, lds_reserve, stream, arena, arena_bytes, files,
-                                   wg_file, total_blocks, seed, out);
-            else
-                hipLaunchKernelGGL((block_sums_staged<110>), grid, block, lds_reserve, stream, arena, arena_bytes,
-                                   files, wg_file, total_blocks, seed, out);
             break;
         case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel
             if (aligned)

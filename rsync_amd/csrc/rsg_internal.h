@@ -36,7 +36,7 @@ inline uint64_t block_sums_scratch_bytes(uint64_t total_blocks) { return 8 + 4 *
 // with 128/512-byte segments, 6 staged at any byte offset) and timing
 // diagnostics (0 off, 1..kBlockSumsDiagMax; outputs meaningless),
 // rsg_blocksums.hip; both per context (rsg_ctx::bs_variant / bs_diag).
-constexpr int kBlockSumsVariantMax = 7;  // 7: unaligned staged, 128-byte segments (A/B)
+constexpr int kBlockSumsVariantMax = 6;
 constexpr int kBlockSumsDiagMax = 8;
 // RSG_BLOCKSUMS_KERNEL (read once): a context's initial variant.
 int block_sums_variant_env();

@@ -25,8 +25,6 @@ for S in "$@"; do
     receive) timeout -k 10 300 python bench.py --workload receive > gpurun_out/${TAG}_receive.json 2> gpurun_out/${TAG}_receive.err || exit 1 ;;
     prof_cfg2) bash tools/profile_kernel.sh ${TAG}_cfg2 block_sums --steps 20 --warmup 5 --no-cpu --no-host-path --no-delivery || exit 1 ;;
     prof_cfg3) PASSES="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE;SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE;FETCH_SIZE" bash tools/profile_kernel.sh ${TAG}_cfg3 roll --workload cfg3 --steps 2 --warmup 1 --cfg3-files 4 --no-cpu --no-host-path || exit 1 ;;
-    confab) RSG_BLOCKSUMS_KERNEL=7 timeout -k 10 400 python -u -m pytest tests/test_gpu_match.py tests/test_gpu_sender_fd.py -m gpu -x -q $T > gpurun_out/${TAG}_confab_tests.log 2>&1 || { tail -30 gpurun_out/${TAG}_confab_tests.log; exit 1; }
-      for M in -1 7 -1 7 -1 7; do RSG_BLOCKSUMS_KERNEL=$M timeout -k 10 200 python bench.py --workload cfg3 --steps 5 --no-cpu --no-host-path > gpurun_out/${TAG}_c.json 2>> gpurun_out/${TAG}_confab.err && { echo "kernel=$M"; cat gpurun_out/${TAG}_c.json; } >> gpurun_out/${TAG}_confab.txt || exit 1; done ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
 done
