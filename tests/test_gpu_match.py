@@ -85,6 +85,19 @@ def test_periodic_dense(eng):
     assert eng.hash_search(src, head, s1, s2, tg, 7) == want
 
 
+@pytest.mark.gpu
+def test_periodic_candidate_overflow(eng):
+    """More candidates than one roll launch may append (kCandCap = 2^22): a
+    6 MiB periodic source halves its scan range and rolls again, reading
+    each range's candidates from the pinned host list the roll writes."""
+    src = np.full(6 << 20, 0xBB, np.uint8)
+    basis = np.full(1 << 20, 0xBB, np.uint8)
+    head, s1, s2 = basis_sums(basis, 0, 11)
+    tg = orc.stable_targets(s1)
+    want, _, _ = orc.hash_search(src, head, s1, s2, tg, 11)
+    assert eng.hash_search(src, head, s1, s2, tg, 11) == want
+
+
 def test_cfg3_shape_vs_oracle(eng):
     """cfg3 recipe at 64 MiB: a ~50%-modified basis with
     long runs plus shifts, reference block sizing (B = sqrt(len))."""
