@@ -1,8 +1,9 @@
 #!/bin/bash
 # One gpurun call's worth of GPU work, each step under its own time limit,
 # chained so that the first failure (or a hang) ends the call.
-#   tools/gpu_run.sh <tag> <step>...   steps: tests | newtests | smoke | ab | bench | cfg3 | cfg4 | cfg5 |
-#                                             filesums | receive | prof_cfg2 | prof_cfg3
+#   tools/gpu_run.sh <tag> <step>...   steps: tests | newtests | smoke | sweep | variants | ab8 | ab |
+#                                             bench | cfg3 | cfg4 | cfg5 | filesums | receive |
+#                                             prof_cfg2 | prof_cfg3
 set -o pipefail
 TAG=$1; shift
 mkdir -p gpurun_out
