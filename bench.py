@@ -683,6 +683,9 @@ def sender_host_path(eng, src, meta, dev_res):
     return out
 
 
+ROLL_ISSUE_NS = 1.91  # measured, see roll_valu_issue
+
+
 def roll_valu_issue(roll_ms, world):
     """The roll's VALU-issue bound (it is VALU-issue-bound, not HBM-bound,
     DESIGN.md §4.2): SQ_INSTS_VALU per launch from the committed PMC pass of
@@ -696,8 +699,19 @@ def roll_valu_issue(roll_ms, world):
         return None
     simds = 4 * int(c["roll_cus"])
     floor_ms = float(c["valu_wave_insts_per_launch"]) * 2 / simds / (float(c["clock_ghz"]) * 1e9) * 1e3
+    # The same count at the issue interval measured for the roll's own
+    # instructions (tools/valu_issue.hip, profiles/r04za_valu_issue.txt: 8
+    # waves per SIMD, 16 independent chains each): v_perm / v_pk_* / SDWA /
+    # v_add3 / v_dot4 alone 1.97 ns per wave-instruction per SIMD, v_xor /
+    # v_and / v_add alone 1.17 ns, an alternating mix of the two kinds 1.91 ns
+    # (the cheap kind gains nothing beside the other).  1.91 ns is the floor of
+    # this mix, whatever the clock did.
+    floor_meas_ms = float(c["valu_wave_insts_per_launch"]) * ROLL_ISSUE_NS * 1e-9 / simds * 1e3
     return {"valu_wave_insts_per_launch": c["valu_wave_insts_per_launch"], "simds": simds,
             "clock_ghz": c["clock_ghz"], "floor_ms": round(floor_ms, 4), "frac": round(floor_ms / roll_ms, 4),
+            "measured_issue_ns": ROLL_ISSUE_NS, "floor_ms_measured_issue": round(floor_meas_ms, 4),
+            "frac_measured_issue": round(floor_meas_ms / roll_ms, 4),
+            "issue_source": "profiles/r04za_valu_issue.txt (tools/valu_issue.hip)",
             "source": c.get("source")}
 
 
