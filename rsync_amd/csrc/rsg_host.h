@@ -53,6 +53,7 @@ struct SearchSlot {
     hipEvent_t scanned = nullptr;      // prefix pass done (side stream)
     hipEvent_t tables_b = nullptr;     // the resolve tables' upload done (side stream)
     hipEvent_t rolled = nullptr;       // roll kernel + count read-back done
+    void *counts_zeroed = nullptr;     // counts.p once zeroed (every roll_count_out leaves it 0)
     hipEvent_t confirmed = nullptr;    // confirmation batch + result read-back done
 };
 constexpr int kSearchSlots = 4;  // jobs i-1 (walk on a worker), i (confirming), i+1 (rolling), i+2 (being issued)

@@ -95,6 +95,10 @@ hipError_t launch_confirm_plan(const uint64_t *cand, uint32_t n, uint64_t size, 
 hipError_t launch_resolve(const uint8_t *records, const DevFile *files, uint64_t n, const uint2 *groups,
                           const uint32_t *hi16, const uint8_t *sum2, int32_t count, int32_t blen, int32_t rem,
                           int32_t s2len, int32_t *res, hipStream_t stream);
+// After a roll, on its stream: the candidate count to the pinned host word
+// `host` and the device counter back to 0 for the next roll (one launch
+// instead of a memset and a 4-byte copy, each with its own dispatch gap).
+hipError_t launch_roll_count_out(uint32_t *count, uint32_t *host, hipStream_t stream);
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
                        const uint32_t *bitmap, const uint16_t *filter16, const uint64_t *table,

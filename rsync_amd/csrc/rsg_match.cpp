@@ -652,6 +652,10 @@ rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
     if ((s = ensure_pin(ctx, sl.list, (uint64_t)kCandCap * 8)) != RSG_OK) return s;
     if ((s = ensure_dev(ctx, sl.counts, 64)) != RSG_OK) return s;
     if ((s = ensure_pin(ctx, sl.count, 64)) != RSG_OK) return s;
+    if (sl.counts_zeroed != sl.counts.p) {  // a new counter: zero once (each roll's count_out re-zeroes it)
+        RSG_HIP(ctx, hipMemsetAsync(sl.counts.p, 0, 4, S.st));
+        sl.counts_zeroed = sl.counts.p;
+    }
     if ((s = ensure_dev(ctx, sl.blob, S.blob_bytes)) != RSG_OK) return s;
     if (host_src || ((uintptr_t)src & 15u)) {  // the scan kernels read 16-byte vectors at 16-byte strides
         if ((s = ensure_dev(ctx, sl.src, S.size + 64)) != RSG_OK) return s;
@@ -691,19 +695,19 @@ rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
     return RSG_OK;
 }
 
-// Roll kernel over tiles [lo, hi) + asynchronous read-back of its candidate
-// count, on the compute stream; event `rolled` marks both done.
+// Roll kernel over tiles [lo, hi) + its candidate count to the pinned host
+// word (and the counter re-zeroed), on the compute stream; event `rolled`
+// marks both done.
 rsg_status launch_range(Search &S, uint32_t lo, uint32_t hi) {
     rsg_ctx *ctx = S.ctx;
     SearchSlot &sl = *S.sl;
-    RSG_HIP(ctx, hipMemsetAsync(sl.counts.p, 0, 4, S.st));
     hipEvent_t t0 = timed_begin(ctx, S.st);
     RSG_HIP(ctx, rsg::launch_roll(S.d_src, S.size, (uint32_t)S.head.block_len, (uint32_t)S.head.rem, (uint64_t)S.end,
                                   lo, hi, (const TileAgg *)sl.agg.p, (const TilePrefix *)sl.prefix.p, S.ntiles,
                                   S.d_filter, S.d_filter16, S.d_table, S.d_table_keys, S.bmask, (uint64_t *)sl.list.p, kCandCap,
                                   (uint32_t *)sl.counts.p, S.cus, S.fused, S.st));
     timed_end(ctx, t0, S.st, 0);
-    RSG_HIP(ctx, hipMemcpyAsync(sl.count.p, sl.counts.p, 4, hipMemcpyDeviceToHost, S.st));
+    RSG_HIP(ctx, rsg::launch_roll_count_out((uint32_t *)sl.counts.p, (uint32_t *)sl.count.p, S.st));
     RSG_HIP(ctx, hipEventRecord(sl.rolled, S.st));
     return RSG_OK;
 }

@@ -1078,6 +1078,18 @@ bool roll_filter_sel() {
     return sel;
 }
 
+__global__ void roll_count_out_kernel(uint32_t *__restrict__ count, uint32_t *__restrict__ host) {
+    if (threadIdx.x == 0) {
+        *host = *count;  // pinned host word, read by the host after the stream's event
+        *count = 0;
+    }
+}
+
+hipError_t launch_roll_count_out(uint32_t *count, uint32_t *host, hipStream_t stream) {
+    hipLaunchKernelGGL(roll_count_out_kernel, dim3(1), dim3(64), 0, stream, count, host);
+    return hipGetLastError();
+}
+
 hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
                        const uint32_t *bitmap, const uint16_t *filter16, const uint64_t *table,
