@@ -653,8 +653,13 @@ __device__ __forceinline__ u16x2 pair_bytes(uint32_t wa, uint32_t wb, int p) {
 
 // NBITS: filter bits per sum, S2[0..3], S2[4..7] (and S2[8..11]); EDGE: the
 // kernel rolls the range's edge tiles itself (else the host leaves them to
-// roll_kernel and passes t_int = tile_hi).
-template <int NBITS, bool EDGE>
+// roll_kernel and passes t_int = tile_hi); BT: B is the tile length (the
+// reference's block length for a 1 GiB file, sqrt(2^30)): the bytes a lane
+// shifts in over tile t are the ones it shifts out over tile t + 1, so their
+// sums and their xor-ed copy carry over instead of being loaded and summed
+// again (16 v_dot4, 8 v_alignbyte, 8 v_xor and two 16-byte loads per lane
+// and tile fewer).
+template <int NBITS, bool EDGE, bool BT>
 __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
     uint32_t t_int, uint32_t tile_hi, const uint16_t *__restrict__ filter_g, const uint32_t *__restrict__ keys,
@@ -743,6 +748,20 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         __syncthreads();
     }
     uint32_t O[OW], A[OW + 4], On[OW];
+    uint32_t Cx[OW];                   // BT: the previous tile's xor-ed shifted bytes = this tile's outgoing ones
+    int32_t c1 = 0, c2 = 0, c1a = 0, c2a = 0;  // BT: and their sums (vec_sums)
+    if constexpr (BT) {
+#pragma unroll
+        for (int k = 0; k < OW; k++) Cx[k] = 0;
+    }
+    auto fetch_shifted = [&](uint32_t tt, uint32_t *a) {  // BT: the next tile's shifted bytes only (sh = 0)
+        const uint8_t *pa = src + (uint64_t)tt * kScanTile + lo + B;
+#pragma unroll
+        for (int q = 0; q < NV; q++) {
+            const u32x4a4m v = *reinterpret_cast<const u32x4a4m *>(pa + 16 * q);
+            a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
+        }
+    };
     auto fetch_plain = [&](uint32_t tt, uint32_t *o, uint32_t *a) {
         const uint8_t *p = src + (uint64_t)tt * kScanTile + lo;
 #pragma unroll
@@ -772,9 +791,27 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         const bool edge = EDGE && t >= t_int;  // windows shorter than B or offsets past end: the scalar path
         uint32_t S[OW];
 #pragma unroll
-        for (int k = 0; k < OW; k++) S[k] = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sh);
+        for (int k = 0; k < OW; k++) S[k] = BT ? A[k] : __builtin_amdgcn_alignbyte(A[k + 1], A[k], sh);
         const bool next = t + 1 < t_end && t + 1 < t_int;
-        if (next) fetch_plain(t + 1, On, A);
+        // BT: the shifted bytes' sums and xor-ed copy before the prefetch reuses A
+        int32_t s1, s2, v1, v2, s1a = 0, s2a = 0;
+        uint32_t Sx[OW];
+        if constexpr (BT) {
+            vec_sums(S, s1, s2);
+            s1a = s1;
+            s2a = s2;
+#pragma unroll
+            for (int c = 1; c < NV; c++) {
+                vec_sums(S + 4 * c, v1, v2);
+                s2 += v2 + 16 * c * v1;
+                s1 += v1;
+            }
+#pragma unroll
+            for (int k = 0; k < OW; k++) Sx[k] = S[k] ^ 0x80808080u;
+            if (next) fetch_shifted(t + 1, A);
+        } else {
+            if (next) fetch_plain(t + 1, On, A);
+        }
         uint2 pe = make_uint2(0, 0);
         uint4 pba, pbb;
         const bool pv = lane < prev_n;
@@ -785,18 +822,30 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         }
         // lane totals, and the first 16 bytes' own (stream a's range) for
         // stream b's start window
-        int32_t o1, o2, s1, s2, v1, v2;
-        vec_sums(O, o1, o2);
-        vec_sums(S, s1, s2);
-        const int32_t o1a = o1, o2a = o2, s1a = s1, s2a = s2;
+        int32_t o1, o2, o1a, o2a;
+        if (BT && have) {  // tile t - 1's shifted bytes, summed there
+            o1 = c1; o2 = c2; o1a = c1a; o2a = c2a;
+        } else {
+            vec_sums(O, o1, o2);
+            o1a = o1;
+            o2a = o2;
 #pragma unroll
-        for (int c = 1; c < NV; c++) {
-            vec_sums(O + 4 * c, v1, v2);
-            o2 += v2 + 16 * c * v1;
-            o1 += v1;
-            vec_sums(S + 4 * c, v1, v2);
-            s2 += v2 + 16 * c * v1;
-            s1 += v1;
+            for (int c = 1; c < NV; c++) {
+                vec_sums(O + 4 * c, v1, v2);
+                o2 += v2 + 16 * c * v1;
+                o1 += v1;
+            }
+        }
+        if constexpr (!BT) {
+            vec_sums(S, s1, s2);
+            s1a = s1;
+            s2a = s2;
+#pragma unroll
+            for (int c = 1; c < NV; c++) {
+                vec_sums(S + 4 * c, v1, v2);
+                s2 += v2 + 16 * c * v1;
+                s1 += v1;
+            }
         }
         // one workgroup scan of exA = ex(s1) - ex(o1), exB (roll_kernel's
         // two-value form: every window here is interior)
@@ -890,11 +939,11 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         const uint32_t W2b = W2 + 16u * W1 + 16u * da - (uint32_t)(s2a - o2a) - B * (uint32_t)o1a;
         u16x2 P1 = as_u16x2(((W1 + C128) & 0xffffu) | ((W1b + C128) << 16));
         u16x2 P2 = as_u16x2((W2 & 0xffffu) | (W2b << 16));
-        uint32_t Ox[OW], Sx[OW];
+        uint32_t Ox[OW];
 #pragma unroll
         for (int k = 0; k < OW; k++) {
-            Ox[k] = O[k] ^ 0x80808080u;
-            Sx[k] = S[k] ^ 0x80808080u;
+            Ox[k] = (BT && have) ? Cx[k] : O[k] ^ 0x80808080u;
+            if constexpr (!BT) Sx[k] = S[k] ^ 0x80808080u;
         }
         constexpr int G = 4;  // pair steps per group: 8 filter reads in flight
         uint32_t one16 = 1;  // the SDWA shift count of the filter addresses (a VGPR operand)
@@ -949,13 +998,18 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
             const uint32_t w1 = ((as_u32(P1) >> 16) - C128) & 0xffffu, w2 = as_u32(P2) >> 16;
             carry[parity] = make_uint2(w1, (uint32_t)(q0 + kScanTile + B) * w1 - w2);
         }
+        if constexpr (BT) {  // this tile's shifted bytes are the next tile's outgoing ones
+#pragma unroll
+            for (int k = 0; k < OW; k++) Cx[k] = Sx[k];
+            c1 = s1; c2 = s2; c1a = s1a; c2a = s2a;
+        }
         }  // interior tile
         if (pv) probe(prev_q0 + pe.x, table_has(pba, pbb, pe.y));
         if (prev_n > 64) drain_rest(qh ^ 1, prev_q0, 64, prev_n);
         prev_n = nq;
         prev_q0 = q0;
         qh ^= 1u;
-        if (next) {
+        if (!BT && next) {
 #pragma unroll
             for (int k = 0; k < OW; k++) O[k] = On[k];
         }
@@ -1059,6 +1113,14 @@ static bool roll_edge_inside() {
     return v;
 }
 
+bool roll_bt() {
+    static const bool v = [] {
+        const char *e = getenv("RSG_ROLL_BT");  // A/B switch: 0 = B == tile length rolls like any other B
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 int roll_filter_bits() {
     static const int v = [] {
         // A/B switch: 2 = bits S2[0..3], S2[4..7] only; default 3 adds S2[8..11]
@@ -1110,12 +1172,14 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
             if (roll_edge_inside()) {
                 // the whole range: the packed kernel rolls its edge tiles itself
                 const uint32_t ga = min(grid, tile_hi - tile_lo);
-                auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, true> : roll_packed_kernel<2, true>;
+                const bool bt = B == kScanTile && roll_bt();
+                auto kern = roll_filter_bits() == 3 ? (bt ? roll_packed_kernel<3, true, true> : roll_packed_kernel<3, true, false>)
+                                                    : (bt ? roll_packed_kernel<2, true, true> : roll_packed_kernel<2, true, false>);
                 hipLaunchKernelGGL(kern, dim3(ga), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
                                    t_int, tile_hi, filter16, table_keys, bmask, cand, cap, count);
                 return hipGetLastError();
             }
-            auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, false> : roll_packed_kernel<2, false>;
+            auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, false, false> : roll_packed_kernel<2, false, false>;
             hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, t_int,
                                t_int, filter16, table_keys, bmask, cand, cap, count);
             const hipError_t e = hipGetLastError();

@@ -129,6 +129,24 @@ def test_packed_roll_runs_vs_oracle(eng, blen):
     assert eng.hash_search(src, head, s1, s2, tg, seed) == want
 
 
+def test_packed_roll_tile_length_blocks_vs_oracle(eng):
+    """B = 32768 = the roll's tile length (the reference's block length for a
+    1 GiB file): the kernel carries each tile's shifted bytes and their sums
+    into the next tile as its outgoing bytes (roll_packed_kernel's BT form).
+    A 56 MiB source gives every workgroup a run of 7 tiles, i.e. 6 carries,
+    against the oracle (match.go:93-210)."""
+    blen = 32768
+    n = (56 << 20) + 4321
+    basis = cases.splitmix64_bytes(4500, n)
+    src = cases.mutate(basis, 4501, 0.5, 1, 3 * blen, n_ins=7, n_del=7)
+    seed = 7654321
+    head, s1, s2 = basis_sums(basis, blen, seed)
+    tg = orc.stable_targets(s1)
+    want, _, _ = orc.hash_search(src, head, s1, s2, tg, seed)
+    assert len(want) > 200
+    assert eng.hash_search(src, head, s1, s2, tg, seed) == want
+
+
 def test_identical_large_property(eng):
     """1 GiB source identical to its basis (B = 32768): every block matches at
     its own offset, in order (size-independent property at full cfg3 file size)."""
