@@ -872,8 +872,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         uint32_t lol = lo;
         asm volatile("" : "+v"(lol));
         uint32_t nq = 0;
-        auto park = [&](bool hit, uint32_t j, uint32_t raw) {
-            const uint64_t bal = __ballot(hit);
+        auto park_m = [&](uint64_t bal, bool hit, uint32_t j, uint32_t raw) {  // bal = __ballot(hit)
             if (bal) {
                 const uint32_t nb = __popcll(bal);
                 if (nq + nb <= kQueueCap) {
@@ -889,6 +888,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 }
             }
         };
+        auto park = [&](bool hit, uint32_t j, uint32_t raw) { park_m(__ballot(hit), hit, j, raw); };
         if constexpr (!EDGE) {
         } else if (edge) {
             // The source's last tiles (roll_kernel's edge path, with this
@@ -978,18 +978,29 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 P1 = P1 + ui - uo;
                 P2 = P2 + uo * negB + P1;
             }
+            // the group's eight hit masks first, then its parks: each park's
+            // branch then tests a mask computed several instructions earlier
+            // instead of waiting on the compare right before it
+            uint64_t mk[2 * G];
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
-                const int j = g0 + jj;
                 const u16x2 x = pk_shr(wd[jj], p2[jj]);
                 const u16x2 y = pk_shr(wd[jj], p2[jj] >> (uint16_t)4);
                 u16x2 xy = x & y;
                 if constexpr (NBITS == 3) xy &= pk_shr(wd[jj], p2[jj] >> (uint16_t)8);
                 uint32_t z = as_u32(xy) & 0x00010001u;
                 asm("" : "+v"(z));
+                mk[2 * jj] = __ballot((z & 0xffffu) != 0);
+                mk[2 * jj + 1] = __ballot(z > 0xffffu);
+            }
+#pragma unroll
+            for (int jj = 0; jj < G; jj++) {
+                const int j = g0 + jj;
                 const uint32_t r1 = as_u32(p1[jj]), r2 = as_u32(p2[jj]);
-                park((z & 0xffffu) != 0, (uint32_t)j, __builtin_amdgcn_perm(r2, r1, 0x05040100u));
-                park(z > 0xffffu, (uint32_t)(H + j), __builtin_amdgcn_perm(r2, r1, 0x07060302u));
+                park_m(mk[2 * jj], __builtin_amdgcn_inverse_ballot_w64(mk[2 * jj]), (uint32_t)j,
+                       __builtin_amdgcn_perm(r2, r1, 0x05040100u));
+                park_m(mk[2 * jj + 1], __builtin_amdgcn_inverse_ballot_w64(mk[2 * jj + 1]), (uint32_t)(H + j),
+                       __builtin_amdgcn_perm(r2, r1, 0x07060302u));
             }
             __builtin_amdgcn_sched_barrier(0);
         }
