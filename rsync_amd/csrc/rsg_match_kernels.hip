@@ -993,14 +993,38 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 mk[2 * jj] = __ballot((z & 0xffffu) != 0);
                 mk[2 * jj + 1] = __ballot(z > 0xffffu);
             }
+            // room in the queue for the whole group (nearly always): parks
+            // without a per-park capacity test; else park_m's own
+            uint32_t gn = 0;
 #pragma unroll
-            for (int jj = 0; jj < G; jj++) {
-                const int j = g0 + jj;
-                const uint32_t r1 = as_u32(p1[jj]), r2 = as_u32(p2[jj]);
-                park_m(mk[2 * jj], __builtin_amdgcn_inverse_ballot_w64(mk[2 * jj]), (uint32_t)j,
-                       __builtin_amdgcn_perm(r2, r1, 0x05040100u));
-                park_m(mk[2 * jj + 1], __builtin_amdgcn_inverse_ballot_w64(mk[2 * jj + 1]), (uint32_t)(H + j),
-                       __builtin_amdgcn_perm(r2, r1, 0x07060302u));
+            for (int k = 0; k < 2 * G; k++) gn += (uint32_t)__popcll(mk[k]);
+            if (nq + gn <= kQueueCap) {
+#pragma unroll
+                for (int k = 0; k < 2 * G; k++) {
+                    const int jj = k >> 1;
+                    const uint64_t bal = mk[k];
+                    if (bal) {
+                        if (__builtin_amdgcn_inverse_ballot_w64(bal)) {
+                            const uint32_t r1 = as_u32(p1[jj]), r2 = as_u32(p2[jj]);
+                            const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                                (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                            queue[wave][qh][nq + below] =
+                                make_uint2(lol + (uint32_t)((k & 1) * H + g0 + jj),
+                                           __builtin_amdgcn_perm(r2, r1, (k & 1) ? 0x07060302u : 0x05040100u));
+                        }
+                        nq += (uint32_t)__popcll(bal);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int jj = 0; jj < G; jj++) {
+                    const int j = g0 + jj;
+                    const uint32_t r1 = as_u32(p1[jj]), r2 = as_u32(p2[jj]);
+                    park_m(mk[2 * jj], __builtin_amdgcn_inverse_ballot_w64(mk[2 * jj]), (uint32_t)j,
+                           __builtin_amdgcn_perm(r2, r1, 0x05040100u));
+                    park_m(mk[2 * jj + 1], __builtin_amdgcn_inverse_ballot_w64(mk[2 * jj + 1]), (uint32_t)(H + j),
+                           __builtin_amdgcn_perm(r2, r1, 0x07060302u));
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
         }
