@@ -113,9 +113,13 @@ constexpr uint32_t kFilter16Words = 1u << 16;
 __host__ __device__ inline uint32_t f16_word(uint32_t sum, uint32_t B) {
     return ((sum + 128u * B) ^ (sum >> 16)) & 0xffffu;
 }
+// The bits sit at 15 - s (s = the nibble): the kernel shifts the word LEFT by
+// s (v_pk_lshlrev_b16 masks the count to 4 bits itself), so every tested bit
+// lands in bit 15 of its half and the AND of the shifted words is the test,
+// read by sign compares with no mask.
 __host__ __device__ inline uint32_t f16_mask(uint32_t sum, int nbits = 2) {
-    const uint32_t m = (1u << ((sum >> 16) & 15u)) | (1u << ((sum >> 20) & 15u));
-    return nbits == 3 ? m | (1u << ((sum >> 24) & 15u)) : m;
+    const uint32_t m = (0x8000u >> ((sum >> 16) & 15u)) | (0x8000u >> ((sum >> 20) & 15u));
+    return nbits == 3 ? m | (0x8000u >> ((sum >> 24) & 15u)) : m;
 }
 int roll_filter_bits();  // RSG_ROLL_BITS (read once): bits per sum in the packed roll's filter, 2 or 3
 int roll_packed();  // RSG_ROLL_PACKED (read once): 0 roll_kernel only, else the packed roll (default)

@@ -629,19 +629,19 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
 // 2^16 16-bit words indexed by P1 ^ P2 (word ((W1 + 128B) ^ W2) mod 2^16, the
 // host builds it shifted; one v_xor for both windows), bits W2[0..3],
 // W2[4..7] and W2[8..11]: a 16-bit shift of both halves at once
-// (v_pk_lshrrev_b16) per bit.  About 0.6 % of non-matching window sums pass
+// (v_pk_lshlrev_b16, the bits stored at 15 - s) per bit.  About 0.6 % of non-matching window sums pass
 // with 32768 basis sums (1.0 % with the first two bits only).
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
 __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 
-// v_pk_lshrrev_b16: each half of w shifted right by the low 4 bits of the
+// v_pk_lshlrev_b16: each half of w shifted left by the low 4 bits of the
 // same half of s (the hardware's own masking; a C shift needs an explicit
 // `& 15` the compiler keeps).
-__device__ __forceinline__ u16x2 pk_shr(u16x2 w, u16x2 s) {
+__device__ __forceinline__ u16x2 pk_shl(u16x2 w, u16x2 s) {
     uint32_t d;
-    asm("v_pk_lshrrev_b16 %0, %1, %2" : "=v"(d) : "v"(as_u32(s)), "v"(as_u32(w)));
+    asm("v_pk_lshlrev_b16 %0, %1, %2" : "=v"(d) : "v"(as_u32(s)), "v"(as_u32(w)));
     return as_u16x2(d);
 }
 
@@ -919,10 +919,10 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 }
 #pragma unroll
                 for (int jj = 0; jj < GE; jj++) {
-                    const uint32_t s2 = raw[jj] >> 16;
-                    uint32_t bits = (word[jj] >> (s2 & 15u)) & (word[jj] >> ((s2 >> 4) & 15u));
-                    if constexpr (NBITS == 3) bits &= word[jj] >> ((s2 >> 8) & 15u);
-                    park((bits & 1u) && (lol + g0 + jj < end_rel), (uint32_t)(g0 + jj), raw[jj]);
+                    const uint32_t s2 = raw[jj] >> 16;  // bits at 15 - s (f16_mask)
+                    uint32_t bits = (word[jj] << (s2 & 15u)) & (word[jj] << ((s2 >> 4) & 15u));
+                    if constexpr (NBITS == 3) bits &= word[jj] << ((s2 >> 8) & 15u);
+                    park((bits & 0x8000u) && (lol + g0 + jj < end_rel), (uint32_t)(g0 + jj), raw[jj]);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -984,14 +984,20 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
             uint64_t mk[2 * G];
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
-                const u16x2 x = pk_shr(wd[jj], p2[jj]);
-                const u16x2 y = pk_shr(wd[jj], p2[jj] >> (uint16_t)4);
+                // every tested bit shifted into bit 15 of its half (f16_mask):
+                // the AND is the test, its two sign bits the two hits (no
+                // mask; the low half by a 16-bit compare, which reads bits
+                // 0..15 only)
+                const u16x2 x = pk_shl(wd[jj], p2[jj]);
+                const u16x2 y = pk_shl(wd[jj], p2[jj] >> (uint16_t)4);
                 u16x2 xy = x & y;
-                if constexpr (NBITS == 3) xy &= pk_shr(wd[jj], p2[jj] >> (uint16_t)8);
-                uint32_t z = as_u32(xy) & 0x00010001u;
+                if constexpr (NBITS == 3) xy &= pk_shl(wd[jj], p2[jj] >> (uint16_t)8);
+                uint32_t z = as_u32(xy);
                 asm("" : "+v"(z));
-                mk[2 * jj] = __ballot((z & 0xffffu) != 0);
-                mk[2 * jj + 1] = __ballot(z > 0xffffu);
+                uint64_t mlo;
+                asm("v_cmp_gt_i16_e64 %0, 0, %1" : "=s"(mlo) : "v"(z));
+                mk[2 * jj] = mlo;
+                mk[2 * jj + 1] = __ballot((int32_t)z < 0);
             }
             // room in the queue for the whole group (nearly always): parks
             // without a per-park capacity test; else park_m's own
