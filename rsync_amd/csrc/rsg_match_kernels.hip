@@ -835,6 +835,10 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 o2 += v2 + 16 * c * v1;
                 o1 += v1;
             }
+            if constexpr (BT) {  // in this (uniform) branch, so Ox = Cx below needs no per-lane select
+#pragma unroll
+                for (int k = 0; k < OW; k++) Cx[k] = O[k] ^ 0x80808080u;
+            }
         }
         if constexpr (!BT) {
             vec_sums(S, s1, s2);
@@ -942,7 +946,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         uint32_t Ox[OW];
 #pragma unroll
         for (int k = 0; k < OW; k++) {
-            Ox[k] = (BT && have) ? Cx[k] : O[k] ^ 0x80808080u;
+            Ox[k] = BT ? Cx[k] : O[k] ^ 0x80808080u;
             if constexpr (!BT) Sx[k] = S[k] ^ 0x80808080u;
         }
         constexpr int G = 4;  // pair steps per group: 8 filter reads in flight
