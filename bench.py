@@ -176,9 +176,15 @@ def main():
     if args.ab:
         from rsync_amd import _lib
         # (product variant, diagnostic) pairs; diagnostics write meaningless records
-        names = {(2, 0): "park", (1, 3): "diag_park_memory_only", (1, 4): "diag_park_hash_only",
+        names = {(2, 0): "park", (7, 0): "park_reg", (1, 3): "diag_park_memory_only",
+                 (1, 9): "diag_park_reg_memory_only", (1, 4): "diag_park_hash_only",
                  (1, 6): "diag_linear_read_ldsdma", (1, 5): "diag_linear_read_plain",
-                 (1, 7): "diag_linear_read_ldsdma_misaligned4", (1, 8): "diag_park_memory_only_aligned"}
+                 (1, 7): "diag_linear_read_ldsdma_misaligned4", (1, 8): "diag_park_memory_only_aligned",
+                 (1, 10): "diag_stream_3w_45k_d1", (1, 11): "diag_stream_3w_21k_d3", (1, 12): "diag_stream_3w_31k_d2",
+                 (1, 13): "diag_stream_8w_8k_d1", (1, 14): "diag_stream_8w_16k_d2", (1, 15): "diag_stream_8w_31k_d2",
+                 (1, 16): "diag_stream_4w_45k_d1", (1, 17): "diag_park_swap_memory_only", (1, 18): "diag_park_swap",
+                 (1, 19): "diag_stream_3w_park_pattern", (1, 20): "diag_park_memory_no_copyout",
+                 (1, 21): "diag_park_memory_no_records", (1, 22): "diag_stream_3w_45k_8wave_wg"}
         res = {v: [] for v in names}
         for _ in range(int(os.environ.get("AB_ROUNDS", "5"))):
             for v in names:

@@ -487,7 +487,10 @@ rsg_status rsg_block_sums_host_multi(rsg_ctx *const *ctxs, int32_t n, const rsg_
  * its contiguous byte-balanced range of the global block sequence (files may
  * be split between ranks on block boundaries) on its own device.  The
  * demuxed bytes equal the single-context call's.  Rank q's records are
- * buffered in host memory until ranks < q have been written. */
+ * buffered in host memory until ranks < q have been written, at most 256 MiB
+ * per rank (plus one generator batch's records): a rank whose queue is full
+ * waits until the writer takes its records, so the call's host memory is
+ * bounded whatever the transfer size. */
 rsg_status rsg_generate_files_fd_multi(rsg_ctx *const *ctxs, int32_t n, const rsg_fd_file *files, uint64_t nfiles,
                                        int32_t seed, int32_t flags, rsg_write_fn write, void *user,
                                        rsg_sum_head *heads_out, uint64_t *bytes_written);

@@ -28,7 +28,8 @@ rsg_status rsg_testing_walk(const uint64_t *cand, uint64_t n, const int32_t *tru
  * meaningless.  1 = staged memory only, 2 = staged hashing only, 3 = park
  * memory only, 4 = park hashing only, 5 = linear read of the arena (plain
  * loads), 6 = linear read (LDS DMA), 7 = linear read (LDS DMA) 4 bytes off
- * 16-byte alignment, 8 = park memory only with 16-byte aligned requests.
+ * 16-byte alignment, 8 = park memory only with 16-byte aligned requests,
+ * 9.. = further memory-pattern diagnostics (rsg_blocksums.hip lists them).
  * 0 = off (default). */
 rsg_status rsg_testing_block_sums_diagnostic(rsg_ctx *ctx, int32_t diag);
 
@@ -40,6 +41,12 @@ rsg_status rsg_testing_block_sums_diagnostic(rsg_ctx *ctx, int32_t diag);
  * the streaming path. */
 rsg_status rsg_testing_md4(const uint8_t *data, uint64_t n, int32_t seeded, int32_t seed, uint64_t piece,
                            uint8_t out[16]);
+
+/* rsg_generate_files_fd_multi's per-rank record queue: *peak (if not NULL)
+ * = the largest number of record bytes any rank had queued during the last
+ * call; cap != 0 sets the bound per rank for later calls (default 256 MiB,
+ * rsg.h).  Process-wide, not per context. */
+rsg_status rsg_testing_multi_queue(uint64_t cap, uint64_t *peak);
 
 #ifdef __cplusplus
 }

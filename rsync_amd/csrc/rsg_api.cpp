@@ -45,6 +45,16 @@ static bool alloc_trace() {  // RSG_TIMING: report every (re)allocation of scrat
     return on;
 }
 
+// Headroom for small scratch only: a regrow frees first (hipFree waits for
+// the whole device), so a buffer that grows a little per call (the sender's
+// per-file candidate counts, lists and results) gets 25 % more and does not
+// regrow every call.  Large buffers (arenas, record buffers, the streaming
+// windows) are sized exactly, to 64 KiB, so batches that fit still fit.
+static uint64_t scratch_size(uint64_t bytes) {
+    if (bytes <= (16ull << 20)) return std::max<uint64_t>(bytes + bytes / 4, 4096);
+    return (bytes + 0xffffull) & ~0xffffull;
+}
+
 rsg_status ensure_dev(rsg_ctx *ctx, DevBuf &b, uint64_t bytes) {
     if (bytes <= b.cap) return RSG_OK;
     if (alloc_trace()) fprintf(stderr, "[rsg] alloc dev %llu -> %llu\n", (unsigned long long)b.cap, (unsigned long long)bytes);
@@ -54,10 +64,7 @@ rsg_status ensure_dev(rsg_ctx *ctx, DevBuf &b, uint64_t bytes) {
         b.p = nullptr;
         b.cap = 0;
     }
-    // headroom: a regrow frees first (hipFree waits for the whole device), so
-    // a buffer that grows a little per call (the sender's per-file candidate
-    // counts) should not regrow every call
-    uint64_t want = std::max<uint64_t>(bytes + std::min<uint64_t>(bytes / 4, 64ull << 20), 4096);
+    const uint64_t want = scratch_size(bytes);
     RSG_HIP(ctx, hipMalloc(&b.p, want));
     b.cap = want;
     return RSG_OK;
@@ -71,7 +78,7 @@ rsg_status ensure_pin(rsg_ctx *ctx, PinBuf &b, uint64_t bytes) {
         b.p = nullptr;
         b.cap = 0;
     }
-    uint64_t want = std::max<uint64_t>(bytes + std::min<uint64_t>(bytes / 4, 64ull << 20), 4096);
+    const uint64_t want = scratch_size(bytes);
     RSG_HIP(ctx, hipHostMalloc(&b.p, want, hipHostMallocDefault));
     b.cap = want;
     return RSG_OK;

@@ -512,6 +512,57 @@ __global__ __launch_bounds__(256) void diag_linear_read(const uint8_t *__restric
     if (acc == 0x12345678u) sink[0] = acc;  // keep the loads alive
 }
 
+// Timing diagnostic: the park kernel's memory pattern without its hand-off.
+// One persistent workgroup per CU (as park), NW streaming waves; chunk c =
+// PER KiB of contiguous arena (PER LDS-DMA instructions), chunk c of the
+// arena belongs to workgroup c % G and wave (c / G) % NW; a wave keeps DEPTH
+// chunks in flight (DEPTH * PER <= 63, the vmcnt cap).  The LDS content is
+// discarded (every wave DMAs into the same 64 KiB).
+__device__ __forceinline__ uint32_t park_quad_offset(uint32_t idx) {
+    const uint32_t j = idx / 45u, u = idx - 45u * j;
+    return u < 44u ? 700u * j + 16u * u : 0x80000000u;
+}
+// PAT = 1: the chunk is a park tile of 64 blocks of 700 bytes (44 800 bytes),
+// requested as park requests it (quad u of block j at 700 j + 16 u, the pad
+// quad not requested).
+template <int NW, int PER, int DEPTH, int PAT = 0>
+__global__ __launch_bounds__(64 * NW) void diag_stream_read(const uint8_t *__restrict__ arena, uint64_t bytes,
+                                                           uint32_t *__restrict__ sink) {
+    static_assert(PER * DEPTH <= 63 && PER <= 64, "vmcnt cap");
+    static_assert(PAT == 0 || PER == 45, "park tiles are 45 requests");
+    __shared__ __attribute__((aligned(16))) uint8_t buf[64 * 1024];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave >= NW) return;  // idle waves (a launch of more waves than streams)
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t chunk = PAT ? 64ull * 700 : (uint64_t)PER * 1024;
+    const uint64_t nch = bytes / chunk;
+    const uint32_t G = gridDim.x;
+    uint32_t issued = 0;
+#pragma unroll 1
+    for (uint64_t c = blockIdx.x + (uint64_t)G * wave; c < nch; c += (uint64_t)G * NW) {
+        const __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(arena + rfl64(c * chunk)), (short)0, 0x7FFFFFFF, 0x00020000);
+        if constexpr (PAT != 0) {
+#pragma unroll
+            for (int i = 0; i < PER; i++)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(buf + 1024 * i),
+                                                         16, park_quad_offset(64u * i + lane), 0, 0, 2);
+        } else {
+#pragma unroll
+            for (int i = 0; i < PER; i++)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(buf + 1024 * i),
+                                                         16, lane * 16 + 1024 * i, 0, 0, 2);
+        }
+        if (++issued >= DEPTH) {
+            if constexpr (DEPTH == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else if constexpr (DEPTH == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (buf[threadIdx.x] == 0x5a && buf[threadIdx.x + 1] == 0xa5 && bytes == 1) sink[0] = 1;
+}
+
 // ---------------------------------------------------------------- park variant (loader + register park)
 // For blocks of at most kRegMaxBytes (703: the reference's 700-byte blocks).
 // Every byte should cross HBM once, in long runs: a tile = 64 consecutive
@@ -734,6 +785,90 @@ __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, con
 #undef RSG_PK_ONE
 }
 
+// Register-staged tile (park LDR = 1): the same 45 requests as pk_issue, but
+// into the loader's VGPRs (R[i] = the 16 bytes DMA instruction i would put at
+// slot bytes [1024 i + 16 l, +16)), so a tile can be in flight while the
+// loader's slot still holds the previous one; pk_reg_store writes it to the
+// slot once that is freed.  Block j / quad offset u16 of request i are stepped
+// instead of tabulated (the tables would cost 90 VGPRs next to R's 180):
+// index 64 i + l advances by 64 = 45 + 19 per request.  Out-of-range requests
+// (quads past the block, the pad) return zeros and fetch nothing.
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+template <int AUX>
+__device__ __forceinline__ void pk_reg_issue(const uint8_t *arena, const PkDesc &d, uint32_t lane, u32x4v R[kPkDma]) {
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(arena + d.base), (short)0, 0x7FFFFFFF, 0x00020000);
+    uint32_t j = lane / 45u;
+    uint32_t u16 = 16u * (lane - 45u * j);
+    // opaque to the optimiser: the stepped (j, u16) sequence is the same for
+    // every tile, and hoisting all 45 steps out of the loader's loop costs
+    // ~90 registers (spills) to save ~5 VALU per request
+    asm volatile("" : "+v"(j), "+v"(u16));
+    if (d.regular) {
+        uint32_t off = d.B * j + u16;  // = B j + u16, stepped with j and u16
+#pragma unroll
+        for (uint32_t i = 0; i < kPkDma; i++) {
+            const uint32_t nj = j == d.jl ? d.nl : d.B;
+            R[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, u16 < nj ? off : 0x80000000u, 0, AUX);
+            const bool wrap = u16 >= 720u - 304u;
+            u16 = wrap ? u16 - 416u : u16 + 304u;
+            j += wrap ? 2u : 1u;
+            off += wrap ? 2u * d.B - 416u : d.B + 304u;
+        }
+    } else {
+        const int rel = (int)(uint32_t)(d.off - d.base);
+        constexpr uint32_t kBatch = 9;  // bpermutes issued back to back, then the loads (pk_issue)
+#pragma unroll
+        for (uint32_t i0 = 0; i0 < kPkDma; i0 += kBatch) {
+            uint32_t rj[kBatch], nj[kBatch], uq[kBatch];
+#pragma unroll
+            for (uint32_t k = 0; k < kBatch; k++) {
+                rj[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * j), rel);
+                nj[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * j), (int)d.n);
+                uq[k] = u16;
+                const bool wrap = u16 >= 720u - 304u;
+                u16 = wrap ? u16 - 416u : u16 + 304u;
+                j += wrap ? 2u : 1u;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kBatch; k++)
+                R[i0 + k] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, uq[k] < nj[k] ? rj[k] + uq[k] : 0x80000000u,
+                                                                   0, AUX);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the loads stay here, ahead of the caller's slot wait
+}
+
+__device__ __forceinline__ void pk_reg_store(uint8_t *dst, uint32_t lane, const u32x4v R[kPkDma]) {
+#pragma unroll
+    for (uint32_t i = 0; i < kPkDma; i++) *reinterpret_cast<u32x4v *>(dst + 1024u * i + 16u * lane) = R[i];
+}
+
+// LDR = 2: store R (the landed tile) into the slot request by request, each
+// register refilled with the next tile's request as soon as it is stored, so
+// the loader's 45 requests stay in flight across the hand-off.
+template <int AUX>
+__device__ __forceinline__ void pk_reg_swap(uint8_t *dst, const uint8_t *arena, const PkDesc &d, uint32_t lane,
+                                            u32x4v R[kPkDma]) {
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(arena + d.base), (short)0, 0x7FFFFFFF, 0x00020000);
+    uint32_t j = lane / 45u;
+    uint32_t u16 = 16u * (lane - 45u * j);
+    asm volatile("" : "+v"(j), "+v"(u16));
+    uint32_t off = d.B * j + u16;
+#pragma unroll
+    for (uint32_t i = 0; i < kPkDma; i++) {
+        *reinterpret_cast<u32x4v *>(dst + 1024u * i + 16u * lane) = R[i];
+        const uint32_t nj = j == d.jl ? d.nl : d.B;
+        R[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, u16 < nj ? off : 0x80000000u, 0, AUX);
+        const bool wrap = u16 >= 720u - 304u;
+        u16 = wrap ? u16 - 416u : u16 + 304u;
+        j += wrap ? 2u : 1u;
+        off += wrap ? 2u * d.B - 416u : d.B + 304u;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 // A block of a direct tile: the lane locates and loads it itself.
 __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uint64_t arena_bytes,
                                        const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file,
@@ -780,7 +915,12 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
 // none 0.1984 ms, loaders only 0.1962, copy-out at 2 0.1950, at 3 0.1942;
 // raising the hasher already while it waits for its slot: no gain,
 // profiles/r04g_ab_park_prio_ticket.json.)
-template <int MODE, int NL, int AUX, int PRIO = 0>
+// LDR: 0 = each loader DMAs its tile into the slot once the slot is freed;
+// 1 = register-staged loaders (pk_reg_issue): a loader's next tile is loaded
+// into its VGPRs right after it publishes the current one, so the HBM latency
+// overlaps the slot's hand-off to a hasher, and a freed slot is refilled by
+// 45 ds_write_b128 instead of waiting out a DMA.
+template <int MODE, int NL, int AUX, int PRIO = 0, int LDR = 0>
 __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
@@ -797,6 +937,58 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint64_t ntiles = (total_blocks + 63) / 64;
     const uint32_t G = gridDim.x;  // one persistent workgroup per CU; tile t belongs to workgroup t % G
 
+    if (LDR >= 1 && wave < NL) {
+        static_assert(LDR == 0 || NL == (int)kPkSlots, "register-staged loaders own one slot each");
+        if (PRIO >= 3) __builtin_amdgcn_s_setprio(3);
+        // loader L owns slot L and the tickets k = L mod 3
+        const uint32_t slot = wave;
+        uint32_t k = wave;
+        uint64_t t = blockIdx.x + (uint64_t)k * G;
+        PkDesc cur, nxt;
+        u32x4v R[kPkDma];
+        bool held = false;  // R holds (or is loading) cur's tile
+        if (t < ntiles) {
+            pk_locate(t, cur, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+            if (cur.staged && MODE != 2) {
+                pk_reg_issue<AUX>(arena, cur, lane, R);
+                held = true;
+            }
+        }
+#pragma unroll 1
+        while (t < ntiles) {
+            const uint64_t tn = t + (uint64_t)kPkSlots * G;
+            // the next tile's descriptor (scalar loads) while this one is in flight
+            if (tn < ntiles) pk_locate(tn, nxt, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+            while (pk_load(&sh.freeq[slot]) != k) __builtin_amdgcn_s_sleep(1);
+            sh.n[slot][lane] = cur.n;
+            if (lane == 0) sh.kind[slot] = cur.staged ? 1u : 0u;
+            bool swapped = false;
+            if (LDR == 2 && held && tn < ntiles && nxt.staged && nxt.regular) {
+                pk_reg_swap<AUX>(&sh.tile[slot][0], arena, nxt, lane, R);
+                swapped = true;
+            } else if (held) {
+                pk_reg_store(&sh.tile[slot][0], lane, R);
+            }
+            if (LDR == 2) {
+                // only the slot's LDS writes must land before the publish; the
+                // next tile's requests stay in flight
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (lane == 0) __hip_atomic_store(&sh.full[slot], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                if (lane == 0) pk_store(&sh.full[slot], k);
+            }
+            k += kPkSlots;
+            t = tn;
+            cur = nxt;
+            held = swapped;
+            if (!swapped && t < ntiles && cur.staged && MODE != 2) {
+                pk_reg_issue<AUX>(arena, cur, lane, R);
+                held = true;
+            }
+        }
+        return;
+    }
     if (wave < NL) {
         if (PRIO >= 3) __builtin_amdgcn_s_setprio(3);
         // ------------------------------------------------------------ loaders
@@ -887,7 +1079,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             uint32_t R[16 * kRegChunks];
             const uint8_t *mine = &sh.tile[slot][0] + lane * kPkPiece;
 #pragma unroll
-            for (uint32_t q = 0; q < 4 * kRegChunks; q++) {
+            for (uint32_t q = 0; q < (MODE == 4 ? 1 : 4 * kRegChunks); q++) {
                 const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
                 R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
             }
@@ -895,9 +1087,11 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);
             if (PRIO >= 3) __builtin_amdgcn_s_setprio(0);
             const uint32_t nfull = n >> 6;
-            if (MODE == 1 || MODE == 3) {
+            if (MODE == 1 || MODE == 3 || MODE == 5) {
 #pragma unroll
                 for (int q = 0; q < 16 * (int)kRegChunks; q++) h[q & 3] ^= R[q];
+            } else if (MODE == 4) {
+                h[0] ^= R[0];
             } else {
 #pragma unroll
                 for (uint32_t c = 0; c < kRegChunks; c++) {
@@ -905,7 +1099,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
                     else if (c == nfull) hash_tail<true>(R + 16 * c, 0u, 0u, n, seed, h, s1, tw);
                 }
             }
-            store_record(out, g, n, s1, tw, h);
+            if (MODE != 5 || h[0] == 0x9e3779b9u) store_record(out, g, n, s1, tw, h);
         } else {
             if (PRIO >= 3) __builtin_amdgcn_s_setprio(0);
             if (lane == 0) {
@@ -997,6 +1191,40 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     hipLaunchKernelGGL((block_sums_park<3, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                        files, wg_file, nwg, total_blocks, seed, out);
                 break;
+            case 10: hipLaunchKernelGGL((diag_stream_read<3, 45, 1>), pgrid, dim3(192), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 11: hipLaunchKernelGGL((diag_stream_read<3, 21, 3>), pgrid, dim3(192), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 12: hipLaunchKernelGGL((diag_stream_read<3, 31, 2>), pgrid, dim3(192), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 13: hipLaunchKernelGGL((diag_stream_read<8, 8, 1>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 14: hipLaunchKernelGGL((diag_stream_read<8, 16, 2>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 15: hipLaunchKernelGGL((diag_stream_read<8, 31, 2>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 16: hipLaunchKernelGGL((diag_stream_read<4, 45, 1>), pgrid, dim3(256), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 17:
+                if (max_blen <= kRegMaxBytes)
+                    hipLaunchKernelGGL((block_sums_park<1, kParkLoaders, 2, 3, 2>), pgrid, pblock, 0, stream, arena,
+                                       arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+                break;
+            case 18:
+                if (max_blen <= kRegMaxBytes)
+                    hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3, 2>), pgrid, pblock, 0, stream, arena,
+                                       arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+                break;
+            case 19: hipLaunchKernelGGL((diag_stream_read<3, 45, 1, 1>), pgrid, dim3(192), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 20:
+                if (max_blen <= kRegMaxBytes)
+                    hipLaunchKernelGGL((block_sums_park<4, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
+                                       files, wg_file, nwg, total_blocks, seed, out);
+                break;
+            case 21:
+                if (max_blen <= kRegMaxBytes)
+                    hipLaunchKernelGGL((block_sums_park<5, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
+                                       files, wg_file, nwg, total_blocks, seed, out);
+                break;
+            case 22: hipLaunchKernelGGL((diag_stream_read<3, 45, 1>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 9:
+                if (max_blen <= kRegMaxBytes)
+                    hipLaunchKernelGGL((block_sums_park<1, kParkLoaders, 2, 3, 1>), pgrid, pblock, 0, stream, arena,
+                                       arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+                break;
         }
         return hipGetLastError();
     }
@@ -1015,7 +1243,8 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     // staged kernel (6) needs a 4-byte aligned arena
     if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
-    if (v == 2 && max_blen > kRegMaxBytes) v = 1;
+    if ((v == 2 || v == 7) && max_blen > kRegMaxBytes) v = 1;
+    if (v == 7 && !aligned) v = 0;
     switch (v) {
         case 1:
             hipLaunchKernelGGL((block_sums_staged<0>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
@@ -1023,6 +1252,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             break;
         case 2:
             hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
+                               files, wg_file, nwg, total_blocks, seed, out);
+            break;
+        case 7:
+            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3, 1>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                files, wg_file, nwg, total_blocks, seed, out);
             break;
         case 6:  // blocks at any byte offset; an aligned batch takes the aligned kernel

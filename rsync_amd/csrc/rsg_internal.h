@@ -33,11 +33,12 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
 inline uint64_t block_sums_scratch_bytes(uint64_t total_blocks) { return 8 + 4 * ((total_blocks + 63) / 64); }
 
 // Product variants (-1 auto, 0 direct, 1 staged, 2 park, 3 long, 4/5 staged
-// with 128/512-byte segments, 6 staged at any byte offset) and timing
+// with 128/512-byte segments, 6 staged at any byte offset, 7 park with
+// register-staged loaders) and timing
 // diagnostics (0 off, 1..kBlockSumsDiagMax; outputs meaningless),
 // rsg_blocksums.hip; both per context (rsg_ctx::bs_variant / bs_diag).
-constexpr int kBlockSumsVariantMax = 6;
-constexpr int kBlockSumsDiagMax = 8;
+constexpr int kBlockSumsVariantMax = 7;
+constexpr int kBlockSumsDiagMax = 22;
 // RSG_BLOCKSUMS_KERNEL (read once): a context's initial variant.
 int block_sums_variant_env();
 // Fallback census of the current device: [0] staged waves, [1] park tiles

@@ -332,7 +332,9 @@ rsg_status rsg_receive_data_batch(rsg_ctx *ctx, rsg_recv_job *jobs, uint64_t njo
         std::vector<CopyJob> copies;
         uint64_t off = 0;
         for (uint64_t q = i; q < i1; q++) {
-            if (jobs[q].status != RSG_OK || host[q - i]) continue;  // failed, or checked on the host already
+            // host jobs first: a host-pool thread may be writing that job's
+            // fields right now, so its status is not read here
+            if (host[q - i] || jobs[q].status != RSG_OK) continue;  // checked on the host, or failed
             sl.lane.push_back(q);
             spans.push_back({off, jobs[q].out_len});
             if (jobs[q].out_len) copies.push_back({nullptr, jobs[q].out, jobs[q].out_len});

@@ -117,11 +117,14 @@ std::vector<std::vector<Pc>> split_batches(const std::vector<Pc> &pieces, int nb
     return out;
 }
 
-// Locks every context of a multi-context call, in array order (callers pass
-// distinct contexts; every entry point takes at most its own lock otherwise).
+// Locks every context of a multi-context call, in one canonical order (by
+// address) whatever the caller's array order, so two threads calling with
+// {a, b} and {b, a} cannot deadlock (callers pass distinct contexts; every
+// entry point takes at most its own lock otherwise).
 struct MultiLock {
     std::vector<rsg_ctx *> c;
     explicit MultiLock(const std::vector<rsg_ctx *> &v) : c(v) {
+        std::sort(c.begin(), c.end(), std::less<rsg_ctx *>());
         for (rsg_ctx *x : c) x->mu.lock();
     }
     ~MultiLock() {
@@ -208,11 +211,20 @@ rsg_status multi_pipeline(const rsg_shard_rank *ranks, int32_t n, int32_t seed, 
 
 uint64_t batch_records(const rsg_shard_batch &sb) { return sb.plan ? sb.plan->host.total_blocks : 0; }
 
-// One rank's records as they come from its generator thread.
+// One rank's records as they come from its generator thread.  The records
+// of ranks > the one being written wait here, so the queue is bounded: a
+// rank's generator blocks once `cap` bytes of its records are queued (the
+// reference generator streams its sums with bounded memory,
+// generator.go:20-52); the host memory of one call is then at most
+// (n - 1) * (cap + one chunk) beyond the generators' own staging.
+uint64_t g_queue_cap = 256ull << 20;        // rsg_testing_set_multi_queue_cap
+std::atomic<uint64_t> g_queue_peak{0};      // largest queue of the last call
 struct RankQueue {
     std::mutex mu;
-    std::condition_variable cv;
+    std::condition_variable cv;     // consumer: a chunk arrived or the rank is done
+    std::condition_variable space;  // producer: the consumer took a chunk, or abort
     std::deque<std::vector<uint8_t>> chunks;
+    uint64_t bytes = 0, cap = 0;
     bool done = false;
     rsg_status status = RSG_OK;
     std::string err;
@@ -224,7 +236,14 @@ int32_t push_chunk(void *user, const uint8_t *data, uint64_t len) {
     if (rq->abort->load()) return 1;
     std::vector<uint8_t> v(data, data + len);
     {
-        std::lock_guard<std::mutex> lk(rq->mu);
+        std::unique_lock<std::mutex> lk(rq->mu);
+        // an empty queue always takes the chunk, whatever its size
+        rq->space.wait(lk, [&] { return rq->bytes == 0 || rq->bytes + len <= rq->cap || rq->abort->load(); });
+        if (rq->abort->load()) return 1;
+        rq->bytes += len;
+        uint64_t pk = g_queue_peak.load();
+        while (rq->bytes > pk && !g_queue_peak.compare_exchange_weak(pk, rq->bytes)) {
+        }
         rq->chunks.push_back(std::move(v));
     }
     rq->cv.notify_one();
@@ -438,9 +457,11 @@ rsg_status rsg_generate_files_fd_multi(rsg_ctx *const *ctxs, int32_t n, const rs
     std::atomic<bool> abort{false};
     std::vector<RankQueue> qs((size_t)n);
     std::vector<std::thread> th;
+    g_queue_peak = 0;
     for (int q = 0; q < n; q++) {
         RankQueue &rq = qs[(size_t)q];
         rq.abort = &abort;
+        rq.cap = g_queue_cap;
         if (shards[(size_t)q].empty()) {
             rq.done = true;
             continue;
@@ -521,10 +542,12 @@ rsg_status rsg_generate_files_fd_multi(rsg_ctx *const *ctxs, int32_t n, const rs
                 if (!rq.chunks.empty()) {
                     chunk = std::move(rq.chunks.front());
                     rq.chunks.pop_front();
+                    rq.bytes -= chunk.size();
                 } else {
                     fin = true;
                 }
             }
+            rq.space.notify_one();
             if (fin) {
                 if (rq.status != RSG_OK) first = fail(c0, rq.status, "rank %d: %s", q, rq.err.c_str());
                 break;
@@ -539,7 +562,13 @@ rsg_status rsg_generate_files_fd_multi(rsg_ctx *const *ctxs, int32_t n, const rs
             }
         }
     }
-    if (first != RSG_OK) abort = true;
+    if (first != RSG_OK) {
+        abort = true;
+        for (RankQueue &rq : qs) {  // wake generators blocked on a full queue
+            std::lock_guard<std::mutex> lk(rq.mu);
+            rq.space.notify_all();
+        }
+    }
     for (auto &t : th) t.join();
     if (first != RSG_OK) return first;
     if (left) return fail(c0, RSG_ERR_HIP, "internal: %llu records missing", (unsigned long long)left);
@@ -550,6 +579,12 @@ rsg_status rsg_generate_files_fd_multi(rsg_ctx *const *ctxs, int32_t n, const rs
     }
     if ((s = flush()) != RSG_OK) return s;
     if (bytes_written) *bytes_written = written;
+    return RSG_OK;
+}
+
+rsg_status rsg_testing_multi_queue(uint64_t cap, uint64_t *peak) {
+    if (peak) *peak = g_queue_peak.load();
+    if (cap) g_queue_cap = cap;
     return RSG_OK;
 }
 

@@ -118,10 +118,12 @@ def test_device_aligned_multi_file(eng):
     assert got == want
 
 
-def test_planned_cfg2_full(eng):
+@pytest.mark.parametrize("variant", [-1, 2, 7])
+def test_planned_cfg2_full(eng, variant):
     """cfg2 at full size (1024 x 1 MiB @ B=700, generated on the device):
     every one of the 1 533 952 records bit-exact vs the oracle (~1.5 s of
-    oracle time), record count and layout exact."""
+    oracle time), record count and layout exact -- the automatic choice and
+    both park loaders (DMA, register-staged)."""
     n_files, size = 1024, 1 << 20
     arena = eng.alloc(n_files * size)
     for f in range(n_files):
@@ -129,8 +131,12 @@ def test_planned_cfg2_full(eng):
     plan = eng.plan([(f * size, size, 700) for f in range(n_files)], n_files * size)
     assert plan.total_records == n_files * 1498
     recs = eng.alloc(plan.total_records * 20)
-    plan.run(arena, cases.SEED, recs)
-    eng.synchronize()
+    try:
+        eng.set_block_sums_kernel(variant)
+        plan.run(arena, cases.SEED, recs)
+        eng.synchronize()
+    finally:
+        eng.set_block_sums_kernel(-1)
     allrec = recs.download(plan.total_records * 20).tobytes()
     for f in range(n_files):
         o = plan.first_record[f] * 20
@@ -178,7 +184,7 @@ def test_generate_and_send_sums_wire(eng):
     assert bytes(conn.buf) == want
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("blen", [700, 64, 1024, 1400, 1773, 4096, 131072])
 def test_kernel_variants_match(eng, variant, blen):
     """Every kernel variant (direct / staged / park / long / staged with 128-
@@ -251,7 +257,7 @@ def test_variants_long_blocks_full_waves(eng, variant):
     assert got == want
 
 
-@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 5, 6, 7])
 def test_variants_device_aligned_arena(eng, variant):
     """Aligned device arena (the staged / park fast paths), files straddling
     waves and tiles, a file ending exactly at the arena end (park's direct

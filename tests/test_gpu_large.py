@@ -133,7 +133,7 @@ def _run(eng, unaligned, variant, B, seed=cases.SEED):
     return files, kinds, rec, first, fb
 
 
-@pytest.mark.parametrize("variant,B", [(-1, 700), (2, 700), (1, 700), (4, 700), (4, 1024), (1, 131072),
+@pytest.mark.parametrize("variant,B", [(-1, 700), (2, 700), (7, 700), (1, 700), (4, 700), (4, 1024), (1, 131072),
                                        (-1, 131072), (5, 4096)])
 def test_aligned_arena_past_4gib(eng, variant, B):
     """Aligned batch on a 5 GiB arena: park (regular and irregular tiles) and

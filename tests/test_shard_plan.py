@@ -158,6 +158,49 @@ def test_generate_files_fd_multi(nctx, mux):
 
 
 @pytest.mark.gpu
+def test_generate_files_fd_multi_bounded_queue():
+    """Rank q's records wait in host memory until ranks < q are written; with
+    the per-rank bound set to 64 KiB (far below one rank's records) the
+    generators block instead of queueing everything, the stream is unchanged
+    and no queue ever held more than the bound plus one generator chunk."""
+    import ctypes
+    import rsync_amd
+    from rsync_amd import _lib
+    from rsync_amd.multi import MultiEngine
+    files = [cases.splitmix64_bytes(7100 + i, 8 << 20) for i in range(16)]  # 64 MiB per rank: >= 2 batches
+    tmp = tempfile.mkdtemp()
+    fds = []
+    peak = ctypes.c_uint64(0)
+    try:
+        for i, f in enumerate(files):
+            p = os.path.join(tmp, f"f{i}")
+            with open(p, "wb") as fh:
+                fh.write(f.tobytes())
+            fds.append(os.open(p, os.O_RDONLY))
+        desc = [(fd, f.size) for fd, f in zip(fds, files)]
+        one = rsync_amd.Engine(0)
+        single = []
+        one.generate_files_fd(desc, cases.SEED, single.append, block_len=700)
+        one.close()
+        _lib.lib.rsg_testing_multi_queue(64 << 10, None)
+        me = MultiEngine([rsync_amd.Engine(0) for _ in range(2)])
+        out = []
+        me.generate_files_fd(desc, cases.SEED, out.append, block_len=700)
+        me.close()
+        _lib.lib.rsg_testing_multi_queue(0, ctypes.byref(peak))
+        assert b"".join(out) == b"".join(single)
+        # one chunk is at most one generator batch's records (32 MiB of blocks)
+        chunk = (32 << 20) // 700 * 20 + 20
+        assert 0 < peak.value <= (64 << 10) + chunk, peak.value
+    finally:
+        _lib.lib.rsg_testing_multi_queue(256 << 20, None)
+        for fd in fds:
+            os.close(fd)
+        import shutil
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+@pytest.mark.gpu
 def test_generate_files_fd_multi_short_file():
     """A file shorter than its stated length on a non-first rank: RSG_ERR_IO
     (io.ReadFull's unexpected EOF), the bytes written a prefix of the stream."""
