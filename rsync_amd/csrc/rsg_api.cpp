@@ -291,6 +291,7 @@ void rsg_ctx_destroy(rsg_ctx *c) {
             if (b->p) hipFree(b->p);
         if (sl.count.p) hipHostFree(sl.count.p);
         if (sl.list.p) hipHostFree(sl.list.p);
+        if (sl.sel.p) hipHostFree(sl.sel.p);
         if (sl.stage.p) hipHostFree(sl.stage.p);
         if (sl.hres.p) hipHostFree(sl.hres.p);
         if (sl.scanned) hipEventDestroy(sl.scanned);

@@ -50,6 +50,7 @@ struct SearchSlot {
     PinBuf count;                      // candidate count read back
     DevBuf res;                        // confirmation results (block index per window)
     PinBuf hres;                       // ... read back; the job's walk reads them on a worker thread
+    PinBuf sel;                        // offsets of the windows a confirm_all batch confirms (the GPU plan reads them)
     hipEvent_t scanned = nullptr;      // prefix pass done (side stream)
     hipEvent_t tables_b = nullptr;     // the resolve tables' upload done (side stream)
     hipEvent_t rolled = nullptr;       // roll kernel + count read-back done

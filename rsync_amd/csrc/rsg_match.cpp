@@ -299,8 +299,49 @@ struct Walker {
     uint64_t dense_until = 0;           // candidates below this offset were judged dense
     uint32_t width = 2;                 // successors per chain step in a dense stretch
 
+    bool spec = spec_on();              // speculative selection of sparse batches
+
     uint32_t window(uint64_t q) const { return (uint32_t)std::min<uint64_t>((uint64_t)head.block_len, size - q); }
     int64_t len_of(int32_t i) const { return (i == head.count - 1 && head.rem != 0) ? head.rem : head.block_len; }
+
+    static bool spec_on() {  // RSG_CONFIRM_SPEC=0 (A/B): confirm every pending candidate of a sparse stretch
+        static const bool on = [] {
+            const char *e = getenv("RSG_CONFIRM_SPEC");
+            return !(e && e[0] == '0');
+        }();
+        return on;
+    }
+    // Candidate j sits in a chain: another candidate exactly B before or after
+    // it, as consecutive matched blocks give (match.go:158 moves the walk
+    // from a match at q to q + B).  A random false weak hit almost never does.
+    bool chained(const std::vector<uint64_t> &C, size_t j) const {
+        const uint64_t B = (uint64_t)head.block_len, c = C[j];
+        const auto f = std::lower_bound(C.begin() + (int64_t)j + 1, C.end(), c + B);
+        if (f != C.end() && *f == c + B) return true;
+        if (c < B) return false;
+        const auto b = std::lower_bound(C.begin(), C.begin() + (int64_t)j, c - B);
+        return b != C.begin() + (int64_t)j && *b == c - B;
+    }
+    // The pending candidates the walk visits from C[i] (visited) on if every
+    // chained pending candidate matches a block of length window() and every
+    // other one fails; known results are taken as they are.  Confirming only
+    // these skips the false weak hits inside matched spans, which the greedy
+    // walk jumps over (match.go:158-167); a wrong guess only uncovers
+    // candidates the next round trip confirms.
+    void spec_batch(const std::vector<uint64_t> &C, const std::vector<int32_t> &res, size_t i,
+                    std::vector<uint32_t> &batch) const {
+        uint64_t x = C[i];
+        for (size_t j = i; j < C.size() && batch.size() < kSparseBatch && (int64_t)C[j] < end; j++) {
+            const uint64_t c = C[j];
+            if (c < x) continue;
+            if (res[j] == -2) {
+                batch.push_back((uint32_t)j);
+                x = chained(C, j) ? c + window(c) : c + 1;
+            } else {
+                x = res[j] >= 0 ? c + (uint64_t)len_of(res[j]) : c + 1;
+            }
+        }
+    }
 
     rsg_status run(const std::vector<uint64_t> &C, uint64_t &pos, std::vector<int32_t> *known) {
         std::vector<int32_t> res = known ? std::move(*known) : std::vector<int32_t>(C.size(), -2);
@@ -329,6 +370,10 @@ struct Walker {
                         dense_until = C[j - 1];
                     } else {
                         width = 2;  // a sparse stretch: the next dense one starts narrow again
+                        if (spec) {
+                            batch.clear();
+                            spec_batch(C, res, i, batch);
+                        }
                     }
                 }
                 if (dense) {
@@ -402,76 +447,87 @@ rsg_status walk(Search &S, const std::vector<uint64_t> &C, uint64_t &pos, std::v
 
 rsg_status launch_range(Search &S, uint32_t lo, uint32_t hi);
 
-// A sparse range's candidates all confirmed at once (what walk() batches for
-// a sparse range anyway), with the plan built on the GPU from the roll's own
-// list: the confirmation starts as soon as the count is known.  The host
-// reads the list back and sorts it while the GPU hashes; C = the sorted
-// distinct offsets, res = their results (the walk's input).
-rsg_status confirm_all(Search &S, uint32_t n, std::vector<uint64_t> &key) {
+// A sparse range's candidates confirmed in one batch with the plan built on
+// the GPU (confirm_plan_kernel) from the windows' offsets: the host sorts the
+// roll's list (pinned host memory the roll wrote), picks the windows the walk
+// will visit (Walker::spec_batch: chained candidates assumed to match, the
+// false weak hits inside their spans skipped), writes their offsets to pinned
+// memory and queues the confirmation.  C = the sorted distinct offsets, sel =
+// the confirmed ones (indices into C), results in sel order.
+rsg_status confirm_all(Search &S, uint32_t n, uint64_t pos, std::vector<uint64_t> &C, std::vector<uint32_t> &sel) {
     rsg_ctx *ctx = S.ctx;
     SearchSlot &sl = *S.sl;
-    HostPlan plan;
-    plan.total_blocks = n;
-    plan.nwg = (n + rsg::kBlockSumThreads - 1) / rsg::kBlockSumThreads;
-    plan.aligned = false;
-    plan.arena_bytes = S.size;
-    plan.max_blen = (uint32_t)S.head.block_len;  // windows are at most B long
-    plan.lds_reserve = S.confirm_lds;
     rsg_status s;
-    if ((s = need_resolve_tables(S)) != RSG_OK) return s;
-    S.pt.mark("c.partb");
-    if ((s = ensure_dev(ctx, ctx->d_files, (uint64_t)n * sizeof(DevFile) + 32)) != RSG_OK) return s;
-    if ((s = ensure_dev(ctx, ctx->d_wg, ((uint64_t)plan.nwg + 1) * sizeof(uint32_t) + 4)) != RSG_OK) return s;
-    if ((s = ensure_dev(ctx, ctx->d_out[0], (uint64_t)n * kRecordBytes)) != RSG_OK) return s;
-    if ((s = ensure_dev(ctx, ctx->d_fb[0], rsg::block_sums_scratch_bytes(n))) != RSG_OK) return s;
-    if ((s = ensure_dev(ctx, sl.res, (uint64_t)n * 4)) != RSG_OK) return s;
-    if ((s = ensure_pin(ctx, sl.hres, (uint64_t)n * 4)) != RSG_OK) return s;
-    RSG_HIP(ctx, rsg::launch_confirm_plan((const uint64_t *)sl.list.p, n, S.size, (uint32_t)S.head.block_len,
-                                          (DevFile *)ctx->d_files.p, (uint32_t *)ctx->d_wg.p, plan.nwg, S.cst));
-    hipEvent_t t0 = timed_begin(ctx, S.cst);
-    if (ctx->timing) ctx->stat_windows += n;
-    if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, S.d_src, S.seed, ctx->d_out[0].p, ctx->d_fb[0].p,
-                         S.cst)) != RSG_OK)
-        return s;
-    RSG_HIP(ctx, rsg::launch_resolve((const uint8_t *)ctx->d_out[0].p, (const DevFile *)ctx->d_files.p, n,
-                                     S.d_groups, S.d_hi16, S.d_sum2, S.head.count, S.head.block_len, S.head.rem,
-                                     S.head.s2len, (int32_t *)sl.res.p, S.cst));
-    timed_end(ctx, t0, S.cst, 1);
-    RSG_HIP(ctx, hipMemcpyAsync(sl.hres.p, sl.res.p, (uint64_t)n * 4, hipMemcpyDeviceToHost, S.cst));
+    C.resize(n);
+    memcpy(C.data(), sl.list.p, (size_t)n * 8);
+    sort_offsets(C);
+    C.erase(std::unique(C.begin(), C.end()), C.end());
+    sel.clear();
+    const size_t i0 = std::lower_bound(C.begin(), C.end(), pos) - C.begin();
+    if (i0 < C.size() && (int64_t)C[i0] < S.end) {
+        Walker w;
+        w.end = S.end;
+        w.size = S.size;
+        w.head = S.head;
+        if (w.spec) {
+            const std::vector<int32_t> unknown(C.size(), -2);
+            w.spec_batch(C, unknown, i0, sel);
+        } else {
+            for (size_t j = i0; j < C.size() && (int64_t)C[j] < S.end; j++) sel.push_back((uint32_t)j);
+        }
+    }
+    S.pt.mark("c.select");
+    const uint32_t m = (uint32_t)sel.size();
+    if (ctx->timing) ctx->stat_windows += m;
+    if (m) {
+        HostPlan plan;
+        plan.total_blocks = m;
+        plan.nwg = (m + rsg::kBlockSumThreads - 1) / rsg::kBlockSumThreads;
+        plan.aligned = false;
+        plan.arena_bytes = S.size;
+        plan.max_blen = (uint32_t)S.head.block_len;  // windows are at most B long
+        plan.lds_reserve = S.confirm_lds;
+        if ((s = need_resolve_tables(S)) != RSG_OK) return s;
+        S.pt.mark("c.partb");
+        if ((s = ensure_pin(ctx, sl.sel, (uint64_t)m * 8)) != RSG_OK) return s;
+        uint64_t *so = (uint64_t *)sl.sel.p;
+        for (uint32_t k = 0; k < m; k++) so[k] = C[sel[k]];
+        if ((s = ensure_dev(ctx, ctx->d_files, (uint64_t)m * sizeof(DevFile) + 32)) != RSG_OK) return s;
+        if ((s = ensure_dev(ctx, ctx->d_wg, ((uint64_t)plan.nwg + 1) * sizeof(uint32_t) + 4)) != RSG_OK) return s;
+        if ((s = ensure_dev(ctx, ctx->d_out[0], (uint64_t)m * kRecordBytes)) != RSG_OK) return s;
+        if ((s = ensure_dev(ctx, ctx->d_fb[0], rsg::block_sums_scratch_bytes(m))) != RSG_OK) return s;
+        if ((s = ensure_dev(ctx, sl.res, (uint64_t)m * 4)) != RSG_OK) return s;
+        if ((s = ensure_pin(ctx, sl.hres, (uint64_t)m * 4)) != RSG_OK) return s;
+        RSG_HIP(ctx, rsg::launch_confirm_plan(so, m, S.size, (uint32_t)S.head.block_len, (DevFile *)ctx->d_files.p,
+                                              (uint32_t *)ctx->d_wg.p, plan.nwg, S.cst));
+        hipEvent_t t0 = timed_begin(ctx, S.cst);
+        if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, S.d_src, S.seed, ctx->d_out[0].p, ctx->d_fb[0].p,
+                             S.cst)) != RSG_OK)
+            return s;
+        RSG_HIP(ctx, rsg::launch_resolve((const uint8_t *)ctx->d_out[0].p, (const DevFile *)ctx->d_files.p, m,
+                                         S.d_groups, S.d_hi16, S.d_sum2, S.head.count, S.head.block_len, S.head.rem,
+                                         S.head.s2len, (int32_t *)sl.res.p, S.cst));
+        timed_end(ctx, t0, S.cst, 1);
+        RSG_HIP(ctx, hipMemcpyAsync(sl.hres.p, sl.res.p, (uint64_t)m * 4, hipMemcpyDeviceToHost, S.cst));
+    }
     if (!sl.confirmed) RSG_HIP(ctx, hipEventCreateWithFlags(&sl.confirmed, sync_event_flags()));
     RSG_HIP(ctx, hipEventRecord(sl.confirmed, S.cst));
     S.pt.mark("c.launch");
-    if ((s = run_hook(S, false)) != RSG_OK) return s;  // the next job's roll, if its tables are built
-    S.pt.mark("c.hook");
-    // the list, keyed (offset << 22 | list index) so the sort carries each
-    // offset's record index (offsets < 2^42, indices < kCandCap = 2^22)
-    // (the roll wrote it to pinned host memory; `rolled` was waited for)
-    key.resize(n);
-    const uint64_t *hl = (const uint64_t *)sl.list.p;
-    for (uint32_t i = 0; i < n; i++) key[i] = (hl[i] << 22) | i;
-    sort_offsets(key, 22);
-    S.pt.mark("c.sort");
-    return run_hook(S, false);
+    return run_hook(S, false);  // the next job's roll, if its tables are built
 }
 
 // The rest of a confirm_all job, after its confirmation was queued: wait for
-// the results, pair them with the sorted distinct offsets, walk.  Touches only
-// S and its slot's pinned results (no HIP call but an event wait), so it can
-// run on a worker thread while the next jobs are confirmed and rolled.
-rsg_status confirm_all_tail(Search &S, const std::vector<uint64_t> &key, uint64_t &pos) {
+// the results, walk (confirming, in further round trips, any window the
+// selection did not foresee).  Touches only S and its slot's pinned results
+// (no HIP call but an event wait) until the walk needs another round trip, so
+// it can run on a worker thread while the next jobs are confirmed and rolled.
+rsg_status confirm_all_tail(Search &S, const std::vector<uint64_t> &C, const std::vector<uint32_t> &sel,
+                            uint64_t &pos) {
     if (hipEventSynchronize(S.sl->confirmed) != hipSuccess) return RSG_ERR_HIP;
     S.pt.mark("c.kernel");
     const int32_t *found = (const int32_t *)S.sl->hres.p;
-    std::vector<uint64_t> C;
-    std::vector<int32_t> res;
-    C.reserve(key.size());
-    res.reserve(key.size());
-    for (uint64_t k : key) {
-        const uint64_t off = k >> 22;
-        if (!C.empty() && C.back() == off) continue;
-        C.push_back(off);
-        res.push_back(found[k & ((1u << 22) - 1)]);
-    }
+    std::vector<int32_t> res(C.size(), -2);
+    for (size_t k = 0; k < sel.size(); k++) res[sel[k]] = found[k];
     rsg_status s = walk(S, C, pos, &res);
     S.pt.mark("walk");
     return s;
@@ -753,21 +809,22 @@ rsg_status finish(Search &S) {
         }();
         if (all_env && n > 0 && n <= kSparseBatch && S.size < (1ull << 42) &&
             (uint64_t)n * (uint64_t)S.head.block_len <= 2 * range + (1u << 20)) {
-            auto key = std::make_shared<std::vector<uint64_t>>();
-            if ((s = confirm_all(S, n, *key)) != RSG_OK) return s;
+            auto Cs = std::make_shared<std::vector<uint64_t>>();
+            auto sel = std::make_shared<std::vector<uint32_t>>();
+            if ((s = confirm_all(S, n, pos, *Cs, *sel)) != RSG_OK) return s;
             if (hi == S.tile_end) {
                 // the job's last range: the caller may run the rest anywhere
                 Search *Sp = &S;
                 const uint64_t p0 = pos;
-                S.tail = [Sp, key, p0]() {
+                S.tail = [Sp, Cs, sel, p0]() {
                     uint64_t p = p0;
-                    const rsg_status st = confirm_all_tail(*Sp, *key, p);
+                    const rsg_status st = confirm_all_tail(*Sp, *Cs, *sel, p);
                     Sp->pos_end = p;
                     return st;
                 };
                 break;
             }
-            if ((s = confirm_all_tail(S, *key, pos)) != RSG_OK) return s;
+            if ((s = confirm_all_tail(S, *Cs, *sel, pos)) != RSG_OK) return s;
             lo = hi;
             continue;
         }

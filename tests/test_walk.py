@@ -114,3 +114,73 @@ def test_dense_alternating_failures():
     assert got == reference_walk(cand, truth, size, head)
     # ~64 visited matches per round trip once the reach set is 8 wide
     assert trips <= len(got) // 32 + 8, trips
+
+
+def _cfg3_like(seed, blen=32768, size=256 << 20, false_hits=2048):
+    """Runs of consecutive matched blocks at shifted offsets (cfg3: a basis
+    with half its blocks modified and a few insertions), plus random false
+    weak hits (equal Sum1, different MD4) everywhere, inside matched spans too."""
+    rng = np.random.default_rng(seed)
+    head = head_for(size, blen)
+    cand, truth, q = [], [], int(rng.integers(0, blen))
+    while q + blen <= size:
+        run = int(rng.integers(1, 12))
+        b0 = int(rng.integers(0, head[0] - run))
+        for k in range(run):
+            if q + blen > size:
+                break
+            cand.append(q)
+            truth.append(b0 + k)
+            q += blen
+        q += int(rng.integers(1, 6 * blen))  # a modified stretch, not a multiple of B
+    fh = rng.integers(0, size - blen, false_hits)
+    cand += fh.tolist()
+    truth += [-1] * false_hits
+    c = np.asarray(cand, np.uint64)
+    t = np.asarray(truth, np.int32)
+    order = np.argsort(c, kind="stable")
+    c, t = c[order], t[order]
+    keep = np.concatenate([[True], c[1:] != c[:-1]])
+    return c[keep], t[keep], size, head
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_sparse_speculative_selection(seed):
+    """cfg3's shape: the sparse batch confirms only the windows the walk
+    visits if chained candidates (another candidate B before or after) match
+    -- the false hits inside matched spans are never hashed -- and the match
+    list is the greedy walk's.  Isolated true matches (one-block runs) and
+    false hits that happen to be chained cost at most a few extra trips."""
+    cand, truth, size, head = _cfg3_like(seed)
+    got, trips, windows = walk(cand, truth, size, head)
+    want = reference_walk(cand, truth, size, head)
+    assert got == want
+    # visited offsets: every match plus the false hits outside matched spans
+    pos, visited = 0, 0
+    for q, b in zip(cand.tolist(), truth.tolist()):
+        if q < pos:
+            continue
+        visited += 1
+        if b >= 0:
+            pos = q + head[1]
+    assert trips <= 4, trips
+    assert windows <= visited + 64 * trips, (windows, visited, cand.size)
+    assert windows < cand.size
+
+
+def test_sparse_speculation_wrong_chains():
+    """Chained false hits (a pair of candidates B apart, both failing MD4)
+    sends the speculative walk past candidates the real walk visits; those
+    are confirmed in later round trips and the result is still exact."""
+    blen = 4096
+    size = 16 << 20
+    head = head_for(size, blen)
+    rng = np.random.default_rng(5)
+    base = np.sort(rng.choice(np.arange(0, size - 2 * blen, 3 * blen), 600, replace=False)).astype(np.uint64)
+    pairs = np.concatenate([base, base + blen])
+    inner = base + 17  # visited after the pair's first candidate fails
+    cand = np.unique(np.concatenate([pairs, inner])).astype(np.uint64)
+    truth = np.where(np.isin(cand, inner), 3, -1).astype(np.int32)
+    got, trips, windows = walk(cand, truth, size, head)
+    assert got == reference_walk(cand, truth, size, head)
+    assert windows <= 2 * cand.size
