@@ -494,41 +494,6 @@ def guarded_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, record
 
 
 
-def make_cfg3_file(eng, basis, src, size, seed, B, rng):
-    """Source = the basis with random runs (1 B .. 2B long) overwritten until
-    ~50% of the bytes differ, plus a few insertions/deletions so matches fall at
-    offsets that are not multiples of B.  Built on the
-    device with splitmix64 fills and device copies; returns the source length."""
-    import rsync_amd
-    from rsync_amd import _lib
-    eng.fill_splitmix64(basis, size, seed)
-    # shifts: copy basis pieces with small gaps/overlaps into src
-    cuts = sorted(rng.choice(np.arange(1, size - 1), 8, replace=False).tolist())
-    pos_src, prev = 0, 0
-    for i, c in enumerate(cuts + [size]):
-        n = max(0, c - prev)
-        _lib.check(_lib.lib.rsg_memcpy_d2d(eng.ctx, rsync_amd.engine.ctypes.c_void_p(src.ptr + pos_src),
-                                            rsync_amd.engine.ctypes.c_void_p(basis.ptr + prev), n), eng.ctx)
-        pos_src += n
-        if i % 2 == 0 and c < size:  # insertion of random bytes
-            k = int(rng.integers(1, 64))
-            eng.fill_splitmix64(src, k, seed * 7919 + i, offset=pos_src)
-            pos_src += k
-        elif c < size:  # deletion
-            prev = c + int(rng.integers(1, 64))
-            continue
-        prev = c
-    total = pos_src
-    touched, run_seed = 0, 1
-    while touched < total // 2:
-        ln = int(rng.integers(1, 2 * B))
-        at = int(rng.integers(0, total - ln))
-        eng.fill_splitmix64(src, ln, seed * 104729 + run_seed, offset=at)
-        run_seed += 1
-        touched += ln
-    return total
-
-
 def bench_sender(args, rank, world, local):
     """cfg3: sender byte-rolling match, 10 x 1 GiB sources vs 50%-modified bases
     on one GPU (the files shard across GPUs with no exchange).  Metric: source
@@ -536,6 +501,7 @@ def bench_sender(args, rank, world, local):
     import torch
     import rsync_amd
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import cases
     eng = rsync_amd.Engine(local)
     size = 1 << 30
     rng = np.random.default_rng(3 + rank)
@@ -544,7 +510,7 @@ def bench_sender(args, rank, world, local):
     for f in range(args.cfg3_files):
         src = eng.alloc(size + 4096)
         seed = 1000 * rank + f + 3
-        n = make_cfg3_file(eng, basis, src, size, seed, 32768, rng)
+        n = cases.make_cfg3_file(eng, basis, src, size, seed, 32768, rng)
         recs, total = eng.block_sums_device(basis, [(0, size, 0)], SEED)
         rec = recs.download(total * 20).reshape(-1, 20)
         recs.free()
@@ -622,7 +588,7 @@ def bench_sender(args, rank, world, local):
                          f"(scalar C restatement of match.go:21-282), 1 thread, {t_cpu:.1f} s"}
     host_path = None
     if rank == 0 and world == 1 and not args.no_host_path:
-        host_path = sender_host_path(eng, srcs[0], metas[0], res[0])
+        host_path = sender_host_path(eng, srcs, metas, res)
     if rank == 0:
         print(json.dumps({"metric": "GiB/s source scanned (sender rolling match), device-resident",
                           "value": round(scanned / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
@@ -653,42 +619,66 @@ def bench_sender(args, rank, world, local):
     eng.close()
 
 
-def sender_host_path(eng, src, meta, dev_res):
-    """The sender from a file (rsg_hash_search_fd, row a13): file 0's source
-    written to /dev/shm (page cache), read by the engine in 256 MiB windows
-    (pread -> pinned -> H2D, overlapped with the search), with and without the
-    whole-file sum MD4(seed || source) (match.go:52-53) computed on a host
-    thread over the same bytes.  PCIe-inclusive; never the line's value."""
+def sender_host_path(eng, srcs, metas, dev_res):
+    """The sender from files (rows a13 + f2): the sources written to /dev/shm
+    (page cache) and read by the engine in 256 MiB windows (pread -> pinned
+    -> H2D, overlapped with the search).
+    * file 0 alone through rsg_hash_search_fd, with and without the
+      whole-file sum MD4(seed || source) (match.go:52-53) on a host thread;
+    * all files through rsg_hash_search_fd_batch (SendFiles' loop), the
+      files' sums on RSG_SUM_THREADS host threads side by side.
+    PCIe-inclusive; never the line's value."""
     import tempfile
-    n, head, s1, s2, tg = meta
-    data = src.download(n)
     tmp = tempfile.mkdtemp(dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
-    p = os.path.join(tmp, "src0")
     out = {}
+    fds = []
     try:
-        with open(p, "wb") as fh:
-            fh.write(data.tobytes())
-        del data
-        fd = os.open(p, os.O_RDONLY)
-        try:
-            want = [(int(o), int(i)) for o, i in zip(dev_res["offset"], dev_res["index"])]
-            eng.hash_search_fd(fd, n, head, s1, s2, tg, SEED)  # warm the staging buffers
-            for tag, fs in (("search_only", False), ("with_file_sum", True)):
-                ts = []
-                for _ in range(3):
-                    t0 = time.perf_counter()
-                    r = eng.hash_search_fd(fd, n, head, s1, s2, tg, SEED, file_sum=fs)
-                    ts.append(time.perf_counter() - t0)
-                m = r[0] if fs else r
-                dt = sorted(ts)[1]
-                out[tag] = {"gib_s": round(n / dt / GIB, 3), "s": round(dt, 4), "matches_equal_device_path": m == want}
-        finally:
-            os.close(fd)
+        for k, (src, meta) in enumerate(zip(srcs, metas)):
+            data = src.download(meta[0])
+            p = os.path.join(tmp, f"src{k}")
+            with open(p, "wb") as fh:
+                fh.write(data.tobytes())
+            del data
+            fds.append(os.open(p, os.O_RDONLY))
+        n, head, s1, s2, tg = metas[0]
+        fd = fds[0]
+        want0 = [(int(o), int(i)) for o, i in zip(dev_res[0]["offset"], dev_res[0]["index"])]
+        eng.hash_search_fd(fd, n, head, s1, s2, tg, SEED)  # warm the staging buffers
+        for tag, fs in (("search_only", False), ("with_file_sum", True)):
+            ts = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                r = eng.hash_search_fd(fd, n, head, s1, s2, tg, SEED, file_sum=fs)
+                ts.append(time.perf_counter() - t0)
+            m = r[0] if fs else r
+            dt = sorted(ts)[1]
+            out[tag] = {"gib_s": round(n / dt / GIB, 3), "s": round(dt, 4), "matches_equal_device_path": m == want0}
+        jobs = [(fd_k, m[0], m[1], m[2], m[3], m[4]) for fd_k, m in zip(fds, metas)]
+        total = sum(m[0] for m in metas)
+        for tag, fs in (("batch_search_only", False), ("batch_with_file_sums", True)):
+            ts = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                r = eng.hash_search_fd_batch(jobs, SEED, file_sums=fs)
+                ts.append(time.perf_counter() - t0)
+            dt = sorted(ts)[1]
+            eq = all([(int(o), int(i)) for o, i in zip(d["offset"], d["index"])] == m for d, (m, _) in zip(dev_res, r))
+            out[tag] = {"gib_s": round(total / dt / GIB, 3), "s": round(dt, 4), "files": len(jobs),
+                        "matches_equal_device_path": eq}
+            if fs:
+                out[tag]["sum_threads"] = int(os.environ.get("RSG_SUM_THREADS", "10"))
+                # file 0's sum against the single-file call's (itself checked against the oracle in the tests)
+                out[tag]["file0_sum_equal_single_call"] = r[0][1] == eng.hash_search_fd(
+                    fds[0], n, head, s1, s2, tg, SEED, file_sum=True)[1]
     finally:
+        for f in fds:
+            os.close(f)
         import shutil
         shutil.rmtree(tmp, ignore_errors=True)
-    out["sample"] = ("file 0 (1 GiB) in /dev/shm, rsg_hash_search_fd with 256 MiB windows; median of 3; "
-                     "with_file_sum adds MD4(seed || source) on a host thread (one serial chain per file)")
+    out["sample"] = ("sources in /dev/shm read by the engine in 256 MiB windows; median of 3. search_only / "
+                     "with_file_sum: file 0 through rsg_hash_search_fd (its MD4(seed || source) on one host "
+                     "thread); batch_*: all files through rsg_hash_search_fd_batch, the files' sums on host "
+                     "threads side by side")
     return out
 
 

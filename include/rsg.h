@@ -34,7 +34,8 @@
 extern "C" {
 #endif
 
-#define RSG_ABI_VERSION 2  /* 2: per-context block-sum kernel knob, multi-GPU calls, rsg_hash_search_fd */
+#define RSG_ABI_VERSION 3  /* 2: per-context block-sum kernel knob, multi-GPU calls, rsg_hash_search_fd;
+                              3: rsg_hash_search_fd_batch */
 /* One wire record: int32 LE sum1 then sum2[16] (generator.go:341-346). */
 #define RSG_RECORD_BYTES 20
 #define RSG_SUM2_BYTES 16
@@ -253,6 +254,38 @@ rsg_status rsg_hash_search_device(rsg_ctx *ctx, const void *d_src, uint64_t src_
 rsg_status rsg_hash_search_fd(rsg_ctx *ctx, int32_t fd, int64_t offset, uint64_t src_len, const rsg_sum_head *head,
                               const uint32_t *sum1, const uint8_t *sum2, const int32_t *targets, int32_t seed,
                               rsg_match *matches, uint64_t match_cap, uint64_t *n_matches, uint8_t file_sum[16]);
+
+/* rsg_hash_search_fd over the files of a transfer (SendFiles' per-file loop,
+ * sender.go:19-115, for sources that are open files): each job is searched
+ * as rsg_hash_search_fd would (windows, B-1 halo, "file has changed
+ * mid-transfer"), in job order, while the jobs' whole-file sums
+ * MD4(int32_LE(seed) || source) (match.go:52-53,220-226) run on
+ * RSG_SUM_THREADS host threads (default 10; longest file first, each thread
+ * reading its file's bytes itself), so several files' serial MD4 chains
+ * proceed side by side instead of one after the other.  file_sum = NULL
+ * skips a job's sum; head.count == 0 (sendFile) reads the file only for it.
+ * Every job's n_matches and status are set: RSG_OK, RSG_ERR_INVALID (its own
+ * arguments), RSG_ERR_TRUNCATED (beyond match_cap; n_matches is the full
+ * count), RSG_ERR_IO (short file / read error).  A HIP or allocation failure
+ * stops the searches and every unfinished job gets its status.  Returns
+ * RSG_OK or the first failing job's status, its message in rsg_last_error. */
+typedef struct rsg_fd_search_job {
+    int32_t fd;              /* open for reading                              */
+    int32_t reserved;
+    int64_t offset;          /* first byte of the source in fd                */
+    uint64_t src_len;        /* the stat'ed size                              */
+    rsg_sum_head head;
+    const uint32_t *sum1;    /* as rsg_hash_search_*                          */
+    const uint8_t *sum2;
+    const int32_t *targets;
+    rsg_match *matches;
+    uint64_t match_cap;
+    uint64_t n_matches;      /* out */
+    uint8_t *file_sum;       /* out: 16 bytes, or NULL                        */
+    int32_t status;          /* out */
+    int32_t reserved2;
+} rsg_fd_search_job;
+rsg_status rsg_hash_search_fd_batch(rsg_ctx *ctx, rsg_fd_search_job *jobs, uint64_t njobs, int32_t seed);
 
 /* Batched search over the files of a transfer: replaces SendFiles' per-file
  * loop (sender.go:19-115) once their sums have been read, i.e. one

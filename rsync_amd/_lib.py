@@ -24,7 +24,7 @@ RECORD_BYTES = 20
 FILESUM_PLAIN = 0   # MD4(file), rsyncchecksum.go:60-66
 FILESUM_SEEDED = 1  # MD4(int32_LE(seed) || file), match.go:52-53
 CHUNK_SIZE = 256 * 1024
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 OK = 0
 ERR_INVALID = -1
@@ -66,6 +66,16 @@ class SearchJob(ctypes.Structure):
                 ("sum1", ctypes.c_void_p), ("sum2", ctypes.c_void_p), ("targets", ctypes.c_void_p),
                 ("matches", ctypes.POINTER(Match)), ("match_cap", ctypes.c_uint64),
                 ("n_matches", ctypes.c_uint64), ("status", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class FdSearchJob(ctypes.Structure):
+    """rsg_fd_search_job: one source file of rsg_hash_search_fd_batch (n_matches, file_sum, status out)."""
+    _fields_ = [("fd", ctypes.c_int32), ("reserved", ctypes.c_int32), ("offset", ctypes.c_int64),
+                ("src_len", ctypes.c_uint64), ("head", SumHead),
+                ("sum1", ctypes.c_void_p), ("sum2", ctypes.c_void_p), ("targets", ctypes.c_void_p),
+                ("matches", ctypes.POINTER(Match)), ("match_cap", ctypes.c_uint64),
+                ("n_matches", ctypes.c_uint64), ("file_sum", ctypes.c_void_p),
+                ("status", ctypes.c_int32), ("reserved2", ctypes.c_int32)]
 
 
 class FdFile(ctypes.Structure):
@@ -147,6 +157,7 @@ _PROTOS = {
                                  ctypes.POINTER(Match), _u64, ctypes.POINTER(_u64), _vp]),
     "rsg_hash_search_batch_device": (_st, [_vp, ctypes.POINTER(SearchJob), _u64, _i32]),
     "rsg_hash_search_batch_host": (_st, [_vp, ctypes.POINTER(SearchJob), _u64, _i32]),
+    "rsg_hash_search_fd_batch": (_st, [_vp, ctypes.POINTER(FdSearchJob), _u64, _i32]),
     "rsg_set_kernel_timing": (_st, [_vp, _i32]),
     "rsg_kernel_times": (_st, [_vp, ctypes.POINTER(ctypes.c_double), _i32]),
     "rsg_encode_tokens": (_st, [_vp, _u64, ctypes.POINTER(SumHead), ctypes.POINTER(Match), _u64,

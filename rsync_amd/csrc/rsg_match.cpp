@@ -1268,9 +1268,128 @@ rsg_status search_fd(rsg_ctx *ctx, int32_t fd, int64_t off0, uint64_t size, cons
     return RSG_OK;
 }
 
+// MD4(int32_LE(seed) || bytes [off, off + n) of fd) (match.go:52-53), the
+// bytes read with pread in 1 MiB pieces (hashed while cache-hot).  0, an
+// errno, or -1 for EOF before n bytes.
+int file_sum_fd(int fd, int64_t off, uint64_t n, int32_t seed, uint8_t out[16], std::vector<uint8_t> &buf) {
+    constexpr uint64_t kPiece = 1ull << 20;
+    buf.resize(kPiece);
+    Md4 h;
+    h.init();
+    const uint8_t sb[4] = {(uint8_t)seed, (uint8_t)(seed >> 8), (uint8_t)(seed >> 16), (uint8_t)(seed >> 24)};
+    h.update(sb, 4);
+    for (uint64_t o = 0; o < n;) {
+        const uint64_t m = std::min(kPiece, n - o);
+        uint64_t got = 0;
+        while (got < m) {
+            const ssize_t r = pread(fd, buf.data() + got, (size_t)(m - got), (off_t)(off + (int64_t)(o + got)));
+            if (r < 0 && errno == EINTR) continue;
+            if (r <= 0) return r < 0 ? errno : -1;
+            got += (uint64_t)r;
+        }
+        h.update(buf.data(), m);
+        o += m;
+    }
+    h.final(out);
+    return 0;
+}
+
+// Host threads for the whole-file sums of a batch (RSG_SUM_THREADS, default
+// 10): one serial MD4 chain per file, so files hash side by side.
+int sum_threads() {  // read per call (one getenv per batch)
+    const char *e = getenv("RSG_SUM_THREADS");
+    const int v = e ? atoi(e) : 10;
+    return std::max(1, std::min(v, 64));
+}
+
 }  // namespace
 
 extern "C" {
+
+rsg_status rsg_hash_search_fd_batch(rsg_ctx *ctx, rsg_fd_search_job *jobs, uint64_t njobs, int32_t seed) {
+    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    RSG_HIP(ctx, hipSetDevice(ctx->device));
+    if (njobs && !jobs) return fail(ctx, RSG_ERR_INVALID, "NULL jobs");
+    std::vector<std::string> msg(njobs);
+    for (uint64_t i = 0; i < njobs; i++) {
+        rsg_fd_search_job &j = jobs[i];
+        j.n_matches = 0;
+        j.status = check_args(ctx, &j.head, j.sum1, j.sum2, j.targets, j.matches, j.match_cap, &j.n_matches);
+        if (j.status == RSG_OK && (j.offset < 0 || j.src_len > (uint64_t)INT64_MAX))
+            j.status = fail(ctx, RSG_ERR_INVALID, "bad offset / length");
+        if (j.status == RSG_OK && j.src_len && j.fd < 0) j.status = fail(ctx, RSG_ERR_INVALID, "bad descriptor");
+        if (j.status != RSG_OK) msg[i] = ctx->err;
+    }
+    // the whole-file sums, longest file first, on their own threads for the
+    // whole call (sendFile hashes beside its reads too, sender.go:184-206)
+    std::vector<uint64_t> order;
+    for (uint64_t i = 0; i < njobs; i++)
+        if (jobs[i].status == RSG_OK && jobs[i].file_sum) order.push_back(i);
+    std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return jobs[a].src_len > jobs[b].src_len; });
+    std::vector<int> sum_code(njobs, 0);
+    std::atomic<uint64_t> next{0};
+    std::vector<std::thread> pool;
+    const int nt = (int)std::min<uint64_t>(order.size(), (uint64_t)sum_threads());
+    for (int t = 0; t < nt; t++)
+        pool.emplace_back([&] {
+            std::vector<uint8_t> buf;
+            for (uint64_t k; (k = next.fetch_add(1)) < order.size();) {
+                rsg_fd_search_job &j = jobs[order[k]];
+                sum_code[order[k]] = file_sum_fd(j.fd, j.offset, j.src_len, seed, j.file_sum, buf);
+            }
+        });
+    struct Join {
+        std::vector<std::thread> &p;
+        ~Join() {
+            for (auto &t : p)
+                if (t.joinable()) t.join();
+        }
+    } join_guard{pool};
+    // the searches, in job order, on this thread (each as rsg_hash_search_fd)
+    rsg_status fatal = RSG_OK;
+    std::string fatal_msg;
+    for (uint64_t i = 0; i < njobs && fatal == RSG_OK; i++) {
+        rsg_fd_search_job &j = jobs[i];
+        if (j.status != RSG_OK || j.head.count == 0 || j.src_len == 0) continue;  // sendFile path: the sum only
+        std::vector<rsg_match> out;
+        rsg_status st = search_fd(ctx, j.fd, j.offset, j.src_len, &j.head, j.sum1, j.sum2, j.targets, seed, out, nullptr);
+        if (st == RSG_OK) {
+            j.n_matches = out.size();
+            if (out.size() > j.match_cap)
+                st = fail(ctx, RSG_ERR_TRUNCATED, "%llu matches, capacity %llu", (unsigned long long)out.size(),
+                          (unsigned long long)j.match_cap);
+            else if (!out.empty())
+                memcpy(j.matches, out.data(), out.size() * sizeof(rsg_match));
+        }
+        if (st != RSG_OK) {
+            if (job_local(st) || st == RSG_ERR_IO) {
+                j.status = st;
+                msg[i] = ctx->err;
+            } else {
+                fatal = st;
+                fatal_msg = ctx->err;
+            }
+        }
+    }
+    for (auto &t : pool) t.join();
+    if (fatal != RSG_OK) {
+        for (uint64_t i = 0; i < njobs; i++)
+            if (jobs[i].status == RSG_OK) jobs[i].status = fatal, msg[i] = fatal_msg;
+    }
+    for (uint64_t i = 0; i < njobs; i++) {
+        if (jobs[i].status != RSG_OK || sum_code[i] == 0) continue;
+        jobs[i].status = RSG_ERR_IO;  // fileio.go:99-104
+        msg[i] = sum_code[i] == -1 ? std::string("file has changed mid-transfer")
+                                   : std::string("file has changed mid-transfer: ") + strerror(sum_code[i]);
+    }
+    for (uint64_t i = 0; i < njobs; i++)
+        if (jobs[i].status != RSG_OK) {
+            ctx->err = msg[i];
+            return jobs[i].status;
+        }
+    return RSG_OK;
+}
 
 rsg_status rsg_set_kernel_timing(rsg_ctx *ctx, int32_t on) {
     if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");

@@ -459,6 +459,45 @@ class Engine:
         m = _matches_list(out, nm.value)
         return (m, dig.tobytes()) if file_sum else m
 
+    def hash_search_fd_batch(self, jobs, seed: int, file_sums: bool = True, raise_on_error: bool = True):
+        """SendFiles' loop over sources that are open files
+        (rsg_hash_search_fd_batch): jobs = [(fd, src_len, head, sum1, sum2,
+        targets)] or with a 7th item, the offset in fd.  Each source is
+        searched as hash_search_fd would, in job order, while the whole-file
+        sums MD4(int32_LE(seed) || source) of several files run on host
+        threads side by side.  -> [(matches, file_sum or None)], or with
+        raise_on_error=False [(status, matches, file_sum)]."""
+        n = len(jobs)
+        arr = (_lib.FdSearchJob * max(n, 1))()
+        keep, outs, sums = [], [], []
+        for k, job in enumerate(jobs):
+            fd, src_len, head, sum1, sum2, targets = job[:6]
+            j = arr[k]
+            j.fd, j.src_len, j.offset = fd, src_len, (job[6] if len(job) > 6 else 0)
+            j.head = head if isinstance(head, SumHead) else SumHead(*head)
+            s1 = np.ascontiguousarray(sum1, dtype=np.uint32)
+            s2 = np.ascontiguousarray(sum2, dtype=np.uint8).reshape(-1)
+            tg = np.ascontiguousarray(targets, dtype=np.int32)
+            keep += [s1, s2, tg]
+            j.sum1, j.sum2, j.targets = _ptr(s1).value, _ptr(s2).value, _ptr(tg).value
+            cap = src_len // max(j.head.block_len, 1) + 2
+            out = np.empty(cap, dtype=_MATCH_DT)
+            outs.append(out)
+            j.matches, j.match_cap = ctypes.cast(out.ctypes.data, ctypes.POINTER(Match)), cap
+            dig = np.zeros(16, np.uint8)
+            sums.append(dig)
+            j.file_sum = _ptr(dig).value if file_sums else None
+        st = lib.rsg_hash_search_fd_batch(self.ctx, arr, n, _i32(seed))
+
+        def res(k):
+            m = outs[k][: arr[k].n_matches]
+            return _matches_list(m, len(m))
+        if raise_on_error:
+            check(st, self.ctx)
+            return [(res(k), sums[k].tobytes() if file_sums else None) for k in range(n)]
+        return [(arr[k].status, res(k) if arr[k].status == _lib.OK else [],
+                 sums[k].tobytes() if file_sums and arr[k].status == _lib.OK else None) for k in range(n)]
+
     def hash_search_batch(self, jobs, seed: int, device: bool = True, raise_on_error: bool = True,
                           as_arrays: bool = False):
         """SendFiles' per-file hashSearch loop (sender.go:19-115) in one

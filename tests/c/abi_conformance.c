@@ -4,7 +4,7 @@
  * A cgo binding (go/rsyncgpu) sees the structs of rsg.h with
  * the C compiler's layout, so this program pins that layout for every struct
  * a caller fills or reads -- rsg_sum_head, rsg_file, rsg_match,
- * rsg_search_job, rsg_fd_file, rsg_shard_batch, rsg_recv_job --
+ * rsg_search_job, rsg_fd_search_job, rsg_fd_file, rsg_shard_batch, rsg_recv_job --
  * at compile time (_Static_assert) and prints
  * it as JSON for tests/test_c_abi.py to compare with the ctypes mirror.
  *
@@ -61,6 +61,21 @@ PIN(rsg_search_job, match_cap, 64);
 PIN(rsg_search_job, n_matches, 72);
 PIN(rsg_search_job, status, 80);
 PIN(rsg_search_job, reserved, 84);
+SIZE(rsg_fd_search_job, 104);
+PIN(rsg_fd_search_job, fd, 0);
+PIN(rsg_fd_search_job, reserved, 4);
+PIN(rsg_fd_search_job, offset, 8);
+PIN(rsg_fd_search_job, src_len, 16);
+PIN(rsg_fd_search_job, head, 24);
+PIN(rsg_fd_search_job, sum1, 40);
+PIN(rsg_fd_search_job, sum2, 48);
+PIN(rsg_fd_search_job, targets, 56);
+PIN(rsg_fd_search_job, matches, 64);
+PIN(rsg_fd_search_job, match_cap, 72);
+PIN(rsg_fd_search_job, n_matches, 80);
+PIN(rsg_fd_search_job, file_sum, 88);
+PIN(rsg_fd_search_job, status, 96);
+PIN(rsg_fd_search_job, reserved2, 100);
 SIZE(rsg_fd_file, 32);
 PIN(rsg_fd_file, fd, 0);
 PIN(rsg_fd_file, idx, 4);
@@ -127,6 +142,14 @@ static void layout(void) {
     F(rsg_search_job, targets); printf(", "); F(rsg_search_job, matches); printf(", ");
     F(rsg_search_job, match_cap); printf(", "); F(rsg_search_job, n_matches); printf(", ");
     F(rsg_search_job, status); printf(", "); F(rsg_search_job, reserved); printf("},\n");
+    printf(" \"rsg_fd_search_job\": {\"size\": %zu, ", sizeof(rsg_fd_search_job));
+    F(rsg_fd_search_job, fd); printf(", "); F(rsg_fd_search_job, reserved); printf(", ");
+    F(rsg_fd_search_job, offset); printf(", "); F(rsg_fd_search_job, src_len); printf(", ");
+    F(rsg_fd_search_job, head); printf(", "); F(rsg_fd_search_job, sum1); printf(", ");
+    F(rsg_fd_search_job, sum2); printf(", "); F(rsg_fd_search_job, targets); printf(", ");
+    F(rsg_fd_search_job, matches); printf(", "); F(rsg_fd_search_job, match_cap); printf(", ");
+    F(rsg_fd_search_job, n_matches); printf(", "); F(rsg_fd_search_job, file_sum); printf(", ");
+    F(rsg_fd_search_job, status); printf(", "); F(rsg_fd_search_job, reserved2); printf("},\n");
     printf(" \"rsg_fd_file\": {\"size\": %zu, ", sizeof(rsg_fd_file));
     F(rsg_fd_file, fd); printf(", "); F(rsg_fd_file, idx); printf(", "); F(rsg_fd_file, offset); printf(", ");
     F(rsg_fd_file, len); printf(", "); F(rsg_fd_file, block_len); printf(", "); F(rsg_fd_file, reserved);

@@ -112,3 +112,38 @@ def match_cases():
     b = splitmix64_bytes(119, 200_000)
     c["identical_sqrt"] = (b.copy(), b, 0, SEED)
     return c
+
+
+def make_cfg3_file(eng, basis, src, size, seed, B, rng):
+    """Source = the basis with random runs (1 B .. 2B long) overwritten until
+    ~50% of the bytes differ, plus a few insertions/deletions so matches fall at
+    offsets that are not multiples of B.  Built on the
+    device with splitmix64 fills and device copies; returns the source length."""
+    import rsync_amd
+    from rsync_amd import _lib
+    eng.fill_splitmix64(basis, size, seed)
+    # shifts: copy basis pieces with small gaps/overlaps into src
+    cuts = sorted(rng.choice(np.arange(1, size - 1), 8, replace=False).tolist())
+    pos_src, prev = 0, 0
+    for i, c in enumerate(cuts + [size]):
+        n = max(0, c - prev)
+        _lib.check(_lib.lib.rsg_memcpy_d2d(eng.ctx, rsync_amd.engine.ctypes.c_void_p(src.ptr + pos_src),
+                                            rsync_amd.engine.ctypes.c_void_p(basis.ptr + prev), n), eng.ctx)
+        pos_src += n
+        if i % 2 == 0 and c < size:  # insertion of random bytes
+            k = int(rng.integers(1, 64))
+            eng.fill_splitmix64(src, k, seed * 7919 + i, offset=pos_src)
+            pos_src += k
+        elif c < size:  # deletion
+            prev = c + int(rng.integers(1, 64))
+            continue
+        prev = c
+    total = pos_src
+    touched, run_seed = 0, 1
+    while touched < total // 2:
+        ln = int(rng.integers(1, 2 * B))
+        at = int(rng.integers(0, total - ln))
+        eng.fill_splitmix64(src, ln, seed * 104729 + run_seed, offset=at)
+        run_seed += 1
+        touched += ln
+    return total

@@ -31,7 +31,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(_lib.lib, s), s
     assert set(syms) == set(_lib.EXPORTED)
-    assert _lib.lib.rsg_abi_version() == _lib.ABI_VERSION == 2
+    assert _lib.lib.rsg_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_no_device_fails_loudly():

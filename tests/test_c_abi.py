@@ -47,7 +47,8 @@ def test_layout_matches_ctypes_mirror():
     assert c["record_bytes"] == _lib.RECORD_BYTES
     assert c["chunk_size"] == _lib.CHUNK_SIZE
     for name, cls in (("rsg_sum_head", _lib.SumHead), ("rsg_file", _lib.File), ("rsg_match", _lib.Match),
-                      ("rsg_search_job", _lib.SearchJob), ("rsg_fd_file", _lib.FdFile),
+                      ("rsg_search_job", _lib.SearchJob), ("rsg_fd_search_job", _lib.FdSearchJob),
+                      ("rsg_fd_file", _lib.FdFile),
                       ("rsg_shard_batch", _lib.ShardBatch), ("rsg_recv_job", _lib.RecvJob),
                       ("rsg_piece", _lib.Piece), ("rsg_shard_rank", _lib.ShardRank)):
         assert c[name] == _ctypes_layout(cls), name

@@ -302,3 +302,35 @@ def test_release_arenas(eng):
     for a, _, _ in _ARENAS.values():
         a.free()
     _ARENAS.clear()
+
+
+def test_cfg3_real_size_vs_oracle(eng):
+    """BASELINE cfg3 at its real size, one file: a 1 GiB basis and a source
+    with ~50 % of its bytes overwritten plus insertions and deletions (the
+    bench's recipe, tests/cases.make_cfg3_file), B = SumSizesSqroot(1 GiB) =
+    32 768.  The basis sums come from the oracle (and equal the kernel's), and
+    the batched device search -- the bench's call -- returns exactly the
+    oracle's hashSearch match list (~7 s of oracle time)."""
+    import rsync_amd
+    size = 1 << 30
+    rng = np.random.default_rng(3)
+    basis = eng.alloc(size)
+    src = eng.alloc(size + 4096)
+    n = cases.make_cfg3_file(eng, basis, src, size, 3, 32768, rng)
+    eng.synchronize()
+    bh = basis.download(size)
+    head = orc.sum_head(size, 0)
+    assert head[1] == 32768
+    rec = orc.block_sums(bh, 0, cases.SEED)
+    recs, total = eng.block_sums_device(basis, [(0, size, 0)], cases.SEED)
+    assert recs.download(total * 20).tobytes() == rec
+    recs.free()
+    s1, s2 = orc.parse_records(rec)
+    tg = orc.stable_targets(s1)
+    got = eng.hash_search_batch([(src, n, head, s1, s2, tg)], cases.SEED)[0]
+    sh = src.download(n)
+    want, _, _ = orc.hash_search(sh, head, s1, s2, tg, cases.SEED)
+    assert len(want) > 10_000
+    assert got == want
+    basis.free()
+    src.free()

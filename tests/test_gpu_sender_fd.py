@@ -130,3 +130,83 @@ def test_offset_into_descriptor(eng, tmp_path):
         os.close(fd)
     want, _, _ = orc.hash_search(src, head, s1, s2, tg, cases.SEED)
     assert got == want and dig == orc.file_sum(1, cases.SEED, src)
+
+
+@pytest.mark.parametrize("sum_threads", ["1", "4"])
+def test_fd_batch_many_files(eng, tmp_path, sum_threads):
+    """rsg_hash_search_fd_batch (SendFiles' loop over open files): every job's
+    matches equal the oracle's hashSearch and every whole-file sum its
+    MD4(int32_LE(seed) || source), whatever the number of sum threads; jobs
+    of several block lengths, a sendFile job (count == 0), an empty source, a
+    source at an offset into its descriptor, a file shorter than its stated
+    length (that job alone fails with "file has changed mid-transfer"), a job
+    with bad arguments (that job alone RSG_ERR_INVALID)."""
+    import rsync_amd
+    rng = np.random.default_rng(77)
+    jobs, want, fds = [], [], []
+    try:
+        for k, blen in enumerate([700, 1024, 4097, 32768, 700, 2048]):
+            basis = cases.splitmix64_bytes(900 + k, int(rng.integers(1 << 20, 3 << 20)))
+            src = cases.mutate(basis, blen, 0.5, 1, 2 * blen, n_ins=4, n_del=4)
+            head, s1, s2, tg = _sums(basis, blen, cases.SEED)
+            fd = _file(tmp_path, f"s{k}", src)
+            fds.append(fd)
+            jobs.append((fd, src.size, head, s1, s2, tg))
+            want.append((orc.hash_search(src, head, s1, s2, tg, cases.SEED)[0], orc.file_sum(1, cases.SEED, src)))
+        # sendFile (no sums) and an empty source
+        src = cases.splitmix64_bytes(950, 300_001)
+        fd = _file(tmp_path, "send", src)
+        fds.append(fd)
+        jobs.append((fd, src.size, (0, 0, 0, 0), np.zeros(0, np.uint32), np.zeros((0, 16), np.uint8),
+                     np.zeros(0, np.int32)))
+        want.append(([], orc.file_sum(1, cases.SEED, src)))
+        head, s1, s2, tg = _sums(cases.splitmix64_bytes(951, 5000), 700, cases.SEED)
+        fd = _file(tmp_path, "empty", np.zeros(0, np.uint8))
+        fds.append(fd)
+        jobs.append((fd, 0, head, s1, s2, tg))
+        want.append(([], orc.file_sum(1, cases.SEED, np.zeros(0, np.uint8))))
+        # at an offset into its descriptor
+        basis = cases.splitmix64_bytes(952, 2 << 20)
+        src = cases.mutate(basis, 700, 0.3, 1, 1400)
+        head, s1, s2, tg = _sums(basis, 700, cases.SEED)
+        fd = _file(tmp_path, "off", np.concatenate([np.full(12345, 7, np.uint8), src]))
+        fds.append(fd)
+        jobs.append((fd, src.size, head, s1, s2, tg, 12345))
+        want.append((orc.hash_search(src, head, s1, s2, tg, cases.SEED)[0], orc.file_sum(1, cases.SEED, src)))
+        # short file: the job fails, the others do not
+        basis = cases.splitmix64_bytes(953, 1 << 20)
+        head, s1, s2, tg = _sums(basis, 1024, cases.SEED)
+        fd = _file(tmp_path, "short", basis[:-1000])
+        fds.append(fd)
+        jobs.append((fd, basis.size, head, s1, s2, tg))
+        want.append(None)
+        # bad arguments: targets not a permutation
+        head, s1, s2, tg = _sums(basis, 1024, cases.SEED)
+        fd = _file(tmp_path, "bad", basis)
+        fds.append(fd)
+        jobs.append((fd, basis.size, head, s1, s2, np.zeros_like(tg)))
+        want.append("invalid")
+        old = os.environ.get("RSG_SUM_THREADS")
+        os.environ["RSG_SUM_THREADS"] = sum_threads  # read per call
+        try:
+            got = eng.hash_search_fd_batch(jobs, cases.SEED, raise_on_error=False)
+        finally:
+            if old is None:
+                del os.environ["RSG_SUM_THREADS"]
+            else:
+                os.environ["RSG_SUM_THREADS"] = old
+        for k, ((st, m, dig), w) in enumerate(zip(got, want)):
+            if w is None:
+                assert st == -7, k
+            elif w == "invalid":
+                assert st == -1, k
+            else:
+                assert st == 0, (k, st)
+                assert m == w[0], k
+                assert dig == w[1], k
+        with pytest.raises(rsync_amd.RsgError) as e:
+            eng.hash_search_fd_batch(jobs[:-1], cases.SEED)
+        assert "changed mid-transfer" in str(e.value)
+    finally:
+        for fd in fds:
+            os.close(fd)
