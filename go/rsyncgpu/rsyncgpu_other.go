@@ -108,3 +108,14 @@ func (nd *Node) GenerateFiles(files []*os.File, idx []int32, sizes []int64, seed
 func (e *Engine) HashSearchFile(f *os.File, size int64, head rsync.SumHead, targets []int32, seed int32) ([]Match, [16]byte, error) {
 	return nil, [16]byte{}, ErrUnavailable
 }
+
+type FileJob struct {
+	File    *os.File
+	Size    int64
+	Head    rsync.SumHead
+	Targets []int32
+}
+
+func (e *Engine) HashSearchFiles(jobs []FileJob, seed int32) ([][]Match, [][16]byte, []error, error) {
+	return nil, nil, nil, ErrUnavailable
+}

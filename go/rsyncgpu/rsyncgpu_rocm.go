@@ -643,3 +643,72 @@ func (e *Engine) HashSearchFile(f *os.File, size int64, head rsync.SumHead, targ
 	}
 	return goMatches(ms[:nm]), sum, nil
 }
+
+// FileJob is one source file of SendFiles' loop (sender.go:19-115) that is an
+// open file: its sums have been read (receiveSums, sender.go:51) and its
+// targets built (sender.go:60-83).  Size is the stat'ed size (sendFile's
+// fi.Size()).
+type FileJob struct {
+	File    *os.File
+	Size    int64
+	Head    rsync.SumHead
+	Targets []int32
+}
+
+// HashSearchFiles replaces hashSearch (sender.go:90) for several open files
+// (rsg_hash_search_fd_batch): each file is read and searched in windows as
+// HashSearchFile does, in job order, while the files' whole-file sums
+// MD4(int32_LE(seed) || source) (match.go:52-53), written after each
+// file's matched(size, -1), run on host threads side by side -- one serial
+// MD4 chain per file, several files at once.  A file shorter than its Size
+// fails only its own job ("file has changed mid-transfer", fileio.go:99-104);
+// per-file errors come back in errs, a device failure is the returned error.
+func (e *Engine) HashSearchFiles(jobs []FileJob, seed int32) ([][]Match, [][16]byte, []error, error) {
+	n := len(jobs)
+	if n == 0 {
+		return nil, nil, nil, nil
+	}
+	cj := unsafe.Slice((*C.rsg_fd_search_job)(C.calloc(C.size_t(n), C.sizeof_rsg_fd_search_job)), n)
+	defer C.free(unsafe.Pointer(&cj[0]))
+	csums := unsafe.Slice((*byte)(C.calloc(C.size_t(n), 16)), 16*n)
+	defer C.free(unsafe.Pointer(&csums[0]))
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	raw := make([][]C.rsg_match, n)
+	for i, j := range jobs {
+		capm := int(j.Size)/max(int(j.Head.BlockLength), 1) + 2
+		raw[i] = make([]C.rsg_match, capm)
+		pin.Pin(&raw[i][0])
+		cj[i].matches, cj[i].match_cap = &raw[i][0], C.uint64_t(capm)
+		cj[i].fd = C.int32_t(j.File.Fd())
+		cj[i].src_len = C.uint64_t(j.Size)
+		sum1, sum2 := sums(j.Head)
+		pin.Pin(&sum2[0])
+		cj[i].sum2 = (*C.uint8_t)(unsafe.Pointer(&sum2[0]))
+		if len(sum1) > 0 {
+			pin.Pin(&sum1[0])
+			pin.Pin(&j.Targets[0])
+			cj[i].sum1 = (*C.uint32_t)(unsafe.Pointer(&sum1[0]))
+			cj[i].targets = (*C.int32_t)(unsafe.Pointer(&j.Targets[0]))
+		}
+		cj[i].head = cHead(j.Head)
+		cj[i].file_sum = (*C.uint8_t)(unsafe.Pointer(&csums[16*i]))
+	}
+	st := C.rsg_hash_search_fd_batch(e.ctx, &cj[0], C.uint64_t(n), C.int32_t(seed))
+	runtime.KeepAlive(jobs)
+	out := make([][]Match, n)
+	fsums := make([][16]byte, n)
+	errs := make([]error, n)
+	for i := range cj {
+		if cj[i].status != C.RSG_OK {
+			errs[i] = fmt.Errorf("rsg status %d", int(cj[i].status))
+			continue
+		}
+		out[i] = goMatches(raw[i][:cj[i].n_matches])
+		copy(fsums[i][:], csums[16*i:16*i+16])
+	}
+	if st != C.RSG_OK && st != C.RSG_ERR_INVALID && st != C.RSG_ERR_TRUNCATED && st != C.RSG_ERR_IO {
+		return out, fsums, errs, e.err(st)
+	}
+	return out, fsums, errs, nil
+}
