@@ -69,9 +69,10 @@ def parse():
     ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5", "filesums", "receive"],
                     help="cfg2 = receiver block sums (the metric); cfg3 = sender match, reported separately")
     ap.add_argument("--cfg3-files", type=int, default=10)
-    ap.add_argument("--batches", type=int, default=4,
+    ap.add_argument("--batches", type=int, default=None,
                     help="batches per rank for the pipelined delivery modes (records of batch b move while "
-                         "batch b+1 is hashed)")
+                         "batch b+1 is hashed); default 4, or 1 at N = 1, where the root's records are "
+                         "written in place and nothing moves for the gather")
     ap.add_argument("--delivery-steps", type=int, default=20, help="timed steps of each delivery mode")
     return ap.parse_args()
 
@@ -277,7 +278,7 @@ def main():
     # hashing: RCCL gather to rank 0, and every rank's own D2H
     if not args.no_delivery:
         from rsync_amd.dist import ShardedBlockSums
-        nb = max(1, args.batches)
+        nb = max(1, args.batches if args.batches is not None else (1 if world == 1 else 4))
         per = -(-n // nb)
         groups = [list(range(g * per, min(n, (g + 1) * per))) for g in range(nb)]
         groups = [g for g in groups if g]
@@ -755,7 +756,8 @@ def bench_mixed(args, rank, world, local):
     from rsync_amd.dist import ShardedBlockSums, rank_arena, shard_layout
     NF = 100_000
     lengths = np.random.default_rng(4).integers(4096, 65537, NF).tolist()
-    lay = shard_layout(lengths, world, max(1, args.batches), BLOCK_LEN)
+    lay = shard_layout(lengths, world, max(1, args.batches if args.batches is not None else (1 if world == 1 else 4)),
+                       BLOCK_LEN)
     eng = rsync_amd.Engine(local)
     stream = torch.cuda.Stream(device=local)
     sptr = stream.cuda_stream

@@ -428,8 +428,10 @@ rsg_status rsg_gatherv_bytes(rsg_ctx *ctx, const void *d_send, const uint64_t *s
  *     bytes of batch b (send_bytes[q], nranks entries, equal on all ranks)
  *     land at d_recv + recv_offsets[q] on the root, so the root's buffer ends
  *     up in global record order (GenerateFiles' file-list order,
- *     generator.go:20-52).  Collective: every rank calls it with the same
- *     nbatch; a rank with no blocks in batch b passes plan = NULL.
+ *     generator.go:20-52).  The root's own kernels write its records
+ *     straight to their landing offsets in d_recv (no self copy; its
+ *     d_records is not written).  Collective: every rank calls it with the
+ *     same nbatch; a rank with no blocks in batch b passes plan = NULL.
  *   rsg_block_sums_d2h: copied to h_records + 20 * record_offset on the
  *     host (ranks do this concurrently over their own PCIe links: the
  *     alternative to gather-then-one-D2H).  Pinned h_records runs at DMA speed.

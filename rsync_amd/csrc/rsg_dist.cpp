@@ -24,15 +24,19 @@ namespace rsgh {
 // Root receives send_bytes[q] bytes from every rank q at recv_off[q] (or the
 // exclusive prefix of send_bytes when recv_off is NULL); grouped
 // ncclSend/ncclRecv, since the sizes are ragged (ncclGather is not).
+// in_place: the root's own bytes are already at d_recv + recv_off[root] (its
+// kernel wrote them there), so there is no self copy.
 rsg_status gatherv(rsg_ctx *ctx, const void *d_send, const uint64_t *send_bytes, void *d_recv,
-                   const uint64_t *recv_off, int32_t root, hipStream_t st) {
+                   const uint64_t *recv_off, int32_t root, hipStream_t st, bool in_place) {
     ncclResult_t r = ncclGroupStart();
     if (ctx->rank == root) {
         uint64_t off = 0;
         for (int q = 0; q < ctx->nranks; q++) {
             uint8_t *dst = (uint8_t *)d_recv + (recv_off ? recv_off[q] : off);
             if (send_bytes[q]) {
-                if (q == root) {
+                if (q == root && in_place) {
+                    // already there
+                } else if (q == root) {
                     const hipError_t e = hipMemcpyAsync(dst, d_send, send_bytes[q], hipMemcpyDeviceToDevice, st);
                     if (e != hipSuccess) {
                         ncclGroupEnd();
@@ -68,9 +72,10 @@ struct Events {  // one per batch, destroyed on every exit
 // Shared driver of the two modes: kernel(b) on ctx->stream, then `move(b)`
 // queued on ctx->side[0] behind an event of kernel(b).  Waits for both
 // streams on every exit (nothing outlives the call).
-template <class Move>
+// out(b, sb): where batch b's records are written.
+template <class Out, class Move>
 rsg_status pipeline(rsg_ctx *ctx, const rsg_shard_batch *batches, uint64_t nbatch, const void *d_arena, int32_t seed,
-                    void *d_records, Move move) {
+                    Out out, Move move) {
     struct Drain {
         rsg_ctx *c;
         ~Drain() {
@@ -86,8 +91,7 @@ rsg_status pipeline(rsg_ctx *ctx, const rsg_shard_batch *batches, uint64_t nbatc
             if (sb.plan->ctx != ctx) return fail(ctx, RSG_ERR_INVALID, "batch %llu: plan of another context",
                                                  (unsigned long long)b);
             const rsg_status s = launch_plan(ctx, sb.plan->host, sb.plan->d_files, sb.plan->d_wg, d_arena, seed,
-                                             (uint8_t *)d_records + sb.record_offset * rsg::kRecordBytes,
-                                             sb.plan->d_scratch, ctx->stream);
+                                             out(b, sb), sb.plan->d_scratch, ctx->stream);
             if (s != RSG_OK) return s;
         }
         RSG_HIP(ctx, hipEventCreateWithFlags(&evs.ev[b], hipEventDisableTiming));
@@ -146,7 +150,8 @@ rsg_status rsg_gatherv_bytes(rsg_ctx *ctx, const void *d_send, const uint64_t *s
     RSG_HIP(ctx, hipSetDevice(ctx->device));
     if (!ctx->comm) return fail(ctx, RSG_ERR_INVALID, "rsg_comm_init not called");
     if (!send_bytes || root < 0 || root >= ctx->nranks) return fail(ctx, RSG_ERR_INVALID, "bad gather arguments");
-    return gatherv(ctx, d_send, send_bytes, d_recv, recv_offsets, root, stream ? (hipStream_t)stream : ctx->stream);
+    return gatherv(ctx, d_send, send_bytes, d_recv, recv_offsets, root, stream ? (hipStream_t)stream : ctx->stream,
+                   false);
 }
 
 rsg_status rsg_block_sums_gather(rsg_ctx *ctx, const rsg_shard_batch *batches, uint64_t nbatch, const void *d_arena,
@@ -165,9 +170,16 @@ rsg_status rsg_block_sums_gather(rsg_ctx *ctx, const rsg_shard_batch *batches, u
                         (unsigned long long)plan_records(batches[b]));
     }
     if (ctx->rank == root && !d_recv) return fail(ctx, RSG_ERR_INVALID, "root needs d_recv");
-    return pipeline(ctx, batches, nbatch, d_arena, seed, d_records, [&](uint64_t, const rsg_shard_batch &sb) {
+    // the root's kernels write its own records straight to their landing
+    // offsets in d_recv: no self copy (at N = 1 nothing moves at all)
+    const bool is_root = ctx->rank == root;
+    auto out = [&](uint64_t, const rsg_shard_batch &sb) -> uint8_t * {
+        return is_root ? (uint8_t *)d_recv + sb.recv_offsets[ctx->rank]
+                    : (uint8_t *)d_records + sb.record_offset * rsg::kRecordBytes;
+    };
+    return pipeline(ctx, batches, nbatch, d_arena, seed, out, [&](uint64_t, const rsg_shard_batch &sb) {
         return gatherv(ctx, (const uint8_t *)d_records + sb.record_offset * rsg::kRecordBytes, sb.send_bytes, d_recv,
-                       sb.recv_offsets, root, ctx->side[0]);
+                       sb.recv_offsets, root, ctx->side[0], true);
     });
 }
 
@@ -177,7 +189,10 @@ rsg_status rsg_block_sums_d2h(rsg_ctx *ctx, const rsg_shard_batch *batches, uint
     std::lock_guard<std::recursive_mutex> lock(ctx->mu);
     RSG_HIP(ctx, hipSetDevice(ctx->device));
     if ((nbatch && !batches) || !h_records) return fail(ctx, RSG_ERR_INVALID, "bad arguments");
-    return pipeline(ctx, batches, nbatch, d_arena, seed, d_records,
+    auto out = [&](uint64_t, const rsg_shard_batch &sb) -> uint8_t * {
+        return (uint8_t *)d_records + sb.record_offset * rsg::kRecordBytes;
+    };
+    return pipeline(ctx, batches, nbatch, d_arena, seed, out,
                     [&](uint64_t, const rsg_shard_batch &sb) -> rsg_status {
                         const uint64_t n = plan_records(sb) * rsg::kRecordBytes;
                         if (n)

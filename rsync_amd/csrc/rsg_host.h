@@ -156,8 +156,9 @@ rsg_status generate_files_fd_impl(rsg_ctx *ctx, const rsg_fd_file *files, uint64
 // Ragged RCCL gather of one rank's bytes to the root (rsg_dist.cpp): root
 // receives send_bytes[q] from rank q at recv_off[q] (NULL: exclusive prefix).
 // Grouped sends/receives; may be nested inside the caller's ncclGroupStart.
+// in_place: the root's own bytes already sit at d_recv + recv_off[root].
 rsg_status gatherv(rsg_ctx *ctx, const void *d_send, const uint64_t *send_bytes, void *d_recv,
-                   const uint64_t *recv_off, int32_t root, hipStream_t st);
+                   const uint64_t *recv_off, int32_t root, hipStream_t st, bool in_place);
 
 // MD4 on the host (rsg_md4_host.cpp): whole-file sums whose serial chain
 // streams through host memory (the sender's h, match.go:52-53; receiveData's

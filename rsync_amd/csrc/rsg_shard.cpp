@@ -146,8 +146,9 @@ rsg_status check_ctxs(rsg_ctx *const *ctxs, int32_t n, std::vector<rsg_ctx *> &o
 // The device-resident step over many contexts: batch b's kernel on every
 // rank's stream, then `move(q, b)` queued on the rank's side[0] stream behind
 // an event of that kernel (every rank's move of batch b issued together).
-template <class Move>
-rsg_status multi_pipeline(const rsg_shard_rank *ranks, int32_t n, int32_t seed, Move move) {
+// out(q, sb): where rank q writes batch sb's records.
+template <class Out, class Move>
+rsg_status multi_pipeline(const rsg_shard_rank *ranks, int32_t n, int32_t seed, Out out, Move move) {
     std::vector<rsg_ctx *> given((size_t)n), cs;
     for (int q = 0; q < n; q++) given[(size_t)q] = ranks[q].ctx;
     rsg_status s = check_ctxs(given.data(), n, cs);
@@ -189,8 +190,7 @@ rsg_status multi_pipeline(const rsg_shard_rank *ranks, int32_t n, int32_t seed, 
             const rsg_shard_batch &sb = ranks[q].batches[b];
             if (sb.plan) {
                 s = launch_plan(ctx, sb.plan->host, sb.plan->d_files, sb.plan->d_wg, ranks[q].d_arena, seed,
-                                (uint8_t *)ranks[q].d_records + sb.record_offset * kRecordBytes, sb.plan->d_scratch,
-                                ctx->stream);
+                                out(q, sb), sb.plan->d_scratch, ctx->stream);
                 if (s != RSG_OK) return fail(c0, s, "rank %d: %s", q, ctx->err.c_str());
             }
             hipEvent_t e = nullptr;
@@ -329,7 +329,12 @@ rsg_status rsg_block_sums_gather_multi(const rsg_shard_rank *ranks, int32_t n, i
                             (unsigned long long)b);
         }
     }
-    return multi_pipeline(ranks, n, seed, [&](std::vector<rsg_ctx *> &cs, uint64_t b) -> rsg_status {
+    // the root's kernels write its records straight to their landing offsets
+    auto out = [&](int q, const rsg_shard_batch &sb) -> uint8_t * {
+        return q == root ? (uint8_t *)d_recv + sb.recv_offsets[q]
+                         : (uint8_t *)ranks[q].d_records + sb.record_offset * kRecordBytes;
+    };
+    return multi_pipeline(ranks, n, seed, out, [&](std::vector<rsg_ctx *> &cs, uint64_t b) -> rsg_status {
         // one thread drives every communicator: their sends and receives go
         // in one group
         ncclResult_t r = ncclGroupStart();
@@ -341,7 +346,7 @@ rsg_status rsg_block_sums_gather_multi(const rsg_shard_rank *ranks, int32_t n, i
             if (hipSetDevice(ctx->device) != hipSuccess) s = fail(cs[0], RSG_ERR_HIP, "hipSetDevice");
             else
                 s = gatherv(ctx, (const uint8_t *)ranks[q].d_records + sb.record_offset * kRecordBytes, sb.send_bytes,
-                            q == root ? d_recv : nullptr, sb.recv_offsets, root, ctx->side[0]);
+                            q == root ? d_recv : nullptr, sb.recv_offsets, root, ctx->side[0], true);
             if (s != RSG_OK && ctx != cs[0]) s = fail(cs[0], s, "rank %d: %s", q, ctx->err.c_str());
         }
         r = ncclGroupEnd();
@@ -353,7 +358,10 @@ rsg_status rsg_block_sums_gather_multi(const rsg_shard_rank *ranks, int32_t n, i
 rsg_status rsg_block_sums_d2h_multi(const rsg_shard_rank *ranks, int32_t n, int32_t seed, uint8_t *h_records) {
     if (!ranks || n < 1) return fail(nullptr, RSG_ERR_INVALID, "need n >= 1 ranks");
     if (!h_records) return fail(ranks[0].ctx, RSG_ERR_INVALID, "h_records is NULL");
-    return multi_pipeline(ranks, n, seed, [&](std::vector<rsg_ctx *> &cs, uint64_t b) -> rsg_status {
+    auto out = [&](int q, const rsg_shard_batch &sb) -> uint8_t * {
+        return (uint8_t *)ranks[q].d_records + sb.record_offset * kRecordBytes;
+    };
+    return multi_pipeline(ranks, n, seed, out, [&](std::vector<rsg_ctx *> &cs, uint64_t b) -> rsg_status {
         for (int q = 0; q < n; q++) {
             rsg_ctx *ctx = cs[(size_t)q];
             const rsg_shard_batch &sb = ranks[q].batches[b];

@@ -185,7 +185,7 @@ def test_sharded_generator_two_ranks_on_gpu():
 @pytest.mark.parametrize("nbatch", [1, 3])
 def test_pipelined_gather_and_d2h_one_rank(nbatch):
     """rsg_block_sums_gather (RCCL communicator of one rank: the root's own
-    batches land by the self copy at their recv offsets) and
+    batches are written by its kernels straight to their recv offsets) and
     rsg_block_sums_d2h, each pipelined over `nbatch` batches: both deliver
     exactly the single-call records."""
     import rsync_amd
