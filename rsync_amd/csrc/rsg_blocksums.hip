@@ -526,7 +526,7 @@ __device__ __forceinline__ uint32_t park_quad_offset(uint32_t idx) {
 // requested as park requests it (quad u of block j at 700 j + 16 u, the pad
 // quad not requested).
 template <int NW, int PER, int DEPTH, int PAT = 0>
-__global__ __launch_bounds__(64 * NW) void diag_stream_read(const uint8_t *__restrict__ arena, uint64_t bytes,
+__global__ __launch_bounds__(512) void diag_stream_read(const uint8_t *__restrict__ arena, uint64_t bytes,
                                                            uint32_t *__restrict__ sink) {
     static_assert(PER * DEPTH <= 63 && PER <= 64, "vmcnt cap");
     static_assert(PAT == 0 || PER == 45, "park tiles are 45 requests");

@@ -28,6 +28,10 @@ SHAPES = [  # (files, file bytes, block length, arenas)
     (256, 4 << 20, 4096, 2),      # 4 KiB blocks
     (1, 32 << 30, 131072, 1),     # cfg5's per-GPU share: one 32 GiB file
     (512, 2 << 20, 2048, 2),      # 2 MiB files (B = 2048)
+    (256, 4 << 20, 4160, 2),      # 5-7: B = 4096 +- 64 (is the 4 KiB stride itself the cost?)
+    (256, 4 << 20, 4032, 2),
+    (256, 4 << 20, 4112, 2),
+    (1, 1 << 30, 32768, 2),       # 8: one 1 GiB file at the reference's sizing (B = sqrt(len) = 32768)
 ]
 VARIANTS = {1: "staged", 4: "staged_seg128", 5: "staged_seg512", 2: "park", 3: "long_deep_prefetch"}
 DIAGS = {1: "diag_staged_memory_only", 2: "diag_staged_hash_only", 6: "diag_linear_read_ldsdma"}
