@@ -189,6 +189,7 @@ def main():
         res = {v: [] for v in names}
         for _ in range(int(os.environ.get("AB_ROUNDS", "5"))):
             for v in names:
+                print(f"ab: {names[v]}", file=sys.stderr, flush=True)
                 eng.set_block_sums_kernel(v[0])
                 eng.set_block_sums_diagnostic(v[1])
                 for i in range(3):
