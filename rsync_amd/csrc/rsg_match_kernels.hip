@@ -748,11 +748,14 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         __syncthreads();
     }
     uint32_t O[OW], A[OW + 4], On[OW];
-    uint32_t Cx[OW];                   // BT: the previous tile's xor-ed shifted bytes = this tile's outgoing ones
-    int32_t c1 = 0, c2 = 0, c1a = 0, c2a = 0;  // BT: and their sums (vec_sums)
+    // BT: the previous tile's shifted bytes = this tile's outgoing ones, kept
+    // as the pair step's operands (xor-ed, the two streams' bytes in 16-bit
+    // halves: the v_perm of the step that shifted them in), and their sums
+    u16x2 Uo[BT ? H : 1];
+    int32_t c1 = 0, c2 = 0, c1a = 0, c2a = 0;
     if constexpr (BT) {
 #pragma unroll
-        for (int k = 0; k < OW; k++) Cx[k] = 0;
+        for (int k = 0; k < H; k++) Uo[k] = u16x2{0, 0};
     }
     auto fetch_shifted = [&](uint32_t tt, uint32_t *a) {  // BT: the next tile's shifted bytes only (sh = 0)
         const uint8_t *pa = src + (uint64_t)tt * kScanTile + lo + B;
@@ -835,9 +838,10 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                 o2 += v2 + 16 * c * v1;
                 o1 += v1;
             }
-            if constexpr (BT) {  // in this (uniform) branch, so Ox = Cx below needs no per-lane select
+            if constexpr (BT) {  // in this (uniform) branch, so the loop's uo = Uo needs no per-lane select
 #pragma unroll
-                for (int k = 0; k < OW; k++) Cx[k] = O[k] ^ 0x80808080u;
+                for (int j = 0; j < H; j++)
+                    Uo[j] = pair_bytes(O[j >> 2] ^ 0x80808080u, O[(j >> 2) + OW / 2] ^ 0x80808080u, j & 3);
             }
         }
         if constexpr (!BT) {
@@ -943,11 +947,13 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
         const uint32_t W2b = W2 + 16u * W1 + 16u * da - (uint32_t)(s2a - o2a) - B * (uint32_t)o1a;
         u16x2 P1 = as_u16x2(((W1 + C128) & 0xffffu) | ((W1b + C128) << 16));
         u16x2 P2 = as_u16x2((W2 & 0xffffu) | (W2b << 16));
-        uint32_t Ox[OW];
+        uint32_t Ox[BT ? 1 : OW];
+        if constexpr (!BT) {
 #pragma unroll
-        for (int k = 0; k < OW; k++) {
-            Ox[k] = BT ? Cx[k] : O[k] ^ 0x80808080u;
-            if constexpr (!BT) Sx[k] = S[k] ^ 0x80808080u;
+            for (int k = 0; k < OW; k++) {
+                Ox[k] = O[k] ^ 0x80808080u;
+                Sx[k] = S[k] ^ 0x80808080u;
+            }
         }
         constexpr int G = 4;  // pair steps per group: 8 filter reads in flight
         uint32_t one16 = 1;  // the SDWA shift count of the filter addresses (a VGPR operand)
@@ -977,10 +983,25 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                     typedef __attribute__((address_space(3))) const uint16_t lds16;
                     wd[jj] = u16x2{*(lds16 *)(uintptr_t)(alo + fb), *(lds16 *)(uintptr_t)(ahi + fb)};
                 }
-                const u16x2 uo = pair_bytes(Ox[j >> 2], Ox[(j >> 2) + OW / 2], j & 3);
-                const u16x2 ui = pair_bytes(Sx[j >> 2], Sx[(j >> 2) + OW / 2], j & 3);
-                P1 = P1 + ui - uo;
-                P2 = P2 + uo * negB + P1;
+                if constexpr (BT) {
+                    // uo's last uses, then ui written over it in place (a tied
+                    // asm operand): the pair carried to the next tile keeps
+                    // its register, no copies at the tile loop's back edge
+                    const u16x2 uo = Uo[j];
+                    P1 = P1 - uo;
+                    P2 = P2 + uo * negB;
+                    uint32_t r = as_u32(uo);
+                    const uint32_t sel = 0x0c000c00u | ((4u + (uint32_t)(j & 3)) << 16) | (uint32_t)(j & 3);
+                    asm("v_perm_b32 %0, %1, %2, %3" : "+v"(r) : "v"(Sx[(j >> 2) + OW / 2]), "v"(Sx[j >> 2]), "s"(sel));
+                    Uo[j] = as_u16x2(r);  // this step's ui: the next tile's outgoing pair
+                    P1 = P1 + Uo[j];
+                    P2 = P2 + P1;
+                } else {
+                    const u16x2 uo = pair_bytes(Ox[j >> 2], Ox[(j >> 2) + OW / 2], j & 3);
+                    const u16x2 ui = pair_bytes(Sx[j >> 2], Sx[(j >> 2) + OW / 2], j & 3);
+                    P1 = P1 + ui - uo;
+                    P2 = P2 + uo * negB + P1;
+                }
             }
             // the group's eight hit masks first, then its parks: each park's
             // branch then tests a mask computed several instructions earlier
@@ -1043,9 +1064,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
             const uint32_t w1 = ((as_u32(P1) >> 16) - C128) & 0xffffu, w2 = as_u32(P2) >> 16;
             carry[parity] = make_uint2(w1, (uint32_t)(q0 + kScanTile + B) * w1 - w2);
         }
-        if constexpr (BT) {  // this tile's shifted bytes are the next tile's outgoing ones
-#pragma unroll
-            for (int k = 0; k < OW; k++) Cx[k] = Sx[k];
+        if constexpr (BT) {  // this tile's shifted bytes are the next tile's outgoing ones (Uo set in the loop)
             c1 = s1; c2 = s2; c1a = s1a; c2a = s2a;
         }
         }  // interior tile
