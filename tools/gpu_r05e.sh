@@ -14,3 +14,5 @@ timeout -k 10 200 python bench.py --workload cfg3 --no-cpu --no-host-path > ${P}
 RSG_LIB_PATH=$PWD/rsync_amd/ab/librsg_base.so timeout -k 10 200 python bench.py --workload cfg3 --no-cpu --no-host-path > ${P}_cfg3_base2.json 2> ${P}_cfg3_base2.err || exit 7
 RSG_CONFIRM_SPEC=0 timeout -k 10 200 python bench.py --workload cfg3 --no-cpu --no-host-path > ${P}_cfg3_nospec2.json 2> ${P}_cfg3_nospec2.err || exit 8
 SWEEP_SHAPES=2,5,6,7,8 timeout -k 10 300 python tools/blocklen_sweep.py > ${P}_sweep.jsonl 2> ${P}_sweep.err || exit 9
+RSG_CONFIRM_CUS=24 timeout -k 10 200 python bench.py --workload cfg3 --no-cpu --no-host-path > ${P}_cfg3_cus24.json 2> ${P}_cfg3_cus24.err || exit 10
+RSG_CONFIRM_CUS=16 timeout -k 10 200 python bench.py --workload cfg3 --no-cpu --no-host-path > ${P}_cfg3_cus16.json 2> ${P}_cfg3_cus16.err || exit 11
