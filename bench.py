@@ -726,17 +726,20 @@ def cfg3_traffic():
         return None
 
 
-def cfg4_traffic(world, records):
-    """Rank 0's HBM bytes per launch from the committed PMC pass (1 GPU only):
-    FETCH_SIZE x 2 (gfx950) + the records written (the WRITE_SIZE pass of that
-    run did not complete, see profiles/r01c_cfg4_pmc_fetch.json)."""
-    if world != 1:
-        return None
+def committed_traffic(key):
+    """HBM bytes per launch of a workload's kernel from the committed rocprofv3
+    PMC passes (FETCH_SIZE x 2 + WRITE_SIZE, profiles/traffic.json, written by
+    tools/summarize_profile.py --traffic-key); not measured in this run."""
     try:
-        t = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
-        return int(t["block_sums_kernel_cfg4_fetch_bytes_per_launch"]) + records * 20
+        return int(json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))[key])
     except Exception:
         return None
+
+
+def cfg4_traffic(world, records):
+    """Rank 0's HBM bytes per launch (1 GPU only: the profile is of one rank's
+    whole set)."""
+    return committed_traffic("block_sums_kernel_cfg4_bytes_per_launch") if world == 1 else None
 
 
 def bench_mixed(args, rank, world, local):
@@ -937,7 +940,8 @@ def bench_long(args, rank, world, local):
                        "parallelism": f"one file per GPU, {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": round(algo / (kernel_ms * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(algo / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(algo / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": committed_traffic("block_sums_kernel_cfg5_bytes_per_launch") if world == 1 else None,
                          "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": int(algo)},
             "sampled_block_parity": {"blocks": len(sample), "equal": parity},
             "cpu_baseline": cpu}), flush=True)
@@ -1026,7 +1030,8 @@ def bench_filesums(args, rank, world, local):
         "modes": res, "spot_parity": {"files": min(k, 256), "equal": parity},
         "roofline": {"bound": "hbm", "kernel": "file_sums_staged<seeded>",
                      "achieved": round(total / (res["seeded"]["kernel_ms"] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": res["seeded"]["kernel_hbm_frac_8tbs"], "traffic": None,
+                     "unit": "GB/s", "frac": res["seeded"]["kernel_hbm_frac_8tbs"],
+                     "traffic": committed_traffic("file_sums_kernel_cfg4set_bytes_per_launch"),
                      "kernel_ms": res["seeded"]["kernel_ms"], "algorithmic_bytes_per_launch": int(total),
                      "note": "value = per call (descriptor staging + lane order + upload + launch + wait); "
                              "roofline = the kernel alone (HIP events)"},

@@ -3,7 +3,7 @@
 # chained so that the first failure (or a hang) ends the call.
 #   tools/gpu_run.sh <tag> <step>...   steps: tests | newtests | smoke | sweep | variants | ab8 | ab |
 #                                             bench | cfg3 | cfg4 | cfg5 | filesums | receive |
-#                                             prof_cfg2 | prof_cfg3
+#                                             prof_cfg2 | prof_cfg3 | prof_cfg4 | prof_cfg5 | prof_filesums
 set -o pipefail
 TAG=$1; shift
 mkdir -p gpurun_out
@@ -26,6 +26,9 @@ for S in "$@"; do
     receive) timeout -k 10 300 python bench.py --workload receive > gpurun_out/${TAG}_receive.json 2> gpurun_out/${TAG}_receive.err || exit 1 ;;
     prof_cfg2) bash tools/profile_kernel.sh ${TAG}_cfg2 block_sums --steps 20 --warmup 5 --no-cpu --no-host-path --no-delivery || exit 1 ;;
     prof_cfg3) PASSES="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE;SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE;FETCH_SIZE" bash tools/profile_kernel.sh ${TAG}_cfg3 roll --workload cfg3 --steps 2 --warmup 1 --cfg3-files 4 --no-cpu --no-host-path || exit 1 ;;
+    prof_cfg4) PASSES="FETCH_SIZE;WRITE_SIZE" bash tools/profile_kernel.sh ${TAG}_cfg4 block_sums --workload cfg4 --steps 20 --no-cpu --no-host-path --no-delivery || exit 1 ;;
+    prof_cfg5) PASSES="FETCH_SIZE;WRITE_SIZE" bash tools/profile_kernel.sh ${TAG}_cfg5 block_sums --workload cfg5 --steps 5 --warmup 2 --no-cpu || exit 1 ;;
+    prof_filesums) PASSES="FETCH_SIZE;WRITE_SIZE" bash tools/profile_kernel.sh ${TAG}_filesums file_sums --workload filesums --no-cpu || exit 1 ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
 done

@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--outdir", default="profiles")
     ap.add_argument("--timed", type=int, default=0,
                     help="the bench's timed launches are the last N dispatches: report their mean too")
+    ap.add_argument("--traffic-key", default=None,
+                    help="also write the HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE) to profiles/traffic.json "
+                         "under this key (cfg4 / cfg5 / filesums lines)")
     ap.add_argument("--roll-cus", type=int, default=224,
                     help="CUs the roll's workgroups occupy (cfg3 batch: all but RSG_CONFIRM_CUS = 32 of 256)")
     a = ap.parse_args()
@@ -73,7 +76,11 @@ def main():
         cur.update(upd)
         json.dump(cur, open(path, "w"), indent=1)
 
-    if "hbm_bytes_per_launch" in out and kernel == "block_sums" and not a.no_traffic:
+    if "hbm_bytes_per_launch" in out and a.traffic_key:
+        merge("traffic.json", {a.traffic_key: out["hbm_bytes_per_launch"]["total"],
+                               a.traffic_key + "_source": f"profiles/{tag}_summary.json: FETCH_SIZE x 2 + WRITE_SIZE "
+                                                         "per launch (rocprofv3 --pmc passes of the bench workload)"})
+    elif "hbm_bytes_per_launch" in out and kernel == "block_sums" and not a.no_traffic:
         merge("traffic.json", {"block_sums_kernel_cfg2_bytes_per_launch": out["hbm_bytes_per_launch"]["total"],
                                "source": f"profiles/{tag}_summary.json"})
     if "roll" in kernel and not a.no_traffic:
