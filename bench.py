@@ -185,7 +185,9 @@ def main():
                  (1, 13): "diag_stream_8w_8k_d1", (1, 14): "diag_stream_8w_16k_d2", (1, 15): "diag_stream_8w_31k_d2",
                  (1, 16): "diag_stream_4w_45k_d1", (1, 17): "diag_park_swap_memory_only", (1, 18): "diag_park_swap",
                  (1, 19): "diag_stream_3w_park_pattern", (1, 20): "diag_park_memory_no_copyout",
-                 (1, 21): "diag_park_memory_no_records", (1, 22): "diag_stream_3w_45k_8wave_wg"}
+                 (1, 21): "diag_park_memory_no_records", (1, 22): "diag_stream_3w_45k_8wave_wg",
+                 (1, 23): "diag_park_rec1_memory_only", (1, 24): "park_rec1_coalesced_records",
+                 (1, 25): "park_rec2_coalesced_nt_records", (1, 26): "diag_park_rec2_memory_only"}
         res = {v: [] for v in names}
         for _ in range(int(os.environ.get("AB_ROUNDS", "5"))):
             for v in names:

@@ -596,6 +596,7 @@ static_assert(kPkTile % 1024 == 0 && kPkPiece % 16 == 0, "tile = whole DMA instr
 
 struct PkShared {
     uint8_t tile[kPkSlots][kPkTile];
+    uint32_t rec[kPkWaves][64 * 5];  // a hasher's 64 records (20 B each), staged for coalesced stores
     uint32_t n[kPkSlots][64];  // block lengths of the slot's tile
     uint32_t full[kPkSlots];
     uint32_t freeq[kPkSlots];
@@ -869,6 +870,39 @@ __device__ __forceinline__ void pk_reg_swap(uint8_t *dst, const uint8_t *arena, 
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// The 64 records of a staged tile (blocks t*64 .. t*64+63: 1280 contiguous
+// bytes of the output) through the hasher's LDS area, so they leave as
+// full 16-byte lanes of 1 KiB runs (64 + 16 quads) instead of 64 lanes each
+// writing 20 bytes at a 20-byte stride: those strided partial-line stores
+// cost the kernel its streaming rate (park memory only with
+// and without its record stores: 0.187 against 0.155 ms per cfg2 launch).
+// REC = 2: the stores are nontemporal (the records are not read again here).
+template <int REC>
+__device__ __forceinline__ void store_tile_records(uint8_t *out, uint64_t t, uint32_t lane, uint32_t *rec, uint32_t n,
+                                                   int32_t s1, uint32_t tw, const uint32_t h[4]) {
+    const uint32_t s2 = n * (uint32_t)s1 - tw;                    // sum (n - i) x_i
+    const uint32_t sum1 = ((uint32_t)s1 & 0xffffu) | (s2 << 16);  // rsyncchecksum.go:50
+    rec[5 * lane + 0] = sum1;
+    rec[5 * lane + 1] = h[0];
+    rec[5 * lane + 2] = h[1];
+    rec[5 * lane + 3] = h[2];
+    rec[5 * lane + 4] = h[3];
+    // other lanes' records are read back: the wave's LDS operations run in
+    // order, so only the compiler must not move the reads above the writes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const u32x4v a = reinterpret_cast<const u32x4v *>(rec)[lane];
+    u32x4a4 *dst = reinterpret_cast<u32x4a4 *>(out + t * (64ull * kRecordBytes));
+    if (REC == 2) __builtin_nontemporal_store(u32x4a4{a.x, a.y, a.z, a.w}, dst + lane);
+    else dst[lane] = u32x4a4{a.x, a.y, a.z, a.w};
+    if (lane < 16) {
+        const u32x4v b = reinterpret_cast<const u32x4v *>(rec)[64 + lane];
+        if (REC == 2) __builtin_nontemporal_store(u32x4a4{b.x, b.y, b.z, b.w}, dst + 64 + lane);
+        else dst[64 + lane] = u32x4a4{b.x, b.y, b.z, b.w};
+    }
+}
+
 // A block of a direct tile: the lane locates and loads it itself.
 __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uint64_t arena_bytes,
                                        const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file,
@@ -920,7 +954,10 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
 // into its VGPRs right after it publishes the current one, so the HBM latency
 // overlaps the slot's hand-off to a hasher, and a freed slot is refilled by
 // 45 ds_write_b128 instead of waiting out a DMA.
-template <int MODE, int NL, int AUX, int PRIO = 0, int LDR = 0>
+// REC: 0 = each lane stores its own 20-byte record (store_record); 1 / 2 =
+// a staged tile's 64 records through LDS as coalesced 16-byte stores
+// (store_tile_records; 2 = nontemporal).
+template <int MODE, int NL, int AUX, int PRIO = 0, int LDR = 0, int REC = 0>
 __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t seed,
@@ -1099,7 +1136,13 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
                     else if (c == nfull) hash_tail<true>(R + 16 * c, 0u, 0u, n, seed, h, s1, tw);
                 }
             }
-            if (MODE != 5 || h[0] == 0x9e3779b9u) store_record(out, g, n, s1, tw, h);
+            if (MODE == 5 && h[0] != 0x9e3779b9u) {
+                // diagnostic: no record stores
+            } else if (REC >= 1) {
+                store_tile_records<REC>(out, t, lane, &sh.rec[wave][0], n, s1, tw, h);
+            } else {
+                store_record(out, g, n, s1, tw, h);
+            }
         } else {
             if (PRIO >= 3) __builtin_amdgcn_s_setprio(0);
             if (lane == 0) {
@@ -1220,6 +1263,19 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                                        files, wg_file, nwg, total_blocks, seed, out);
                 break;
             case 22: hipLaunchKernelGGL((diag_stream_read<3, 45, 1>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 23:
+            case 24:
+            case 25:
+            case 26:
+                if (max_blen <= kRegMaxBytes) {
+                    auto kern = diag == 23   ? block_sums_park<1, kParkLoaders, 2, 3, 0, 1>
+                                : diag == 24 ? block_sums_park<0, kParkLoaders, 2, 3, 0, 1>
+                                : diag == 25 ? block_sums_park<0, kParkLoaders, 2, 3, 0, 2>
+                                             : block_sums_park<1, kParkLoaders, 2, 3, 0, 2>;
+                    hipLaunchKernelGGL(kern, pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file, nwg,
+                                       total_blocks, seed, out);
+                }
+                break;
             case 9:
                 if (max_blen <= kRegMaxBytes)
                     hipLaunchKernelGGL((block_sums_park<1, kParkLoaders, 2, 3, 1>), pgrid, pblock, 0, stream, arena,

@@ -314,13 +314,16 @@ struct Walker {
     // Candidate j sits in a chain: another candidate exactly B before or after
     // it, as consecutive matched blocks give (match.go:158 moves the walk
     // from a match at q to q + B).  A random false weak hit almost never does.
-    bool chained(const std::vector<uint64_t> &C, size_t j) const {
+    // f / b: monotone cursors (the callers visit j in increasing order), so a
+    // selection over n candidates costs O(n), not 2 n binary searches.
+    bool chained(const std::vector<uint64_t> &C, size_t j, size_t &f, size_t &b) const {
         const uint64_t B = (uint64_t)head.block_len, c = C[j];
-        const auto f = std::lower_bound(C.begin() + (int64_t)j + 1, C.end(), c + B);
-        if (f != C.end() && *f == c + B) return true;
+        if (f <= j) f = j + 1;
+        while (f < C.size() && C[f] < c + B) f++;
+        if (f < C.size() && C[f] == c + B) return true;
         if (c < B) return false;
-        const auto b = std::lower_bound(C.begin(), C.begin() + (int64_t)j, c - B);
-        return b != C.begin() + (int64_t)j && *b == c - B;
+        while (b < j && C[b] < c - B) b++;
+        return b < j && C[b] == c - B;
     }
     // The pending candidates the walk visits from C[i] (visited) on if every
     // chained pending candidate matches a block of length window() and every
@@ -331,12 +334,13 @@ struct Walker {
     void spec_batch(const std::vector<uint64_t> &C, const std::vector<int32_t> &res, size_t i,
                     std::vector<uint32_t> &batch) const {
         uint64_t x = C[i];
+        size_t f = i + 1, b = 0;
         for (size_t j = i; j < C.size() && batch.size() < kSparseBatch && (int64_t)C[j] < end; j++) {
             const uint64_t c = C[j];
             if (c < x) continue;
             if (res[j] == -2) {
                 batch.push_back((uint32_t)j);
-                x = chained(C, j) ? c + window(c) : c + 1;
+                x = chained(C, j, f, b) ? c + window(c) : c + 1;
             } else {
                 x = res[j] >= 0 ? c + (uint64_t)len_of(res[j]) : c + 1;
             }
