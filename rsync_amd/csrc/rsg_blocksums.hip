@@ -893,7 +893,19 @@ __device__ __forceinline__ void store_tile_records(uint8_t *out, uint64_t t, uin
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const u32x4v a = reinterpret_cast<const u32x4v *>(rec)[lane];
-    u32x4a4 *dst = reinterpret_cast<u32x4a4 *>(out + t * (64ull * kRecordBytes));
+    uint8_t *tile_out = out + t * (64ull * kRecordBytes);
+    if constexpr (REC >= 4) {
+        // buffer stores with an explicit cache policy: 4 = nt | sc1, 5 = nt | sc0 | sc1
+        constexpr int aux = REC == 4 ? (2 | 16) : (1 | 2 | 16);
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)tile_out, (short)0, 1280, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(a, r, 16u * lane, 0, aux);
+        if (lane < 16) {
+            const u32x4v b = reinterpret_cast<const u32x4v *>(rec)[64 + lane];
+            __builtin_amdgcn_raw_buffer_store_b128(b, r, 1024u + 16u * lane, 0, aux);
+        }
+        return;
+    }
+    u32x4a4 *dst = reinterpret_cast<u32x4a4 *>(tile_out);
     if (REC == 2) __builtin_nontemporal_store(u32x4a4{a.x, a.y, a.z, a.w}, dst + lane);
     else dst[lane] = u32x4a4{a.x, a.y, a.z, a.w};
     if (lane < 16) {
@@ -901,6 +913,16 @@ __device__ __forceinline__ void store_tile_records(uint8_t *out, uint64_t t, uin
         if (REC == 2) __builtin_nontemporal_store(u32x4a4{b.x, b.y, b.z, b.w}, dst + 64 + lane);
         else dst[64 + lane] = u32x4a4{b.x, b.y, b.z, b.w};
     }
+}
+
+// A lane's own record with nontemporal stores (park REC = 3).
+__device__ __forceinline__ void store_record_nt(uint8_t *out, uint64_t g, uint32_t n, int32_t s1, uint32_t t,
+                                                const uint32_t h[4]) {
+    const uint32_t s2 = n * (uint32_t)s1 - t;
+    const uint32_t sum1 = ((uint32_t)s1 & 0xffffu) | (s2 << 16);
+    u32x4a4 *o = reinterpret_cast<u32x4a4 *>(out + g * kRecordBytes);
+    __builtin_nontemporal_store(u32x4a4{sum1, h[0], h[1], h[2]}, o);
+    __builtin_nontemporal_store(h[3], reinterpret_cast<uint32_t *>(out + g * kRecordBytes + 16));
 }
 
 // A block of a direct tile: the lane locates and loads it itself.
@@ -1138,6 +1160,8 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             }
             if (MODE == 5 && h[0] != 0x9e3779b9u) {
                 // diagnostic: no record stores
+            } else if (REC == 3) {
+                store_record_nt(out, g, n, s1, tw, h);
             } else if (REC >= 1) {
                 store_tile_records<REC>(out, t, lane, &sh.rec[wave][0], n, s1, tw, h);
             } else {
@@ -1272,6 +1296,21 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                                 : diag == 24 ? block_sums_park<0, kParkLoaders, 2, 3, 0, 1>
                                 : diag == 25 ? block_sums_park<0, kParkLoaders, 2, 3, 0, 2>
                                              : block_sums_park<1, kParkLoaders, 2, 3, 0, 2>;
+                    hipLaunchKernelGGL(kern, pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file, nwg,
+                                       total_blocks, seed, out);
+                }
+                break;
+            case 27:
+            case 28:
+            case 29:
+            case 30:
+            case 31:
+                if (max_blen <= kRegMaxBytes) {
+                    auto kern = diag == 27   ? block_sums_park<0, kParkLoaders, 2, 3, 0, 3>
+                                : diag == 28 ? block_sums_park<0, kParkLoaders, 2, 3, 1, 2>
+                                : diag == 29 ? block_sums_park<1, kParkLoaders, 2, 3, 1, 2>
+                                : diag == 30 ? block_sums_park<0, kParkLoaders, 2, 3, 0, 4>
+                                             : block_sums_park<0, kParkLoaders, 2, 3, 0, 5>;
                     hipLaunchKernelGGL(kern, pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file, nwg,
                                        total_blocks, seed, out);
                 }

@@ -289,6 +289,11 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
 //  * the sparse test scans up to kSparseBatch pending candidates; a dense
 //    verdict is remembered up to the last candidate it scanned, so a dense
 //    stretch does not rescan them every round trip.
+static bool walk_debug() {
+    static const bool on = getenv("RSG_WALK_DEBUG") != nullptr;
+    return on;
+}
+
 struct Walker {
     int64_t end = 0;   // visited offsets are < end (match.go:70)
     uint64_t size = 0;
@@ -419,6 +424,10 @@ struct Walker {
                 }
                 last_dense = dense;
                 consumed = 0;
+                if (known && walk_debug())  // RSG_WALK_DEBUG: why a job with known results needs another round trip
+                    fprintf(stderr, "[rsg walk] extra round trip at candidate %zu/%zu offset %llu (pos %llu, %s, batch %zu)\n",
+                            i, C.size(), (unsigned long long)c, (unsigned long long)pos, dense ? "dense" : "sparse",
+                            batch.size());
                 batches++;
                 windows += batch.size();
                 rsg_status s = verify(batch, res);
