@@ -29,6 +29,7 @@
 namespace rsg {
 
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
 // Fallback census (rsg_block_sums_fallbacks): [0] full 64-block waves of the
 // staged kernels, [1] full 64-block tiles of the park kernel that could not
@@ -143,6 +144,61 @@ __device__ __forceinline__ void store_record(uint8_t *out, uint64_t g, uint32_t 
     uint32_t *o = reinterpret_cast<uint32_t *>(out + g * kRecordBytes);
     o[0] = sum1;
     o[1] = h[0]; o[2] = h[1]; o[3] = h[2]; o[4] = h[3];
+}
+
+// The 64 records of a staged tile (blocks t*64 .. t*64+63: 1280 contiguous
+// bytes of the output) through the hasher's LDS area, so they leave as
+// full 16-byte lanes of 1 KiB runs (64 + 16 quads) instead of 64 lanes each
+// writing 20 bytes at a 20-byte stride: those strided partial-line stores
+// cost the kernel its streaming rate (DESIGN.md §4.1, park memory only with
+// and without its record stores: 0.187 against 0.155 ms per cfg2 launch).
+// REC = 2: the stores are nontemporal (the records are not read again here).
+template <int REC>
+__device__ __forceinline__ void store_tile_records(uint8_t *out, uint64_t t, uint32_t lane, uint32_t *rec, uint32_t n,
+                                                   int32_t s1, uint32_t tw, const uint32_t h[4]) {
+    const uint32_t s2 = n * (uint32_t)s1 - tw;                    // sum (n - i) x_i
+    const uint32_t sum1 = ((uint32_t)s1 & 0xffffu) | (s2 << 16);  // rsyncchecksum.go:50
+    rec[5 * lane + 0] = sum1;
+    rec[5 * lane + 1] = h[0];
+    rec[5 * lane + 2] = h[1];
+    rec[5 * lane + 3] = h[2];
+    rec[5 * lane + 4] = h[3];
+    // other lanes' records are read back: the wave's LDS operations run in
+    // order, so only the compiler must not move the reads above the writes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const u32x4v a = reinterpret_cast<const u32x4v *>(rec)[lane];
+    uint8_t *tile_out = out + t * (64ull * kRecordBytes);
+    if constexpr (REC >= 4) {
+        // buffer stores with an explicit cache policy: 4 = nt | sc1, 5 = nt | sc0 | sc1
+        constexpr int aux = REC == 4 ? (2 | 16) : (1 | 2 | 16);
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)tile_out, (short)0, 1280, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(a, r, 16u * lane, 0, aux);
+        if (lane < 16) {
+            const u32x4v b = reinterpret_cast<const u32x4v *>(rec)[64 + lane];
+            __builtin_amdgcn_raw_buffer_store_b128(b, r, 1024u + 16u * lane, 0, aux);
+        }
+        return;
+    }
+    u32x4a4 *dst = reinterpret_cast<u32x4a4 *>(tile_out);
+    if (REC == 2) __builtin_nontemporal_store(u32x4a4{a.x, a.y, a.z, a.w}, dst + lane);
+    else dst[lane] = u32x4a4{a.x, a.y, a.z, a.w};
+    if (lane < 16) {
+        const u32x4v b = reinterpret_cast<const u32x4v *>(rec)[64 + lane];
+        if (REC == 2) __builtin_nontemporal_store(u32x4a4{b.x, b.y, b.z, b.w}, dst + 64 + lane);
+        else dst[64 + lane] = u32x4a4{b.x, b.y, b.z, b.w};
+    }
+}
+
+// A lane's own record with nontemporal stores (park REC = 3).
+__device__ __forceinline__ void store_record_nt(uint8_t *out, uint64_t g, uint32_t n, int32_t s1, uint32_t t,
+                                                const uint32_t h[4]) {
+    const uint32_t s2 = n * (uint32_t)s1 - t;
+    const uint32_t sum1 = ((uint32_t)s1 & 0xffffu) | (s2 << 16);
+    u32x4a4 *o = reinterpret_cast<u32x4a4 *>(out + g * kRecordBytes);
+    __builtin_nontemporal_store(u32x4a4{sum1, h[0], h[1], h[2]}, o);
+    __builtin_nontemporal_store(h[3], reinterpret_cast<uint32_t *>(out + g * kRecordBytes + 16));
 }
 
 // File of block g: the largest f in [wg_file[wg], wg_file[wg+1]] with
@@ -471,7 +527,11 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     }
 #undef RSG_DMA_SEGMENT
 #undef RSG_READ_SEGMENT
-    store_record(out, g, n, s1, t, h);
+    // a full wave's 64 records are contiguous (blocks wave_first ..): staged
+    // in the wave's slab (its last segment has been read) and written as
+    // coalesced nontemporal stores, as the park kernel does (round 5)
+    if (MODE == 0) store_tile_records<2>(out, wave_first / 64, lane, reinterpret_cast<uint32_t *>(slab), n, s1, t, h);
+    else store_record(out, g, n, s1, t, h);
 }
 
 // ---------------------------------------------------------------- read ceilings
@@ -794,7 +854,6 @@ __device__ __forceinline__ void pk_issue(const uint8_t *arena, uint8_t *dst, con
 // instead of tabulated (the tables would cost 90 VGPRs next to R's 180):
 // index 64 i + l advances by 64 = 45 + 19 per request.  Out-of-range requests
 // (quads past the block, the pad) return zeros and fetch nothing.
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 template <int AUX>
 __device__ __forceinline__ void pk_reg_issue(const uint8_t *arena, const PkDesc &d, uint32_t lane, u32x4v R[kPkDma]) {
     const __amdgpu_buffer_rsrc_t rsrc =
@@ -868,61 +927,6 @@ __device__ __forceinline__ void pk_reg_swap(uint8_t *dst, const uint8_t *arena, 
         off += wrap ? 2u * d.B - 416u : d.B + 304u;
     }
     __builtin_amdgcn_sched_barrier(0);
-}
-
-// The 64 records of a staged tile (blocks t*64 .. t*64+63: 1280 contiguous
-// bytes of the output) through the hasher's LDS area, so they leave as
-// full 16-byte lanes of 1 KiB runs (64 + 16 quads) instead of 64 lanes each
-// writing 20 bytes at a 20-byte stride: those strided partial-line stores
-// cost the kernel its streaming rate (DESIGN.md §4.1, park memory only with
-// and without its record stores: 0.187 against 0.155 ms per cfg2 launch).
-// REC = 2: the stores are nontemporal (the records are not read again here).
-template <int REC>
-__device__ __forceinline__ void store_tile_records(uint8_t *out, uint64_t t, uint32_t lane, uint32_t *rec, uint32_t n,
-                                                   int32_t s1, uint32_t tw, const uint32_t h[4]) {
-    const uint32_t s2 = n * (uint32_t)s1 - tw;                    // sum (n - i) x_i
-    const uint32_t sum1 = ((uint32_t)s1 & 0xffffu) | (s2 << 16);  // rsyncchecksum.go:50
-    rec[5 * lane + 0] = sum1;
-    rec[5 * lane + 1] = h[0];
-    rec[5 * lane + 2] = h[1];
-    rec[5 * lane + 3] = h[2];
-    rec[5 * lane + 4] = h[3];
-    // other lanes' records are read back: the wave's LDS operations run in
-    // order, so only the compiler must not move the reads above the writes
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const u32x4v a = reinterpret_cast<const u32x4v *>(rec)[lane];
-    uint8_t *tile_out = out + t * (64ull * kRecordBytes);
-    if constexpr (REC >= 4) {
-        // buffer stores with an explicit cache policy: 4 = nt | sc1, 5 = nt | sc0 | sc1
-        constexpr int aux = REC == 4 ? (2 | 16) : (1 | 2 | 16);
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)tile_out, (short)0, 1280, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b128(a, r, 16u * lane, 0, aux);
-        if (lane < 16) {
-            const u32x4v b = reinterpret_cast<const u32x4v *>(rec)[64 + lane];
-            __builtin_amdgcn_raw_buffer_store_b128(b, r, 1024u + 16u * lane, 0, aux);
-        }
-        return;
-    }
-    u32x4a4 *dst = reinterpret_cast<u32x4a4 *>(tile_out);
-    if (REC == 2) __builtin_nontemporal_store(u32x4a4{a.x, a.y, a.z, a.w}, dst + lane);
-    else dst[lane] = u32x4a4{a.x, a.y, a.z, a.w};
-    if (lane < 16) {
-        const u32x4v b = reinterpret_cast<const u32x4v *>(rec)[64 + lane];
-        if (REC == 2) __builtin_nontemporal_store(u32x4a4{b.x, b.y, b.z, b.w}, dst + 64 + lane);
-        else dst[64 + lane] = u32x4a4{b.x, b.y, b.z, b.w};
-    }
-}
-
-// A lane's own record with nontemporal stores (park REC = 3).
-__device__ __forceinline__ void store_record_nt(uint8_t *out, uint64_t g, uint32_t n, int32_t s1, uint32_t t,
-                                                const uint32_t h[4]) {
-    const uint32_t s2 = n * (uint32_t)s1 - t;
-    const uint32_t sum1 = ((uint32_t)s1 & 0xffffu) | (s2 << 16);
-    u32x4a4 *o = reinterpret_cast<u32x4a4 *>(out + g * kRecordBytes);
-    __builtin_nontemporal_store(u32x4a4{sum1, h[0], h[1], h[2]}, o);
-    __builtin_nontemporal_store(h[3], reinterpret_cast<uint32_t *>(out + g * kRecordBytes + 16));
 }
 
 // A block of a direct tile: the lane locates and loads it itself.
@@ -1197,6 +1201,10 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
 // with LDS DMA, 7 = the same with every request 4 bytes off a 16-byte
 // boundary, 8 = park memory only with 16-byte aligned quad requests.
 constexpr int kParkLoaders = 3;  // 1 / 2 / 3 loaders measured
+// Record stores of the park kernel: a tile's 64 records staged in LDS and
+// written as coalesced nontemporal 16-byte stores (DESIGN.md §4.1, round 5:
+// 0.1864-0.1893 ms against 0.1943-0.1946 for per-lane 20-byte stores).
+constexpr int kParkRec = 2;
 int block_sums_variant_env() {
     static const int v = [] {
         const char *e = getenv("RSG_BLOCKSUMS_KERNEL");
@@ -1300,6 +1308,11 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                                        total_blocks, seed, out);
                 }
                 break;
+            case 32:  // the round-4 product: per-lane record stores
+                if (max_blen <= kRegMaxBytes)
+                    hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3, 0, 0>), pgrid, pblock, 0, stream, arena,
+                                       arena_bytes, files, wg_file, nwg, total_blocks, seed, out);
+                break;
             case 27:
             case 28:
             case 29:
@@ -1346,7 +1359,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                                total_blocks, seed, out);
             break;
         case 2:
-            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3>), pgrid, pblock, 0, stream, arena, arena_bytes,
+            hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3, 0, kParkRec>), pgrid, pblock, 0, stream, arena, arena_bytes,
                                files, wg_file, nwg, total_blocks, seed, out);
             break;
         case 7:
