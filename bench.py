@@ -189,7 +189,9 @@ def main():
                  (1, 23): "diag_park_rec1_memory_only", (1, 24): "park_rec1_coalesced_records",
                  (1, 25): "park_rec2_coalesced_nt_records", (1, 26): "diag_park_rec2_memory_only",
                  (1, 27): "park_rec3_lane_nt_records", (1, 28): "park_reg_rec2", (1, 29): "diag_park_reg_rec2_memory_only",
-                 (1, 30): "park_rec4_nt_sc1", (1, 31): "park_rec5_nt_sc0_sc1", (1, 32): "park_round4_lane_records"}
+                 (1, 30): "park_rec4_nt_sc1", (1, 31): "park_rec5_nt_sc0_sc1", (1, 32): "park_round4_lane_records",
+                 (1, 33): "diag_stream_rw_interleaved_1tile", (1, 34): "diag_stream_rw_contiguous_1tile",
+                 (1, 35): "diag_stream_rw_contiguous_8tiles", (1, 36): "diag_stream_r_park_pattern_8wave"}
         res = {v: [] for v in names}
         for _ in range(int(os.environ.get("AB_ROUNDS", "5"))):
             for v in names:

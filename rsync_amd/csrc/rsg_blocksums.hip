@@ -623,6 +623,59 @@ __global__ __launch_bounds__(512) void diag_stream_read(const uint8_t *__restric
     if (buf[threadIdx.x] == 0x5a && buf[threadIdx.x + 1] == 0xa5 && bytes == 1) sink[0] = 1;
 }
 
+// Timing diagnostic: the stream above plus the records' write stream.  3
+// waves, chunk = one park tile (64 x 700 bytes, 45 DMA instructions); per
+// chunk 1280 bytes of "records" are due at out + 1280 * chunk.  ASSIGN 0:
+// chunk c belongs to workgroup c % G (park's order); 1: workgroup w owns the
+// contiguous chunks [w n / G, (w + 1) n / G).  WB: chunks whose records a wave
+// writes at once (coalesced nt 16-byte stores; with ASSIGN 1 they are
+// contiguous in the output, with ASSIGN 0 they are 1280-byte pieces).
+template <int ASSIGN, int WB>
+__global__ __launch_bounds__(512) void diag_stream_rw(const uint8_t *__restrict__ arena, uint64_t bytes,
+                                                      uint8_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[64 * 1024];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave >= 3) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t chunk = 64ull * 700;
+    const uint64_t nch = bytes / chunk;
+    const uint32_t G = gridDim.x;
+    // ASSIGN 1: the workgroup's range split again into one contiguous range per wave
+    const uint64_t w0 = nch * blockIdx.x / G, w1 = nch * (blockIdx.x + 1) / G;
+    const uint64_t c0 = ASSIGN ? w0 + (w1 - w0) * wave / 3 : blockIdx.x + (uint64_t)G * wave;
+    const uint64_t c1 = ASSIGN ? w0 + (w1 - w0) * (wave + 1) / 3 : nch;
+    const uint64_t step = ASSIGN ? 1 : 3ull * G;
+    uint32_t pending = 0;
+    uint64_t first = 0;
+#pragma unroll 1
+    for (uint64_t c = c0; c < c1; c += step) {
+        const __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(arena + rfl64(c * chunk)), (short)0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 45; i++)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(buf + 1024 * i), 16,
+                                                     park_quad_offset(64u * i + lane), 0, 0, 2);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (pending == 0) first = c;
+        if (++pending == WB || c + step >= c1) {
+            // this wave's records of its `pending` last chunks
+            const u32x4v v = reinterpret_cast<const u32x4v *>(buf)[lane];
+            if (ASSIGN) {  // the pending chunks are consecutive: one contiguous burst
+                u32x4a4 *o = reinterpret_cast<u32x4a4 *>(out + first * 1280ull);
+                for (uint32_t q = lane; q < 80u * pending; q += 64)
+                    __builtin_nontemporal_store(u32x4a4{v.x, v.y, v.z, v.w}, o + q);
+            } else {
+                for (uint32_t k = 0; k < pending; k++) {
+                    u32x4a4 *o = reinterpret_cast<u32x4a4 *>(out + (first + (uint64_t)k * step) * 1280ull);
+                    __builtin_nontemporal_store(u32x4a4{v.x, v.y, v.z, v.w}, o + lane);
+                    if (lane < 16) __builtin_nontemporal_store(u32x4a4{v.x, v.y, v.z, v.w}, o + 64 + lane);
+                }
+            }
+            pending = 0;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- park variant (loader + register park)
 // For blocks of at most kRegMaxBytes (703: the reference's 700-byte blocks).
 // Every byte should cross HBM once, in long runs: a tile = 64 consecutive
@@ -1308,6 +1361,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                                        total_blocks, seed, out);
                 }
                 break;
+            case 33: hipLaunchKernelGGL((diag_stream_rw<0, 1>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
+            case 34: hipLaunchKernelGGL((diag_stream_rw<1, 1>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
+            case 35: hipLaunchKernelGGL((diag_stream_rw<1, 8>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
+            case 36: hipLaunchKernelGGL((diag_stream_read<3, 45, 1, 1>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
             case 32:  // the round-4 product: per-lane record stores
                 if (max_blen <= kRegMaxBytes)
                     hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3, 0, 0>), pgrid, pblock, 0, stream, arena,
