@@ -191,7 +191,12 @@ def main():
                  (1, 27): "park_rec3_lane_nt_records", (1, 28): "park_reg_rec2", (1, 29): "diag_park_reg_rec2_memory_only",
                  (1, 30): "park_rec4_nt_sc1", (1, 31): "park_rec5_nt_sc0_sc1", (1, 32): "park_round4_lane_records",
                  (1, 33): "diag_stream_rw_interleaved_1tile", (1, 34): "diag_stream_rw_contiguous_1tile",
-                 (1, 35): "diag_stream_rw_contiguous_8tiles", (1, 36): "diag_stream_r_park_pattern_8wave"}
+                 (1, 35): "diag_stream_rw_contiguous_8tiles", (1, 36): "diag_stream_r_park_pattern_8wave",
+                 (1, 37): "diag_stream_rw_contiguous_4tiles", (1, 38): "diag_stream_rw_contiguous_16tiles",
+                 (1, 39): "diag_stream_rw_contiguous_32tiles", (1, 40): "diag_stream_rw_interleaved_8tiles"}
+        only = os.environ.get("AB_ONLY")  # comma-separated substrings: A/B only the matching entries
+        if only:
+            names = {v: n for v, n in names.items() if any(o in n for o in only.split(","))}
         res = {v: [] for v in names}
         for _ in range(int(os.environ.get("AB_ROUNDS", "5"))):
             for v in names:

@@ -1365,6 +1365,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             case 34: hipLaunchKernelGGL((diag_stream_rw<1, 1>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
             case 35: hipLaunchKernelGGL((diag_stream_rw<1, 8>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
             case 36: hipLaunchKernelGGL((diag_stream_read<3, 45, 1, 1>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 37: hipLaunchKernelGGL((diag_stream_rw<1, 4>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
+            case 38: hipLaunchKernelGGL((diag_stream_rw<1, 16>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
+            case 39: hipLaunchKernelGGL((diag_stream_rw<1, 32>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
+            case 40: hipLaunchKernelGGL((diag_stream_rw<0, 8>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
             case 32:  // the round-4 product: per-lane record stores
                 if (max_blen <= kRegMaxBytes)
                     hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3, 0, 0>), pgrid, pblock, 0, stream, arena,
