@@ -707,9 +707,15 @@ constexpr uint32_t kPkWaves = 8;
 constexpr uint32_t kPkThreads = 64 * kPkWaves;
 static_assert(kPkTile % 1024 == 0 && kPkPiece % 16 == 0, "tile = whole DMA instructions");
 
+constexpr uint32_t kRecRing = 16;  // tiles of records the workgroup stages (REC 6); two groups of 8
 struct PkShared {
     uint8_t tile[kPkSlots][kPkTile];
-    uint32_t rec[kPkWaves][64 * 5];  // a hasher's 64 records (20 B each), staged for coalesced stores
+    // REC 1..5: wave w's 64 records (20 B each) at rec[320 w]; REC 6: a ring
+    // of kRecRing tiles' records, ticket k's at rec[320 (k % kRecRing)]
+    uint32_t rec[kRecRing * 64 * 5];
+    uint32_t ring_kind[kRecRing];  // REC 6: 1 = flush the slot's records, 0 = written directly
+    uint32_t ring_done[2];         // REC 6: tiles of the group (8 tickets) whose records are in
+    uint32_t ring_flushed[2];      // REC 6: the last group flushed from each half of the ring
     uint32_t n[kPkSlots][64];  // block lengths of the slot's tile
     uint32_t full[kPkSlots];
     uint32_t freeq[kPkSlots];
@@ -1014,6 +1020,62 @@ __device__ __forceinline__ void pk_direct(const uint8_t *__restrict__ arena, uin
     store_record(out, g, nn, s1, tw, h);
 }
 
+// REC 6: the workgroup's records leave in bursts of 8 tiles.  Writing them
+// tile by tile interleaves a small write with the reads every ~2 us per CU,
+// and HBM pays for every read/write switch (a bare
+// 3-wave reader with 1 280 bytes of records per tile 0.185 ms, the same
+// records written 8 tiles at a time 0.169, reads alone 0.150).  Ticket k's
+// records go to ring slot k % 16 (a group = tickets 8m .. 8m + 7, its half
+// m % 2); the hasher that completes a group writes its tiles' records (8
+// separate 1 280-byte pieces of the output) as coalesced nt stores and
+// releases the half.  A hasher waits for its half's previous group (m - 2)
+// to be flushed before writing into it: groups complete in ticket order up
+// to the hashers in flight, so that wait is on older tickets only.
+// put = false: a direct tile whose lanes stored their records themselves.
+__device__ __forceinline__ void pk_ring_put(PkShared &sh, uint32_t k, uint64_t t, uint32_t G, uint64_t ntiles,
+                                            uint32_t lane, uint32_t n, int32_t s1, uint32_t tw, const uint32_t h[4],
+                                            uint8_t *__restrict__ out, bool put) {
+    const uint32_t r = k % kRecRing, m = k / 8u, half = m & 1u;
+    while (pk_load(&sh.ring_flushed[half]) != m - 2u) __builtin_amdgcn_s_sleep(1);
+    if (put) {
+        const uint32_t s2 = n * (uint32_t)s1 - tw;
+        uint32_t *rec = &sh.rec[320u * r + 5u * lane];
+        rec[0] = ((uint32_t)s1 & 0xffffu) | (s2 << 16);  // rsyncchecksum.go:50
+        rec[1] = h[0];
+        rec[2] = h[1];
+        rec[3] = h[2];
+        rec[4] = h[3];
+    }
+    if (lane == 0) sh.ring_kind[r] = put ? 1u : 0u;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    uint32_t old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(&sh.ring_done[half], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    old = __builtin_amdgcn_readfirstlane(old);
+    // this workgroup's tickets: t = blockIdx.x + k G < ntiles
+    const uint64_t nk = (ntiles - blockIdx.x + G - 1) / G;
+    const uint32_t gsize = (uint32_t)min<uint64_t>(8, nk - 8ull * m);
+    if (old + 1 != gsize) return;
+    // the group's last tile: flush the group
+    for (uint32_t j = 0; j < gsize; j++) {
+        const uint32_t kk = 8u * m + j, rr = kk % kRecRing;
+        if (!__builtin_amdgcn_readfirstlane(sh.ring_kind[rr])) continue;
+        const uint64_t tt = blockIdx.x + (uint64_t)kk * G;
+        const u32x4v* src = reinterpret_cast<const u32x4v *>(&sh.rec[320u * rr]);
+        u32x4a4 *dst = reinterpret_cast<u32x4a4 *>(out + tt * (64ull * kRecordBytes));
+        const u32x4v a = src[lane];
+        __builtin_nontemporal_store(u32x4a4{a.x, a.y, a.z, a.w}, dst + lane);
+        if (lane < 16) {
+            const u32x4v b = src[64 + lane];
+            __builtin_nontemporal_store(u32x4a4{b.x, b.y, b.z, b.w}, dst + 64 + lane);
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring's reads are done before the half is released
+    if (lane == 0) {
+        sh.ring_done[half] = 0;
+        pk_store(&sh.ring_flushed[half], m);
+    }
+}
+
 // MODE 0 = product; diagnostics: 1 = memory only (DMA + copy, no hashing),
 // 2 = hashing only (no DMA: the hashers hash whatever the slots hold),
 // 3 = memory only with every quad request 16-byte aligned (ALN above).
@@ -1047,6 +1109,10 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     if (threadIdx.x < kPkSlots) {
         sh.full[threadIdx.x] = ~0u;
         sh.freeq[threadIdx.x] = threadIdx.x;
+    }
+    if (threadIdx.x < 2) {
+        sh.ring_done[threadIdx.x] = 0;
+        sh.ring_flushed[threadIdx.x] = threadIdx.x - 2u;  // "group -2 / -1 flushed": both halves free
     }
     if (threadIdx.x == 0) sh.ticket = 0;
     __syncthreads();
@@ -1217,10 +1283,12 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             }
             if (MODE == 5 && h[0] != 0x9e3779b9u) {
                 // diagnostic: no record stores
+            } else if (REC == 6) {
+                pk_ring_put(sh, k, t, G, ntiles, lane, n, s1, tw, h, out, true);
             } else if (REC == 3) {
                 store_record_nt(out, g, n, s1, tw, h);
             } else if (REC >= 1) {
-                store_tile_records<REC>(out, t, lane, &sh.rec[wave][0], n, s1, tw, h);
+                store_tile_records<REC>(out, t, lane, &sh.rec[320u * wave], n, s1, tw, h);
             } else {
                 store_record(out, g, n, s1, tw, h);
             }
@@ -1231,6 +1299,10 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
                 if (MODE == 0 && t * 64 + 64 <= total_blocks) count_fallback(1);
             }
             if (g < total_blocks) pk_direct(arena, arena_bytes, files, wg_file, nwg256, g, seed, out);
+            if (REC == 6) {
+                const uint32_t z[4] = {0, 0, 0, 0};
+                pk_ring_put(sh, k, t, G, ntiles, lane, 0, 0, 0, z, out, false);  // its records are out already
+            }
         }
     }
 }
@@ -1369,6 +1441,15 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             case 38: hipLaunchKernelGGL((diag_stream_rw<1, 16>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
             case 39: hipLaunchKernelGGL((diag_stream_rw<1, 32>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
             case 40: hipLaunchKernelGGL((diag_stream_rw<0, 8>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
+            case 41:
+            case 42:
+                if (max_blen <= kRegMaxBytes) {
+                    auto kern = diag == 41 ? block_sums_park<0, kParkLoaders, 2, 3, 0, 6>
+                                           : block_sums_park<1, kParkLoaders, 2, 3, 0, 6>;
+                    hipLaunchKernelGGL(kern, pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file, nwg,
+                                       total_blocks, seed, out);
+                }
+                break;
             case 32:  // the round-4 product: per-lane record stores
                 if (max_blen <= kRegMaxBytes)
                     hipLaunchKernelGGL((block_sums_park<0, kParkLoaders, 2, 3, 0, 0>), pgrid, pblock, 0, stream, arena,
