@@ -462,6 +462,12 @@ def measure_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, record
         (dt,) = max_over_ranks(world, time.perf_counter() - t0)
         return {"ms_per_step": round(dt * 1e3 / steps, 4), "gib_s": round(bytes_all * steps / dt / GIB, 2)}
 
+    # floor of any synchronous delivery call: the same kernels, one host
+    # synchronisation per step, nothing moved
+    def synced(i):
+        sb.run_kernels(arenas[i & 1], SEED, recs)
+        eng.synchronize()
+    out["kernel_synced"] = timed(synced)
     # every rank copies its own records to pinned host memory over its own PCIe link
     host = eng.alloc_pinned(max(sb.my_records, 1) * rsync_amd.RECORD_BYTES)
     out["d2h_parallel_pipelined"] = timed(lambda i: sb.run_d2h(arenas[i & 1], SEED, recs, host))

@@ -1046,14 +1046,19 @@ __device__ __forceinline__ void pk_ring_put(PkShared &sh, uint32_t k, uint64_t t
         rec[3] = h[2];
         rec[4] = h[3];
     }
-    if (lane == 0) sh.ring_kind[r] = put ? 1u : 0u;
+    // Every branch below is on wave-uniform scalars and the single-lane
+    // stores are written by all lanes (same value): a lane-0-only store next
+    // to the early return let the compiler split the wave at the loop exit
+    // (lanes 1-63 ran on into the next ticket without lane 0: deadlock).
+    sh.ring_kind[r] = put ? 1u : 0u;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     uint32_t old = 0;
     if (lane == 0) old = __hip_atomic_fetch_add(&sh.ring_done[half], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
     old = __builtin_amdgcn_readfirstlane(old);
     // this workgroup's tickets: t = blockIdx.x + k G < ntiles
     const uint64_t nk = (ntiles - blockIdx.x + G - 1) / G;
-    const uint32_t gsize = (uint32_t)min<uint64_t>(8, nk - 8ull * m);
+    const uint64_t left = nk - 8ull * m;
+    const uint32_t gsize = __builtin_amdgcn_readfirstlane(left < 8 ? (uint32_t)left : 8u);
     if (old + 1 != gsize) return;
     // the group's last tile: flush the group
     for (uint32_t j = 0; j < gsize; j++) {
@@ -1070,10 +1075,8 @@ __device__ __forceinline__ void pk_ring_put(PkShared &sh, uint32_t k, uint64_t t
         }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring's reads are done before the half is released
-    if (lane == 0) {
-        sh.ring_done[half] = 0;
-        pk_store(&sh.ring_flushed[half], m);
-    }
+    sh.ring_done[half] = 0;
+    pk_store(&sh.ring_flushed[half], m);
 }
 
 // MODE 0 = product; diagnostics: 1 = memory only (DMA + copy, no hashing),

@@ -10,6 +10,8 @@
 // hashing of the next batch:
 //   kernel(b)  on ctx->stream            kernel(b+1) ...
 //   move(b)    on ctx->side[0], after an event recorded behind kernel(b)
+// (one batch: the move follows the kernel on ctx->stream; the root of a
+// one-rank gather has nothing to move).
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -69,22 +71,29 @@ struct Events {  // one per batch, destroyed on every exit
     }
 };
 
-// Shared driver of the two modes: kernel(b) on ctx->stream, then `move(b)`
-// queued on ctx->side[0] behind an event of kernel(b).  Waits for both
-// streams on every exit (nothing outlives the call).
+// Shared driver of the two modes: kernel(b) on ctx->stream, then `move(b, sb,
+// stream)`.  With more than one batch the moves run on ctx->side[0] behind an
+// event of kernel(b), so batch b moves while batch b + 1 hashes; one batch has
+// nothing to overlap and moves on ctx->stream right behind its kernel, and
+// moves = false (the root of a one-rank gather: its kernels write the records
+// where they land) runs the kernels alone -- no events, no second stream.
+// Waits for the streams it used on every exit (nothing outlives the call).
 // out(b, sb): where batch b's records are written.
 template <class Out, class Move>
 rsg_status pipeline(rsg_ctx *ctx, const rsg_shard_batch *batches, uint64_t nbatch, const void *d_arena, int32_t seed,
-                    Out out, Move move) {
-    struct Drain {
+                    Out out, Move move, bool moves) {
+    const bool side = moves && nbatch > 1;
+    struct Drain {  // error exits: drain whatever was queued
         rsg_ctx *c;
+        bool armed = true;
         ~Drain() {
+            if (!armed) return;
             (void)hipStreamSynchronize(c->stream);
             (void)hipStreamSynchronize(c->side[0]);
         }
     } drain{ctx};
     Events evs;
-    evs.ev.assign(nbatch, nullptr);
+    evs.ev.assign(side ? nbatch : 0, nullptr);
     for (uint64_t b = 0; b < nbatch; b++) {
         const rsg_shard_batch &sb = batches[b];
         if (sb.plan) {
@@ -94,14 +103,20 @@ rsg_status pipeline(rsg_ctx *ctx, const rsg_shard_batch *batches, uint64_t nbatc
                                              out(b, sb), sb.plan->d_scratch, ctx->stream);
             if (s != RSG_OK) return s;
         }
-        RSG_HIP(ctx, hipEventCreateWithFlags(&evs.ev[b], hipEventDisableTiming));
-        RSG_HIP(ctx, hipEventRecord(evs.ev[b], ctx->stream));
-        RSG_HIP(ctx, hipStreamWaitEvent(ctx->side[0], evs.ev[b], 0));
-        const rsg_status s = move(b, sb);
+        if (!moves) continue;
+        hipStream_t ms = ctx->stream;
+        if (side) {
+            RSG_HIP(ctx, hipEventCreateWithFlags(&evs.ev[b], hipEventDisableTiming));
+            RSG_HIP(ctx, hipEventRecord(evs.ev[b], ctx->stream));
+            RSG_HIP(ctx, hipStreamWaitEvent(ctx->side[0], evs.ev[b], 0));
+            ms = ctx->side[0];
+        }
+        const rsg_status s = move(b, sb, ms);
         if (s != RSG_OK) return s;
     }
     RSG_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    RSG_HIP(ctx, hipStreamSynchronize(ctx->side[0]));
+    if (side) RSG_HIP(ctx, hipStreamSynchronize(ctx->side[0]));
+    drain.armed = false;
     return RSG_OK;
 }
 
@@ -177,10 +192,13 @@ rsg_status rsg_block_sums_gather(rsg_ctx *ctx, const rsg_shard_batch *batches, u
         return is_root ? (uint8_t *)d_recv + sb.recv_offsets[ctx->rank]
                     : (uint8_t *)d_records + sb.record_offset * rsg::kRecordBytes;
     };
-    return pipeline(ctx, batches, nbatch, d_arena, seed, out, [&](uint64_t, const rsg_shard_batch &sb) {
-        return gatherv(ctx, (const uint8_t *)d_records + sb.record_offset * rsg::kRecordBytes, sb.send_bytes, d_recv,
-                       sb.recv_offsets, root, ctx->side[0], true);
-    });
+    return pipeline(
+        ctx, batches, nbatch, d_arena, seed, out,
+        [&](uint64_t, const rsg_shard_batch &sb, hipStream_t st) {
+            return gatherv(ctx, (const uint8_t *)d_records + sb.record_offset * rsg::kRecordBytes, sb.send_bytes,
+                           d_recv, sb.recv_offsets, root, st, true);
+        },
+        ctx->nranks > 1);
 }
 
 rsg_status rsg_block_sums_d2h(rsg_ctx *ctx, const rsg_shard_batch *batches, uint64_t nbatch, const void *d_arena,
@@ -193,14 +211,15 @@ rsg_status rsg_block_sums_d2h(rsg_ctx *ctx, const rsg_shard_batch *batches, uint
         return (uint8_t *)d_records + sb.record_offset * rsg::kRecordBytes;
     };
     return pipeline(ctx, batches, nbatch, d_arena, seed, out,
-                    [&](uint64_t, const rsg_shard_batch &sb) -> rsg_status {
+                    [&](uint64_t, const rsg_shard_batch &sb, hipStream_t st) -> rsg_status {
                         const uint64_t n = plan_records(sb) * rsg::kRecordBytes;
                         if (n)
                             RSG_HIP(ctx, hipMemcpyAsync(h_records + sb.record_offset * rsg::kRecordBytes,
                                                         (const uint8_t *)d_records + sb.record_offset * rsg::kRecordBytes,
-                                                        n, hipMemcpyDeviceToHost, ctx->side[0]));
+                                                        n, hipMemcpyDeviceToHost, st));
                         return RSG_OK;
-                    });
+                    },
+                    true);
 }
 
 }  // extern "C"
