@@ -484,6 +484,14 @@ def measure_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, record
     eng.comm_init(world, rank, uid)
     recv = eng.alloc(max(records_all, 1) * rsync_amd.RECORD_BYTES) if rank == 0 else None
     out["kernel_plus_gather_pipelined"] = timed(lambda i: sb.run_gather(arenas[i & 1], SEED, recs, recv, 0))
+    if os.environ.get("BENCH_DELIVERY_DIAG"):  # where the N = 1 gather's time goes
+        out["diag_kernel_synced_after_comm"] = timed(synced)
+        if recv is not None and world == 1:
+            def synced_recv(i):
+                sb.run_kernels(arenas[i & 1], SEED, recv)
+                eng.synchronize()
+            out["diag_kernel_synced_into_recv"] = timed(synced_recv)
+        out["diag_gather_again"] = timed(lambda i: sb.run_gather(arenas[i & 1], SEED, recs, recv, 0))
     out["kernel_plus_gather_pipelined"]["bytes_to_root"] = (records_all - sb.my_records) * rsync_amd.RECORD_BYTES
     out["recv"] = recv
     return out

@@ -961,6 +961,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
 #pragma unroll
         for (int g0 = 0; g0 < H; g0 += G) {
             u16x2 p1[G], p2[G], wd[G];
+            uint32_t wl[G], wh[G];  // the two filter words of each step, joined after the group's loads
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
                 const int j = g0 + jj;
@@ -981,7 +982,8 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                         "v_lshlrev_b32_sdwa %1, %3, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
                         : "=&v"(alo), "=&v"(ahi) : "v"(xa), "v"(one16));
                     typedef __attribute__((address_space(3))) const uint16_t lds16;
-                    wd[jj] = u16x2{*(lds16 *)(uintptr_t)(alo + fb), *(lds16 *)(uintptr_t)(ahi + fb)};
+                    wl[jj] = *(lds16 *)(uintptr_t)(alo + fb);
+                    wh[jj] = *(lds16 *)(uintptr_t)(ahi + fb);
                 }
                 if constexpr (BT) {
                     // uo's last uses, then ui written over it in place (a tied
@@ -1003,6 +1005,14 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
                     P2 = P2 + uo * negB + P1;
                 }
             }
+            // The group's eight filter reads are all issued before the first
+            // is used: the words are joined into pairs only here, so the first
+            // join waits for its own two reads while the other six are in
+            // flight (joined right after each pair of reads, every step waited
+            // out the whole LDS latency).
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int jj = 0; jj < G; jj++) wd[jj] = as_u16x2(__builtin_amdgcn_perm(wh[jj], wl[jj], 0x05040100u));
             // the group's eight hit masks first, then its parks: each park's
             // branch then tests a mask computed several instructions earlier
             // instead of waiting on the compare right before it
