@@ -445,13 +445,61 @@ def measure_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, record
     (rsg_block_sums_gather / rsg_block_sums_d2h): kernel of batch b+1 while
     batch b's records move.  Each timed step hashes the rank's whole share
     and delivers it; rates are all ranks' input bytes / the max-over-ranks
-    wall time.  -> dict for the bench line."""
+    wall time.  -> dict for the bench line.
+    The communicator is set up before any leg is timed, ~0.1 s of steps run
+    after its init, and every leg runs 8 untimed steps first (see below).
+    BENCH_DELIVERY_DIAG=2 (one rank): per-chunk kernel times before and
+    after the init, and the gather again after the d2h leg."""
     import rsync_amd
     out = {"batches": sb.nbatch}
     steps = max(2, args.delivery_steps)
+    diag = os.environ.get("BENCH_DELIVERY_DIAG") == "2" and world == 1
+    if diag:  # per-chunk times of the kernel synchronised per step, before and after the communicator's init
+        import torch
+        ts = torch.cuda.Stream()
+
+        def chunk():
+            t0 = time.perf_counter()
+            for i in range(20):
+                sb.run_kernels(arenas[i & 1], SEED, recs)
+                eng.synchronize()
+            wall = (time.perf_counter() - t0) / 20
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(ts)
+            for i in range(20):
+                sb.run_kernels(arenas[i & 1], SEED, recs, stream=ts.cuda_stream)
+            e1.record(ts)
+            e1.synchronize()
+            return [round(wall * 1e3, 4), round(e0.elapsed_time(e1) / 20, 4)]
+        out["diag_before_comm"] = [chunk() for _ in range(5)]
+    if world > 1:
+        import torch.distributed as dist
+        uid = [rsync_amd.Engine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        uid = uid[0]
+    else:
+        uid = rsync_amd.Engine.comm_unique_id()
+    eng.comm_init(world, rank, uid)
+    if diag:
+        t_init = time.perf_counter()
+        out["diag_after_comm"] = [chunk() + [round((time.perf_counter() - t_init) * 1e3, 1)] for _ in range(12)]
+    recv = eng.alloc(max(records_all, 1) * rsync_amd.RECORD_BYTES) if rank == 0 else None
+
+    def synced(i):
+        sb.run_kernels(arenas[i & 1], SEED, recs)
+        eng.synchronize()
+    # ~0.1 s of steps before any leg is timed: the kernel ran up to 25 % slower
+    # in the first ~25 ms after ncclCommInitRank (r05q: HIP-event kernel time
+    # 0.231, 0.211, 0.198 ms in the first three 20-step chunks, 0.186-0.191
+    # after), a start-up transient of the communicator, not a cost of the step
+    t_w = time.perf_counter()
+    i = 0
+    while time.perf_counter() - t_w < 0.1:
+        synced(i)
+        i += 1
 
     def timed(fn):
-        for i in range(2):
+        for i in range(8):
             fn(i)
         if world > 1:
             import torch.distributed as dist
@@ -464,35 +512,19 @@ def measure_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, record
 
     # floor of any synchronous delivery call: the same kernels, one host
     # synchronisation per step, nothing moved
-    def synced(i):
-        sb.run_kernels(arenas[i & 1], SEED, recs)
-        eng.synchronize()
     out["kernel_synced"] = timed(synced)
+    # RCCL gather of every rank's records to rank 0 (one rank: its kernels
+    # write the records where they land, nothing moves)
+    out["kernel_plus_gather_pipelined"] = timed(lambda i: sb.run_gather(arenas[i & 1], SEED, recs, recv, 0))
+    out["kernel_plus_gather_pipelined"]["bytes_to_root"] = (records_all - sb.my_records) * rsync_amd.RECORD_BYTES
     # every rank copies its own records to pinned host memory over its own PCIe link
     host = eng.alloc_pinned(max(sb.my_records, 1) * rsync_amd.RECORD_BYTES)
     out["d2h_parallel_pipelined"] = timed(lambda i: sb.run_d2h(arenas[i & 1], SEED, recs, host))
     out["d2h_parallel_pipelined"]["bytes_to_host_per_rank"] = sb.my_records * rsync_amd.RECORD_BYTES
     eng.free_pinned(host)
-    # RCCL gather of every rank's records to rank 0 (one rank: the root's self copy)
-    if world > 1:
-        import torch.distributed as dist
-        uid = [rsync_amd.Engine.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        uid = uid[0]
-    else:
-        uid = rsync_amd.Engine.comm_unique_id()
-    eng.comm_init(world, rank, uid)
-    recv = eng.alloc(max(records_all, 1) * rsync_amd.RECORD_BYTES) if rank == 0 else None
-    out["kernel_plus_gather_pipelined"] = timed(lambda i: sb.run_gather(arenas[i & 1], SEED, recs, recv, 0))
-    if os.environ.get("BENCH_DELIVERY_DIAG"):  # where the N = 1 gather's time goes
-        out["diag_kernel_synced_after_comm"] = timed(synced)
-        if recv is not None and world == 1:
-            def synced_recv(i):
-                sb.run_kernels(arenas[i & 1], SEED, recv)
-                eng.synchronize()
-            out["diag_kernel_synced_into_recv"] = timed(synced_recv)
-        out["diag_gather_again"] = timed(lambda i: sb.run_gather(arenas[i & 1], SEED, recs, recv, 0))
-    out["kernel_plus_gather_pipelined"]["bytes_to_root"] = (records_all - sb.my_records) * rsync_amd.RECORD_BYTES
+    if diag:
+        out["diag_gather_after_d2h"] = timed(lambda i: sb.run_gather(arenas[i & 1], SEED, recs, recv, 0))
+        out["diag_synced_after_d2h"] = timed(synced)
     out["recv"] = recv
     return out
 

@@ -309,10 +309,16 @@ struct Walker {
     uint32_t window(uint64_t q) const { return (uint32_t)std::min<uint64_t>((uint64_t)head.block_len, size - q); }
     int64_t len_of(int32_t i) const { return (i == head.count - 1 && head.rem != 0) ? head.rem : head.block_len; }
 
-    static bool spec_on() {  // RSG_CONFIRM_SPEC=0 (A/B): confirm every pending candidate of a sparse stretch
+    // RSG_CONFIRM_SPEC=1: speculative selection of sparse batches.  Off by
+    // default: it confirms 15 % fewer windows on cfg3 (19 957 against 23 515
+    // per GiB) but must sort the roll's list before queueing them and costs
+    // a round trip where a guess fails, while without it the confirmation is
+    // queued straight from the list; cfg3 1014-1038 against 1002-1058 GiB/s,
+    // two interleaved rounds (profiles/r05q_cfg3_confirm_ab.txt).
+    static bool spec_on() {
         static const bool on = [] {
             const char *e = getenv("RSG_CONFIRM_SPEC");
-            return !(e && e[0] == '0');
+            return e && e[0] == '1';
         }();
         return on;
     }
@@ -459,38 +465,71 @@ rsg_status walk(Search &S, const std::vector<uint64_t> &C, uint64_t &pos, std::v
 }
 
 rsg_status launch_range(Search &S, uint32_t lo, uint32_t hi);
+rsg_status queue_confirm(Search &S, const uint64_t *off, uint32_t m);
 
 // A sparse range's candidates confirmed in one batch with the plan built on
-// the GPU (confirm_plan_kernel) from the windows' offsets: the host sorts the
-// roll's list (pinned host memory the roll wrote), picks the windows the walk
-// will visit (Walker::spec_batch: chained candidates assumed to match, the
-// false weak hits inside their spans skipped), writes their offsets to pinned
-// memory and queues the confirmation.  C = the sorted distinct offsets, sel =
-// the confirmed ones (indices into C), results in sel order.
+// the GPU (confirm_plan_kernel) from the windows' offsets (the roll's list,
+// pinned host memory the roll wrote).  Speculative selection (RSG_CONFIRM_SPEC=1):
+// the host sorts the list first and picks the windows the walk will visit
+// (Walker::spec_batch: chained candidates assumed to match, the false weak
+// hits inside their spans skipped).  C = the sorted distinct offsets, sel[k] =
+// the index in C of the k-th confirmed window (results in that order).
 rsg_status confirm_all(Search &S, uint32_t n, uint64_t pos, std::vector<uint64_t> &C, std::vector<uint32_t> &sel) {
-    rsg_ctx *ctx = S.ctx;
     SearchSlot &sl = *S.sl;
     rsg_status s;
+    Walker w;
+    w.end = S.end;
+    w.size = S.size;
+    w.head = S.head;
+    // Without the speculative selection every candidate is confirmed, so the
+    // confirmation is queued straight from the roll's list in its append
+    // order, and the host sorts while the GPU hashes (sorting first kept the
+    // confirmation waiting 0.25-0.3 ms per 1 GiB file, r05n).
+    const bool raw = !w.spec;
+    if (raw) {
+        sel.clear();
+        S.pt.mark("c.select");
+        if ((s = queue_confirm(S, (const uint64_t *)sl.list.p, n)) != RSG_OK) return s;
+        // (offset << 22 | list index) sorted by offset; sel[k] = the sorted
+        // index of list entry k (found[] is in list order)
+        static_assert(kCandCap <= (1u << 22), "list index in 22 bits");
+        std::vector<uint64_t> key(n);
+        const uint64_t *list = (const uint64_t *)sl.list.p;
+        for (uint32_t k = 0; k < n; k++) key[k] = (list[k] << 22) | k;
+        sort_offsets(key, 22);
+        C.clear();
+        C.reserve(n);
+        sel.assign(n, 0);
+        for (uint32_t i = 0; i < n; i++) {
+            const uint64_t c = key[i] >> 22;
+            if (C.empty() || C.back() != c) C.push_back(c);
+            sel[key[i] & ((1u << 22) - 1)] = (uint32_t)(C.size() - 1);
+        }
+        S.pt.mark("c.sort");
+        return run_hook(S, false);  // the next job's roll, if its tables are built
+    }
     C.resize(n);
     memcpy(C.data(), sl.list.p, (size_t)n * 8);
     sort_offsets(C);
     C.erase(std::unique(C.begin(), C.end()), C.end());
     sel.clear();
     const size_t i0 = std::lower_bound(C.begin(), C.end(), pos) - C.begin();
-    if (i0 < C.size() && (int64_t)C[i0] < S.end) {
-        Walker w;
-        w.end = S.end;
-        w.size = S.size;
-        w.head = S.head;
-        if (w.spec) {
-            const std::vector<int32_t> unknown(C.size(), -2);
-            w.spec_batch(C, unknown, i0, sel);
-        } else {
-            for (size_t j = i0; j < C.size() && (int64_t)C[j] < S.end; j++) sel.push_back((uint32_t)j);
-        }
-    }
+    if (i0 < C.size() && (int64_t)C[i0] < S.end) w.spec_batch(C, std::vector<int32_t>(C.size(), -2), i0, sel);
     S.pt.mark("c.select");
-    const uint32_t m = (uint32_t)sel.size();
+    std::vector<uint64_t> so(sel.size());
+    for (size_t k = 0; k < sel.size(); k++) so[k] = C[sel[k]];
+    if ((s = queue_confirm(S, so.data(), (uint32_t)so.size())) != RSG_OK) return s;
+    return run_hook(S, false);  // the next job's roll, if its tables are built
+}
+
+// Queue the confirmation of the m windows at offsets off[0..m) (host memory,
+// copied to the slot's pinned buffer unless it is that buffer or the roll's
+// list): plan built on the GPU, block sums, resolve, results to pinned
+// memory in off[] order; event `confirmed` behind them.
+rsg_status queue_confirm(Search &S, const uint64_t *off, uint32_t m) {
+    rsg_ctx *ctx = S.ctx;
+    SearchSlot &sl = *S.sl;
+    rsg_status s;
     if (ctx->timing) ctx->stat_windows += m;
     if (m) {
         HostPlan plan;
@@ -502,9 +541,12 @@ rsg_status confirm_all(Search &S, uint32_t n, uint64_t pos, std::vector<uint64_t
         plan.lds_reserve = S.confirm_lds;
         if ((s = need_resolve_tables(S)) != RSG_OK) return s;
         S.pt.mark("c.partb");
-        if ((s = ensure_pin(ctx, sl.sel, (uint64_t)m * 8)) != RSG_OK) return s;
-        uint64_t *so = (uint64_t *)sl.sel.p;
-        for (uint32_t k = 0; k < m; k++) so[k] = C[sel[k]];
+        const uint64_t *so = off;
+        if (off != (const uint64_t *)sl.list.p) {  // the GPU reads the offsets from pinned memory
+            if ((s = ensure_pin(ctx, sl.sel, (uint64_t)m * 8)) != RSG_OK) return s;
+            memcpy(sl.sel.p, off, (size_t)m * 8);
+            so = (const uint64_t *)sl.sel.p;
+        }
         if ((s = ensure_dev(ctx, ctx->d_files, (uint64_t)m * sizeof(DevFile) + 32)) != RSG_OK) return s;
         if ((s = ensure_dev(ctx, ctx->d_wg, ((uint64_t)plan.nwg + 1) * sizeof(uint32_t) + 4)) != RSG_OK) return s;
         if ((s = ensure_dev(ctx, ctx->d_out[0], (uint64_t)m * kRecordBytes)) != RSG_OK) return s;
@@ -526,7 +568,7 @@ rsg_status confirm_all(Search &S, uint32_t n, uint64_t pos, std::vector<uint64_t
     if (!sl.confirmed) RSG_HIP(ctx, hipEventCreateWithFlags(&sl.confirmed, sync_event_flags()));
     RSG_HIP(ctx, hipEventRecord(sl.confirmed, S.cst));
     S.pt.mark("c.launch");
-    return run_hook(S, false);  // the next job's roll, if its tables are built
+    return RSG_OK;
 }
 
 // The rest of a confirm_all job, after its confirmation was queued: wait for
@@ -1511,6 +1553,7 @@ rsg_status rsg_testing_walk(const uint64_t *cand, uint64_t n, const int32_t *tru
     w.size = size;
     w.head = *head;
     w.out = &found;
+    if (stats[0] == 1 || stats[0] == 2) w.spec = stats[0] == 1;  // on input: the selection mode (0 = RSG_CONFIRM_SPEC)
     w.verify = [truth](const std::vector<uint32_t> &idx, std::vector<int32_t> &res) {
         for (uint32_t k : idx) res[k] = truth[k];
         return RSG_OK;

@@ -14,14 +14,16 @@ import pytest
 from rsync_amd import _lib
 
 
-def walk(cand, truth, size, head):
+def walk(cand, truth, size, head, spec=0):
+    """spec: 1 = speculative selection of sparse batches, 2 = every pending
+    candidate, 0 = the library's default (RSG_CONFIRM_SPEC)."""
     cand = np.ascontiguousarray(cand, np.uint64)
     truth = np.ascontiguousarray(truth, np.int32)
     h = _lib.SumHead(*head)
     cap = max(1, cand.size)
     out = (_lib.Match * cap)()
     n = ctypes.c_uint64()
-    stats = (ctypes.c_uint64 * 2)()
+    stats = (ctypes.c_uint64 * 2)(spec, 0)
     _lib.check(_lib.lib.rsg_testing_walk(cand.ctypes.data, cand.size, truth.ctypes.data, size,
                                          ctypes.byref(h), out, cap, ctypes.byref(n), stats))
     return [(out[k].offset, out[k].index) for k in range(n.value)], stats[0], stats[1]
@@ -152,7 +154,7 @@ def test_sparse_speculative_selection(seed):
     list is the greedy walk's.  Isolated true matches (one-block runs) and
     false hits that happen to be chained cost at most a few extra trips."""
     cand, truth, size, head = _cfg3_like(seed)
-    got, trips, windows = walk(cand, truth, size, head)
+    got, trips, windows = walk(cand, truth, size, head, spec=1)
     want = reference_walk(cand, truth, size, head)
     assert got == want
     # visited offsets: every match plus the false hits outside matched spans
@@ -181,6 +183,18 @@ def test_sparse_speculation_wrong_chains():
     inner = base + 17  # visited after the pair's first candidate fails
     cand = np.unique(np.concatenate([pairs, inner])).astype(np.uint64)
     truth = np.where(np.isin(cand, inner), 3, -1).astype(np.int32)
-    got, trips, windows = walk(cand, truth, size, head)
+    got, trips, windows = walk(cand, truth, size, head, spec=1)
     assert got == reference_walk(cand, truth, size, head)
     assert windows <= 2 * cand.size
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_sparse_every_candidate_one_round_trip(seed):
+    """The default sparse batch (no speculation): every candidate of the
+    stretch is confirmed in the one round trip, so the walk never waits for
+    another, and the match list is the greedy walk's."""
+    cand, truth, size, head = _cfg3_like(seed)
+    got, trips, windows = walk(cand, truth, size, head, spec=2)
+    assert got == reference_walk(cand, truth, size, head)
+    assert trips == 1
+    assert windows == cand.size
