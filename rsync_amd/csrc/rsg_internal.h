@@ -104,7 +104,13 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
                        const uint32_t *bitmap, const uint16_t *filter16, const uint64_t *table,
                        const uint32_t *table_keys, uint32_t bmask, uint64_t *cand, uint32_t cap, uint32_t *count,
-                       uint32_t grid, bool fused, hipStream_t stream);
+                       const uint32_t *ovf, uint32_t grid, bool fused, hipStream_t stream);
+// The roll's tables (bitmap, filter16 if packed, bucket table of nb buckets
+// and its key-only copy) built on the GPU from sum1[0..count), into zeroed
+// memory; *ovf = 1 if some key found no slot (rsg_match_kernels.hip).
+hipError_t launch_build_tables(const uint32_t *sum1, int32_t count, uint32_t B, uint32_t rem, bool packed,
+                               uint32_t *bitmap, uint16_t *filter16, uint64_t *table, uint32_t *keys, uint32_t nb,
+                               uint32_t *ovf, hipStream_t stream);
 // The packed roll's filter (roll_packed_kernel, fused mode, interior tiles):
 // 2^16 16-bit words, word ((s1 + 128 B) xor s2) mod 2^16, bits s2[0..3],
 // s2[4..7] and (by default) s2[8..11].  s1 of a long window of random bytes is

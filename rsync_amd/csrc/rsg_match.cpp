@@ -109,6 +109,8 @@ struct Search {
     std::function<rsg_status()> tail;        // set by finish(): the rest of the job (wait + walk), any thread
     // device tables inside the slot's blob
     uint64_t off_filter = 0, off_filter16 = 0, off_table = 0, off_keys = 0, blob_a_bytes = 0;  // part A
+    bool gpu_tab = false;   // part A built on the GPU from the Sum1 copy at off_sum1 (tables_roll)
+    uint64_t off_sum1 = 0;
     uint64_t off_groups = 0, off_hi16 = 0, off_sum2 = 0, blob_bytes = 0;                       // part B
     std::future<rsg_status> part_b;  // part B's build (a worker's), if not done inline
     bool part_b_up = false;          // part B's upload is queued
@@ -596,6 +598,16 @@ rsg_status confirm_all_tail(Search &S, const std::vector<uint64_t> &C, const std
 // roll can start before part B exists.  Part B is what the confirmation's
 // resolve reads: basis sums grouped by Sum1 in targets order, their sum2s.
 // Blob layout: filter | filter16 | table | keys | groups | hi16 | sum2.
+// RSG_GPU_TABLES=0 (A/B): part A built on the host (the first job of a
+// batch waited ~0.5 ms for it with the GPU idle, r05t)
+static bool gpu_tables_on() {
+    static const bool on = [] {
+        const char *e = getenv("RSG_GPU_TABLES");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 rsg_status tables_roll(Search &S, const uint32_t *sum1, const int32_t *targets) {
     (void)targets;
     rsg_ctx *ctx = S.ctx;
@@ -608,11 +620,38 @@ rsg_status tables_roll(Search &S, const uint32_t *sum1, const int32_t *targets) 
     const uint64_t ntiles64 = (S.size + kScanTile - 1) / kScanTile;
     if (ntiles64 >= 0xFFFFFFF0ull) return fail(ctx, RSG_ERR_INVALID, "source too large");
     S.ntiles = (uint32_t)ntiles64;
+    auto up = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
+    const bool packed = (uint32_t)B <= rsg::kFusedMaxB && rsg::roll_packed();
+    if (gpu_tables_on() && count > 0) {
+        // the same blob layout, filled by build_tables_kernel (enqueue_scan)
+        // from a copy of the Sum1 array; at least two buckets per key
+        uint32_t nb = 16;
+        while (nb < 2u * (uint32_t)count) nb <<= 1;
+        S.bmask = nb - 1;
+        S.gpu_tab = true;
+        const uint64_t n_filter = rsg::kFilterBits / 8, n_filter16 = packed ? rsg::kFilter16Words * 2ull : 0;
+        const uint64_t n_table = (uint64_t)nb * rsg::kBucketWays * 8, n_keys = (uint64_t)nb * rsg::kBucketWays * 4;
+        S.off_filter = 0;
+        S.off_filter16 = up(n_filter);
+        S.off_table = S.off_filter16 + up(n_filter16);
+        S.off_keys = S.off_table + up(n_table);
+        S.off_sum1 = S.off_keys + up(n_keys);
+        S.blob_a_bytes = S.off_sum1 + up((uint64_t)count * 4);
+        S.off_groups = S.blob_a_bytes;
+        S.off_hi16 = S.off_groups + up((uint64_t)count * 8);
+        S.off_sum2 = S.off_hi16 + up(65537ull * 4);
+        S.blob_bytes = S.off_sum2 + up((uint64_t)count * 16);
+        rsg_status s;
+        if ((s = ensure_pin(ctx, sl.stage, S.blob_bytes)) != RSG_OK) return s;
+        memcpy((uint8_t *)sl.stage.p + S.off_sum1, sum1, (size_t)count * 4);
+        S.pt.mark("tables");
+        return RSG_OK;
+    }
+    S.gpu_tab = false;
     // the filters on a second thread (they need only the sums; bits set per
     // block, a repeated Sum1 sets the same bits)
     auto &bitmap = T.bitmap;
     auto &filter16 = T.filter16;  // the packed roll's filter (interior tiles of the fused mode)
-    const bool packed = (uint32_t)B <= rsg::kFusedMaxB && rsg::roll_packed();
     std::thread filters([&] {
         bitmap.assign(rsg::kFilterBits / 32, 0);
         filter16.clear();
@@ -677,10 +716,11 @@ rsg_status tables_roll(Search &S, const uint32_t *sum1, const int32_t *targets) 
         const uint64_t e = table[i];
         tkeys[i] = (uint32_t)e != 0 ? (uint32_t)(e >> 32) : first_key;  // empty slots: a key that exists
     }
+    S.pt.mark("t.table");
     filters.join();
+    S.pt.mark("t.filt");
     // blob layout, 256-byte aligned parts; the whole blob is sized here so
     // part B never regrows the stage under part A's upload
-    auto up = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
     const uint64_t n_filter = bitmap.size() * 4, n_table = table.size() * 8, n_filter16 = filter16.size() * 2;
     const uint64_t n_groups = (uint64_t)count * 8, n_hi16 = 65537ull * 4, n_sum2 = (uint64_t)count * 16;
     S.off_filter = 0;
@@ -764,7 +804,8 @@ rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
     if ((s = ensure_dev(ctx, sl.counts, 64)) != RSG_OK) return s;
     if ((s = ensure_pin(ctx, sl.count, 64)) != RSG_OK) return s;
     if (sl.counts_zeroed != sl.counts.p) {  // a new counter: zero once (each roll's count_out re-zeroes it)
-        RSG_HIP(ctx, hipMemsetAsync(sl.counts.p, 0, 4, S.st));
+        // (word 1: the GPU table build's overflow flag)
+        RSG_HIP(ctx, hipMemsetAsync(sl.counts.p, 0, 8, S.side));
         sl.counts_zeroed = sl.counts.p;
     }
     if ((s = ensure_dev(ctx, sl.blob, S.blob_bytes)) != RSG_OK) return s;
@@ -784,7 +825,21 @@ rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
     // The tables' upload (~1.7 MB for a 32 768-block basis) goes on the side
     // stream too: on the compute stream it sat between two files' rolls
     // (≈ 50 µs of PCIe per file in the batch timeline).
-    RSG_HIP(ctx, hipMemcpyAsync(sl.blob.p, sl.stage.p, S.blob_a_bytes, hipMemcpyHostToDevice, S.side));
+    if (S.gpu_tab) {
+        // the Sum1 copy up, the filters and table zeroed, then built in place
+        uint8_t *b = (uint8_t *)sl.blob.p;
+        RSG_HIP(ctx, hipMemcpyAsync(b + S.off_sum1, (const uint8_t *)sl.stage.p + S.off_sum1,
+                                    (uint64_t)S.head.count * 4, hipMemcpyHostToDevice, S.side));
+        RSG_HIP(ctx, hipMemsetAsync(b, 0, S.off_keys, S.side));
+        RSG_HIP(ctx, hipMemsetAsync((uint32_t *)sl.counts.p + 1, 0, 4, S.side));
+        RSG_HIP(ctx, rsg::launch_build_tables(
+                         (const uint32_t *)(b + S.off_sum1), S.head.count, (uint32_t)S.head.block_len,
+                         (uint32_t)S.head.rem, S.off_table > S.off_filter16, (uint32_t *)(b + S.off_filter),
+                         (uint16_t *)(b + S.off_filter16), (uint64_t *)(b + S.off_table), (uint32_t *)(b + S.off_keys),
+                         S.bmask + 1, (uint32_t *)sl.counts.p + 1, S.side));
+    } else {
+        RSG_HIP(ctx, hipMemcpyAsync(sl.blob.p, sl.stage.p, S.blob_a_bytes, hipMemcpyHostToDevice, S.side));
+    }
     RSG_HIP(ctx, hipEventRecord(sl.scanned, S.side));  // also orders the realigning copy and the upload
     const uint8_t *blob = (const uint8_t *)sl.blob.p;
     S.d_groups = (const uint2 *)(blob + S.off_groups);
@@ -816,7 +871,7 @@ rsg_status launch_range(Search &S, uint32_t lo, uint32_t hi) {
     RSG_HIP(ctx, rsg::launch_roll(S.d_src, S.size, (uint32_t)S.head.block_len, (uint32_t)S.head.rem, (uint64_t)S.end,
                                   lo, hi, (const TileAgg *)sl.agg.p, (const TilePrefix *)sl.prefix.p, S.ntiles,
                                   S.d_filter, S.d_filter16, S.d_table, S.d_table_keys, S.bmask, (uint64_t *)sl.list.p, kCandCap,
-                                  (uint32_t *)sl.counts.p, S.cus, S.fused, S.st));
+                                  (uint32_t *)sl.counts.p, (const uint32_t *)sl.counts.p + 1, S.cus, S.fused, S.st));
     timed_end(ctx, t0, S.st, 0);
     RSG_HIP(ctx, rsg::launch_roll_count_out((uint32_t *)sl.counts.p, (uint32_t *)sl.count.p, S.st));
     RSG_HIP(ctx, hipEventRecord(sl.rolled, S.st));
@@ -932,6 +987,25 @@ bool job_local(rsg_status s) { return s == RSG_ERR_INVALID || s == RSG_ERR_TRUNC
 // builds job i+2's tables during confirm(i).  Two files' kernels never share
 // the CUs except the memory-bound prefix pass: a confirmation kernel (few
 // lanes, serial MD4 chains) beside a roll kernel ran 3x slower.
+// RSG_START_SERIAL=0 (A/B): the first two jobs' tables build side by side
+// before job 0's roll is queued
+static bool start_serial() {
+    static const bool on = [] {
+        const char *e = getenv("RSG_START_SERIAL");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// RSG_START_INLINE=0 (A/B): job 0's roll tables on a worker thread too
+static bool start_inline() {
+    static const bool on = [] {
+        const char *e = getenv("RSG_START_INLINE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed, bool host_src) {
     if (njobs && !jobs) return fail(ctx, RSG_ERR_INVALID, "NULL jobs");
     PhaseTimer bt;  // RSG_TIMING: the call's start-up and drain
@@ -1005,7 +1079,9 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
         std::unique_ptr<Search> S;
         std::future<rsg_status> tab;
     } pends[2];  // job i is prepared into pends[i & 1]
-    auto prepare = [&](uint64_t i) -> rsg_status {
+    // inline_a: part A on this thread (job 0 of a serial start: the caller
+    // waits for it next anyway, and a fresh worker thread built it ~2x slower)
+    auto prepare = [&](uint64_t i, bool inline_a = false) -> rsg_status {
         rsg_search_job &j = jobs[i];
         const int slot = (int)(i % kSearchSlots);
         live[slot].reset();  // job i - 3 of this slot was finished, its GPU work waited for
@@ -1041,11 +1117,19 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
         // job's first confirmation
         auto part_a = std::make_shared<std::promise<rsg_status>>();
         pend.tab = part_a->get_future();
-        raw->part_b = std::async(std::launch::async, [raw, &j, part_a] {
+        if (inline_a) {
             const rsg_status sa = tables_roll(*raw, j.sum1, j.targets);
             part_a->set_value(sa);
-            return sa != RSG_OK ? sa : tables_resolve(*raw, j.sum1, j.sum2, j.targets);
-        });
+            raw->part_b = std::async(std::launch::async, [raw, &j, sa] {
+                return sa != RSG_OK ? sa : tables_resolve(*raw, j.sum1, j.sum2, j.targets);
+            });
+        } else {
+            raw->part_b = std::async(std::launch::async, [raw, &j, part_a] {
+                const rsg_status sa = tables_roll(*raw, j.sum1, j.targets);
+                part_a->set_value(sa);
+                return sa != RSG_OK ? sa : tables_resolve(*raw, j.sum1, j.sum2, j.targets);
+            });
+        }
         pend.S = std::move(S);
         pend.i = i;
         pend.valid = true;
@@ -1078,6 +1162,14 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
     uint64_t i = 0;
     if (!overlap) {
         if (njobs) fatal = start(0);
+    } else if (start_serial()) {
+        // job 0 alone first: its roll queues as soon as its own tables are
+        // built (built beside job 1's they took twice as long, and the GPU
+        // idles until then); job 1's tables build while roll 0 runs
+        fatal = prepare(0, start_inline());
+        if (fatal == RSG_OK) fatal = issue(0);
+        if (fatal == RSG_OK && njobs > 1) fatal = prepare(1);
+        if (fatal == RSG_OK && njobs > 1) fatal = issue(1);
     } else {  // the first two jobs' tables build side by side
         for (uint64_t k = 0; k < std::min<uint64_t>(njobs, 2) && fatal == RSG_OK; k++) fatal = prepare(k);
         for (uint64_t k = 0; k < std::min<uint64_t>(njobs, 2) && fatal == RSG_OK; k++) fatal = issue(k);
@@ -1299,6 +1391,8 @@ rsg_status search_fd(rsg_ctx *ctx, int32_t fd, int64_t off0, uint64_t size, cons
             S.off_table = T->off_table;
             S.off_keys = T->off_keys;
             S.blob_a_bytes = T->blob_a_bytes;
+            S.gpu_tab = T->gpu_tab;
+            S.off_sum1 = T->off_sum1;
             S.off_groups = T->off_groups;
             S.off_hi16 = T->off_hi16;
             S.off_sum2 = T->off_sum2;

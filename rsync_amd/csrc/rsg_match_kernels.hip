@@ -275,7 +275,8 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
     uint32_t tile_hi, const TileAgg *__restrict__ agg, const TilePrefix *__restrict__ pre, uint32_t ntiles,
     const uint32_t *__restrict__ bitmap_g, const uint64_t *__restrict__ table, uint32_t bmask,
-    uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count, uint32_t fused) {
+    uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count, uint32_t fused,
+    const uint32_t *__restrict__ ovf) {
     constexpr uint32_t kWaves = kRollThreads / 64;
     constexpr uint32_t P = kRollPerThread;     // offsets per lane
     constexpr int OW = (int)P / 4;             // words of a lane's own bytes
@@ -292,6 +293,9 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     const uint32_t Bt = B / kScanTile;
     const TilePrefix tot = fused ? TilePrefix{0, 0} : pre[ntiles];
     const uint32_t rem_flag = (rem != 0 && rem != B) ? 4u : 2u;
+    // a table the GPU build could not complete (build_tables_kernel): every
+    // filter hit is a candidate, the confirmation sorts them out
+    const uint32_t all_flags = __builtin_amdgcn_readfirstlane(*ovf) ? 7u : 0u;
     uint32_t parity = 0;
 
     // Exact probes of a wave's parked hits (one queue half = one tile); true
@@ -301,7 +305,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_kernel(
     auto probe = [&](uint64_t q, uint32_t sum, uint32_t fl) {
         const uint32_t k = (uint32_t)min<uint64_t>((uint64_t)B, size - q);
         const uint32_t need = (k == B) ? 2u : ((k == rem) ? rem_flag : 0u);
-        if (fl & need) {
+        if ((fl | all_flags) & need) {
             const uint32_t at = atomicAdd(count, 1u);
             if (at < cap) cand[at] = q;
         }
@@ -663,7 +667,8 @@ template <int NBITS, bool EDGE, bool BT>
 __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     const uint8_t *__restrict__ src, uint64_t size, uint32_t B, uint32_t rem, uint64_t end, uint32_t tile_lo,
     uint32_t t_int, uint32_t tile_hi, const uint16_t *__restrict__ filter_g, const uint32_t *__restrict__ keys,
-    uint32_t bmask, uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count) {
+    uint32_t bmask, uint64_t *__restrict__ cand, uint32_t cap, uint32_t *__restrict__ count,
+    const uint32_t *__restrict__ ovf) {
     constexpr uint32_t kWaves = kRollThreads / 64;
     constexpr uint32_t P = kRollPerThread;  // offsets per lane (2 streams of P/2)
     constexpr int OW = (int)P / 4;
@@ -683,6 +688,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t C128 = (128u * B) & 0xffffu;  // the filter index offset of P1
+    const bool all = __builtin_amdgcn_readfirstlane(*ovf) != 0;  // incomplete table (roll_kernel's all_flags)
     uint32_t parity = 0;
 
     // Exact probes of a wave's parked hits: the window at q (length k =
@@ -690,7 +696,7 @@ __global__ __launch_bounds__(kRollThreads) void roll_packed_kernel(
     // is a basis Sum1 and some block has length k.
     auto probe = [&](uint64_t q, bool present) {
         const uint32_t k = (uint32_t)min<uint64_t>((uint64_t)B, size - q);
-        if (present && (k == B || k == rem)) {
+        if ((present || all) && (k == B || k == rem)) {
             const uint32_t at = atomicAdd(count, 1u);
             if (at < cap) cand[at] = q;
         }
@@ -1214,6 +1220,103 @@ bool roll_filter_sel() {
     return sel;
 }
 
+// ------------------------------------------------------------- roll tables
+// Part A of the basis tables (rsg_match.cpp: tables_roll) built on the GPU
+// from the uploaded Sum1 array, one lane per block k: the Bloom filter bits,
+// the packed roll's 16-bit filter bits and the 2-choice bucket table entry
+// {Sum1 << 32 | flags} (flags: 1, and 2 = a block of length B, 4 = the
+// shorter last block).  An entry goes into the first free slot of the less
+// filled bucket by a 64-bit CAS (slots fill in order, so a scan stops at the
+// first empty one); an equal key already present gets its flags OR-ed in,
+// as the host build merges them.  Both buckets full: *ovf = 1, and the rolls
+// take every filter hit as a candidate (the confirmation and resolve, from
+// the host-built exact groups, keep the result exact).  The table has at
+// least 2 buckets per key (4 ways each), so that is reserved for pathological
+// key sets.
+__global__ __launch_bounds__(256) void build_tables_kernel(const uint32_t *__restrict__ sum1, int32_t count,
+                                                           uint32_t B, uint32_t rem, int nbits, int sel, int packed,
+                                                           uint32_t *__restrict__ bitmap,
+                                                           uint32_t *__restrict__ filter16w,
+                                                           unsigned long long *__restrict__ table, uint32_t bmask,
+                                                           uint32_t *__restrict__ ovf) {
+    const int32_t k = (int32_t)(blockIdx.x * 256u + threadIdx.x);
+    if (k >= count) return;
+    const uint32_t v = sum1[k];
+    if (sel) {
+        atomicOr(&bitmap[sel_word(v)], sel_mask(v));
+    } else {
+        const uint32_t h = filter_hash(v);
+        atomicOr(&bitmap[filter_word(h)], filter_mask(h));
+    }
+    if (packed) {
+        const uint32_t w = f16_word(v, B);
+        atomicOr(&filter16w[w >> 1], (f16_mask(v, nbits) & 0xffffu) << (16u * (w & 1u)));
+    }
+    const uint32_t len = (k == count - 1 && rem != 0) ? rem : B;  // types.go: the last block may be short
+    const unsigned long long f = 1u | (len == B ? 2u : 4u);
+    const unsigned long long e = ((unsigned long long)v << 32) | f;
+    const uint32_t hb[2] = {bucket_hash1(v) & bmask, bucket_hash2(v) & bmask};
+    const int nbk = hb[1] == hb[0] ? 1 : 2;
+    for (int attempt = 0; attempt < 64; attempt++) {
+        uint32_t fill[2] = {kBucketWays, kBucketWays};
+        for (int b = 0; b < nbk; b++) {
+            unsigned long long *bk = table + (uint64_t)hb[b] * kBucketWays;
+            uint32_t i = 0;
+            for (; i < kBucketWays; i++) {
+                const unsigned long long x = __hip_atomic_load(&bk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (x == 0) break;
+                if ((uint32_t)(x >> 32) == v) {
+                    atomicOr(&bk[i], f);
+                    return;
+                }
+            }
+            fill[b] = i;
+        }
+        const int b = (nbk == 2 && fill[1] < fill[0]) ? 1 : 0;
+        if (fill[b] >= kBucketWays) break;
+        unsigned long long *slot = table + (uint64_t)hb[b] * kBucketWays + fill[b];
+        const unsigned long long old = atomicCAS(slot, 0ull, e);
+        if (old == 0) return;
+        if ((uint32_t)(old >> 32) == v) {
+            atomicOr(slot, f);
+            return;
+        }
+        // another key took the slot: scan again
+    }
+    atomicOr(ovf, 1u);
+}
+
+// The packed roll's key-only copy of the table (empty slots: an existing key).
+__global__ __launch_bounds__(256) void table_keys_kernel(const unsigned long long *__restrict__ table, uint32_t n,
+                                                         const uint32_t *__restrict__ sum1,
+                                                         uint32_t *__restrict__ keys) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long e = table[i];
+    keys[i] = (uint32_t)e != 0 ? (uint32_t)(e >> 32) : sum1[0];
+}
+
+hipError_t launch_build_tables(const uint32_t *sum1, int32_t count, uint32_t B, uint32_t rem, bool packed,
+                               uint32_t *bitmap, uint16_t *filter16, uint64_t *table, uint32_t *keys, uint32_t nb,
+                               uint32_t *ovf, hipStream_t stream) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(build_tables_kernel, dim3(((uint32_t)count + 255) / 256), dim3(256), 0, stream, sum1, count, B,
+                       rem, roll_filter_bits(), roll_filter_sel() ? 1 : 0, packed ? 1 : 0, bitmap,
+                       reinterpret_cast<uint32_t *>(filter16), reinterpret_cast<unsigned long long *>(table), nb - 1,
+                       ovf);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint32_t n = nb * kBucketWays;
+    hipLaunchKernelGGL(table_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, stream,
+                       reinterpret_cast<const unsigned long long *>(table), n, sum1, keys);
+    e = hipGetLastError();
+    // RSG_TESTING_TABLE_OVF=1: report an incomplete table anyway (tests of
+    // the rolls' every-filter-hit fallback)
+    static const bool force = getenv("RSG_TESTING_TABLE_OVF") != nullptr;
+    if (e == hipSuccess && force) e = hipMemsetAsync(ovf, 1, 4, stream);
+    return e;
+}
+
 __global__ void roll_count_out_kernel(uint32_t *__restrict__ count, uint32_t *__restrict__ host) {
     if (threadIdx.x == 0) {
         *host = *count;  // pinned host word, read by the host after the stream's event
@@ -1230,7 +1333,7 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                        uint32_t tile_hi, const TileAgg *agg, const TilePrefix *pre, uint32_t ntiles,
                        const uint32_t *bitmap, const uint16_t *filter16, const uint64_t *table,
                        const uint32_t *table_keys, uint32_t bmask, uint64_t *cand, uint32_t cap, uint32_t *count,
-                       uint32_t grid, bool fused, hipStream_t stream) {
+                       const uint32_t *ovf, uint32_t grid, bool fused, hipStream_t stream) {
     if (tile_hi <= tile_lo) return hipSuccess;
     if (fused && filter16) {
         // Interior tiles [tile_lo, t_int): every offset of tile t visited
@@ -1250,12 +1353,12 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
                 auto kern = roll_filter_bits() == 3 ? (bt ? roll_packed_kernel<3, true, true> : roll_packed_kernel<3, true, false>)
                                                     : (bt ? roll_packed_kernel<2, true, true> : roll_packed_kernel<2, true, false>);
                 hipLaunchKernelGGL(kern, dim3(ga), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
-                                   t_int, tile_hi, filter16, table_keys, bmask, cand, cap, count);
+                                   t_int, tile_hi, filter16, table_keys, bmask, cand, cap, count, ovf);
                 return hipGetLastError();
             }
             auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, false, false> : roll_packed_kernel<2, false, false>;
             hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, t_int,
-                               t_int, filter16, table_keys, bmask, cand, cap, count);
+                               t_int, filter16, table_keys, bmask, cand, cap, count, ovf);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -1265,7 +1368,7 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
     const uint32_t g = min(grid, tile_hi - tile_lo);
     auto kern = roll_filter_sel() ? roll_kernel<true> : roll_kernel<false>;
     hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, tile_hi, agg,
-                       pre, ntiles, bitmap, table, bmask, cand, cap, count, fused ? 1u : 0u);
+                       pre, ntiles, bitmap, table, bmask, cand, cap, count, fused ? 1u : 0u, ovf);
     return hipGetLastError();
 }
 

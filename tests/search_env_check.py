@@ -1,0 +1,53 @@
+"""Run by tests/test_gpu_match.py in a child process, so that switches the
+library reads once per process (RSG_GPU_TABLES, RSG_TESTING_TABLE_OVF,
+RSG_CONFIRM_SPEC) take effect: the golden match cases and seeded random
+searches through the C-ABI against the C oracle.  Prints "ok <n>" on success,
+raises on the first mismatch."""
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
+
+import cases  # noqa: E402
+from oracle import oracle as orc  # noqa: E402
+
+
+def main():
+    import rsync_amd
+    eng = rsync_amd.Engine(0)
+    gold = json.load(open(os.path.join(HERE, "golden", "match_cases.json")))
+    n = 0
+    for name, (src, basis, blen, seed) in sorted(cases.match_cases().items()):
+        head = orc.sum_head(basis.size, blen)
+        if head[0]:
+            s1, s2 = orc.parse_records(orc.block_sums(basis, blen, seed))
+        else:
+            s1, s2 = np.zeros(0, np.uint32), np.zeros((0, 16), np.uint8)
+        got = eng.hash_search(src, head, s1, s2, orc.stable_targets(s1), seed)
+        assert [list(m) for m in got] == gold[name]["matches"], name
+        n += 1
+    for k in range(6):
+        rng = np.random.default_rng(300 + k)
+        size = int(rng.integers(1, 3_000_000))
+        basis = cases.splitmix64_bytes(900 + k, size)
+        src = cases.mutate(basis, 950 + k, float(rng.uniform(0, 0.6)), 1, 70000,
+                           n_ins=int(rng.integers(0, 5)), n_del=int(rng.integers(0, 5)))
+        blen = int(rng.choice([0, 700, 4096, 32768]))
+        seed = int(rng.integers(-2**31, 2**31))
+        head = orc.sum_head(basis.size, blen)
+        s1, s2 = orc.parse_records(orc.block_sums(basis, blen, seed))
+        tg = orc.stable_targets(s1)
+        want, _, _ = orc.hash_search(src, head, s1, s2, tg, seed)
+        assert eng.hash_search(src, head, s1, s2, tg, seed) == want, k
+        n += 1
+    eng.close()
+    print("ok", n)
+
+
+if __name__ == "__main__":
+    main()

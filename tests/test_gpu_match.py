@@ -389,3 +389,20 @@ def test_receive_data_batch_mixed_sizes(eng):
     for k, (st, data, used) in enumerate(got):
         if st == _lib.OK:
             assert data == orc.receive_data(jobs[k][0], jobs[k][1], jobs[k][2], seed)[0], k
+
+
+@pytest.mark.parametrize("env", [{"RSG_GPU_TABLES": "0"}, {"RSG_TESTING_TABLE_OVF": "1"}, {"RSG_CONFIRM_SPEC": "1"}],
+                         ids=["host_tables", "table_overflow_fallback", "speculative_selection"])
+def test_search_modes_vs_oracle(env):
+    """The search's other modes, each in a child process (the library reads
+    these switches once): roll tables built on the host; a GPU-built table
+    reported incomplete, so the rolls pass every filter hit on as a candidate
+    and the confirmation alone decides; the speculative confirmation batches.
+    Golden cases and random searches against the oracle in every mode."""
+    import subprocess
+    import sys
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "search_env_check.py")
+    r = subprocess.run([sys.executable, script], env={**os.environ, **env}, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert r.stdout.strip().startswith("ok"), r.stdout
