@@ -987,6 +987,16 @@ bool job_local(rsg_status s) { return s == RSG_ERR_INVALID || s == RSG_ERR_TRUNC
 // builds job i+2's tables during confirm(i).  Two files' kernels never share
 // the CUs except the memory-bound prefix pass: a confirmation kernel (few
 // lanes, serial MD4 chains) beside a roll kernel ran 3x slower.
+// RSG_LAST_OWN=0 (A/B): the last job's confirmation on the confirmation
+// stream too, behind the previous job's
+static bool last_own() {
+    static const bool on = [] {
+        const char *e = getenv("RSG_LAST_OWN");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // RSG_START_SERIAL=0 (A/B): the first two jobs' tables build side by side
 // before job 0's roll is queued
 static bool start_serial() {
@@ -1104,6 +1114,14 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
             S->cst = ctx->confirm;
             S->roll_grid = (uint32_t)std::max(1, dev_cus - spare);
             S->confirm_lds = 8192;
+            if (i + 1 == njobs && last_own()) {
+                // the last job's confirmation has no roll to share the chip
+                // with: it queues behind its own roll on the roll stream and
+                // runs beside job i-1's, instead of after it (the drain was
+                // confirm(n-2)'s rest + confirm(n-1), r05q trace)
+                S->cst = ctx->side[0];
+                S->confirm_lds = 0;
+            }
         }
         S->side = ctx->side[1];
         S->copy = ctx->stream;
