@@ -422,7 +422,8 @@ template <int KIND>
 __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
-    constexpr bool UNAL = KIND >= 100;
+    constexpr bool UNAL = (KIND % 1000) >= 100;
+    constexpr bool DB = KIND >= 1000;  // two slabs per wave: segment s+2's DMA issues while s+1 lands
     // nt policy on the DMA: every byte is read once (A/B against the default
     // policy, profiles/r02f_blocklen_sweep_nt.jsonl: B = 4096 0.239 -> 0.219 ms,
     // cfg5 6.48 -> 6.25 ms, B = 1024 and the sender's confirmation unchanged)
@@ -432,12 +433,12 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     constexpr uint32_t kSegBytes = Seg<SEG>::kSegBytes, kUnits = Seg<SEG>::kUnits, kPiece = Seg<SEG>::kPiece;
     constexpr uint32_t kWaveSlab = Seg<SEG>::kWaveSlab, kDmaPerSeg = Seg<SEG>::kDmaPerSeg;
     constexpr uint32_t kChunks = Seg<SEG>::kChunks;
-    __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * kWaveSlab];
+    __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * kWaveSlab * (DB ? 2 : 1)];
     const uint32_t lane = threadIdx.x & 63u;
     // readfirstlane: provably wave-uniform values keep the LDS base (M0) and
     // the buffer descriptor in SGPRs (no waterfall loops around the DMA).
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint8_t *slab = slab_all + wave * kWaveSlab;
+    uint8_t *slab = slab_all + wave * kWaveSlab * (DB ? 2 : 1);
     const uint64_t wave_first = (uint64_t)blockIdx.x * kBlockSumThreads + wave * 64u;
     const uint64_t g = wave_first + lane;
     uint64_t off = 0;
@@ -488,8 +489,9 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
 #define RSG_DMA_SEGMENT(S_)                                                                                      \
     do {                                                                                                         \
         const uint32_t so_ = kSegBytes * (S_);                                                                   \
+        uint8_t *sb_ = slab + (DB ? kWaveSlab * ((S_) & 1u) : 0u);                                               \
         _Pragma("unroll") for (uint32_t i_ = 0; i_ < kDmaPerSeg; i_++)                                           \
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(slab + 1024u * i_), \
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(sb_ + 1024u * i_), \
                                                      16, voff[i_], so_, 0, DMA_AUX);                             \
     } while (0)
 #define RSG_READ_SEGMENT()                                                                                       \
@@ -501,13 +503,49 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
         }                                                                                                        \
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                       \
     } while (0)
-    if (MODE != 2) RSG_DMA_SEGMENT(0);
-    RSG_READ_SEGMENT();
     const uint32_t nfull = n >> 6;
     uint32_t h[4];
     md4_init(h);
     int32_t s1 = 0;
     uint32_t t = 0;
+    if constexpr (DB) {
+        // segment cs sits in slab half cs & 1; at the top of iteration cs the
+        // DMAs of cs and cs+1 are outstanding (vmcnt counts instructions, in
+        // order): wait for cs's, read it, refill its half with cs+2, hash cs
+        if (MODE != 2) {
+            RSG_DMA_SEGMENT(0u);
+            if (S > 1) RSG_DMA_SEGMENT(1u);
+        }
+#pragma unroll 1
+        for (uint32_t cs = 0; cs < S; cs++) {
+            if (cs + 1 < S) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDmaPerSeg) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint8_t *mh = mine + kWaveSlab * (cs & 1u);
+#pragma unroll
+            for (int q = 0; q < (int)(SEG / 16) + (UNAL ? 1 : 0); q++) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(mh + 16 * q);
+                R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (MODE != 2 && cs + 2 < S) RSG_DMA_SEGMENT(cs + 2);
+            if (MODE == 1) {
+#pragma unroll
+                for (int q = 0; q < (int)(SEG / 4); q++) h[q & 3] ^= R[q];
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < kChunks; i++) {
+                    const uint32_t c = kChunks * cs + i;
+                    if (c < nfull) hash_chunk<!UNAL>(R + 16 * i, R[16 * i + 16], sh, c, h, s1, t);
+                    else if (c == nfull) hash_tail<!UNAL>(R + 16 * i, R[16 * i + 16], sh, n, seed, h, s1, t);
+                }
+            }
+        }
+        if (MODE == 0) store_tile_records<2>(out, wave_first / 64, lane, reinterpret_cast<uint32_t *>(slab), n, s1, t, h);
+        else store_record(out, g, n, s1, t, h);
+        return;
+    }
+    if (MODE != 2) RSG_DMA_SEGMENT(0);
+    RSG_READ_SEGMENT();
 #pragma unroll 1
     for (uint32_t cs = 0; cs < S; cs++) {
         const bool more = cs + 1 < S;
@@ -1444,6 +1482,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             case 38: hipLaunchKernelGGL((diag_stream_rw<1, 16>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
             case 39: hipLaunchKernelGGL((diag_stream_rw<1, 32>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
             case 40: hipLaunchKernelGGL((diag_stream_rw<0, 8>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
+            case 43: hipLaunchKernelGGL((block_sums_staged<1011>), grid, block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
+            case 44: hipLaunchKernelGGL((block_sums_staged<1001>), grid, block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
+            case 45: hipLaunchKernelGGL((block_sums_staged<11>), grid, block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
             case 41:
             case 42:
                 if (max_blen <= kRegMaxBytes) {
@@ -1494,7 +1535,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5)) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v == 8 || v == 9)) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
     if ((v == 2 || v == 7) && max_blen > kRegMaxBytes) v = 1;
     if (v == 7 && !aligned) v = 0;
@@ -1525,6 +1566,14 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             break;
         case 5:
             hipLaunchKernelGGL((block_sums_staged<20>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
+                               total_blocks, seed, out);
+            break;
+        case 8:  // 128-byte segments, two slabs per wave
+            hipLaunchKernelGGL((block_sums_staged<1010>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
+                               total_blocks, seed, out);
+            break;
+        case 9:  // 256-byte segments, two slabs per wave
+            hipLaunchKernelGGL((block_sums_staged<1000>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
                                total_blocks, seed, out);
             break;
         case 3: {

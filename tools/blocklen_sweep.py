@@ -33,8 +33,10 @@ SHAPES = [  # (files, file bytes, block length, arenas)
     (256, 4 << 20, 4112, 2),
     (1, 1 << 30, 32768, 2),       # 8: one 1 GiB file at the reference's sizing (B = sqrt(len) = 32768)
 ]
-VARIANTS = {1: "staged", 4: "staged_seg128", 5: "staged_seg512", 2: "park", 3: "long_deep_prefetch"}
-DIAGS = {1: "diag_staged_memory_only", 2: "diag_staged_hash_only", 6: "diag_linear_read_ldsdma"}
+VARIANTS = {1: "staged", 4: "staged_seg128", 5: "staged_seg512", 8: "staged_seg128_db", 9: "staged_db", 2: "park",
+            3: "long_deep_prefetch"}
+DIAGS = {1: "diag_staged_memory_only", 45: "diag_staged_seg128_memory_only", 43: "diag_staged_seg128_db_memory_only",
+         44: "diag_staged_db_memory_only", 2: "diag_staged_hash_only", 6: "diag_linear_read_ldsdma"}
 
 
 def main():
