@@ -204,9 +204,11 @@ __device__ __forceinline__ void store_record_nt(uint8_t *out, uint64_t g, uint32
 // File of block g: the largest f in [wg_file[wg], wg_file[wg+1]] with
 // first_block <= g (zero-length files own no blocks and are skipped).
 // Returns the block's arena offset and length (generator.go:334).
+// wg: the 256-block workgroup slot g belongs to (wg_file's index; the
+// launch's blockIdx.x unless a persistent workgroup loops over slots)
 __device__ __forceinline__ void locate_block(const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file,
-                                             uint64_t g, uint64_t &off, uint32_t &n) {
-    uint32_t lo = wg_file[blockIdx.x], hi = wg_file[blockIdx.x + 1];
+                                             uint64_t g, uint64_t &off, uint32_t &n, uint64_t wg) {
+    uint32_t lo = wg_file[wg], hi = wg_file[wg + 1];
     while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
         if (files[mid].first_block <= g) lo = mid; else hi = mid - 1;
@@ -217,6 +219,10 @@ __device__ __forceinline__ void locate_block(const DevFile *__restrict__ files, 
     const uint64_t left = F.len - boff;
     n = left < F.blen ? (uint32_t)left : F.blen;
     off = F.offset + boff;
+}
+__device__ __forceinline__ void locate_block(const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file,
+                                             uint64_t g, uint64_t &off, uint32_t &n) {
+    locate_block(files, wg_file, g, off, n, blockIdx.x);
 }
 
 // One lane hashes its whole block with its own 16-byte loads (one chunk of
@@ -423,7 +429,8 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
     constexpr bool UNAL = (KIND % 1000) >= 100;
-    constexpr bool DB = KIND >= 1000;  // two slabs per wave: segment s+2's DMA issues while s+1 lands
+    constexpr bool DB = (KIND / 1000) % 2 == 1;  // two slabs per wave: segment s+2's DMA issues while s+1 lands
+    constexpr bool PERSIST = KIND >= 2000;       // each wave loops over 64-block groups (grid = resident waves)
     // nt policy on the DMA: every byte is read once (A/B against the default
     // policy, profiles/r02f_blocklen_sweep_nt.jsonl: B = 4096 0.239 -> 0.219 ms,
     // cfg5 6.48 -> 6.25 ms, B = 1024 and the sender's confirmation unchanged)
@@ -439,11 +446,12 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     // the buffer descriptor in SGPRs (no waterfall loops around the DMA).
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint8_t *slab = slab_all + wave * kWaveSlab * (DB ? 2 : 1);
-    const uint64_t wave_first = (uint64_t)blockIdx.x * kBlockSumThreads + wave * 64u;
+    // one 64-block group: the wave's blocks [wave_first, wave_first + 64)
+    auto group = [&](const uint64_t wave_first) {
     const uint64_t g = wave_first + lane;
     uint64_t off = 0;
     uint32_t n = 0;
-    if (g < total_blocks) locate_block(files, wg_file, g, off, n);
+    if (g < total_blocks) locate_block(files, wg_file, g, off, n, wave_first / kBlockSumThreads);
     const uint32_t sh = UNAL ? (uint32_t)(off & 3u) : 0u;
     const uint64_t loff = off - sh;  // 4-byte aligned fetch start
     const uint32_t nseg = n ? (n >> 6) / kChunks + 1 : 0;  // segments through the tail chunk
@@ -570,6 +578,19 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     // coalesced nontemporal stores, as the park kernel does (round 5)
     if (MODE == 0) store_tile_records<2>(out, wave_first / 64, lane, reinterpret_cast<uint32_t *>(slab), n, s1, t, h);
     else store_record(out, g, n, s1, t, h);
+    };
+    if constexpr (PERSIST) {
+        const uint64_t groups = (total_blocks + 63) / 64, stride = (uint64_t)gridDim.x * (kBlockSumThreads / 64);
+#pragma unroll 1
+        for (uint64_t gw = (uint64_t)blockIdx.x * (kBlockSumThreads / 64) + wave; gw < groups; gw += stride) {
+            group(gw * 64);
+            // the next group's DMA rewrites the slab: the records' LDS
+            // staging reads (store_tile_records) must be done
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+    } else {
+        group((uint64_t)blockIdx.x * kBlockSumThreads + wave * 64u);
+    }
 }
 
 // ---------------------------------------------------------------- read ceilings
@@ -627,20 +648,33 @@ template <int NW, int PER, int DEPTH, int PAT = 0>
 __global__ __launch_bounds__(512) void diag_stream_read(const uint8_t *__restrict__ arena, uint64_t bytes,
                                                            uint32_t *__restrict__ sink) {
     static_assert(PER * DEPTH <= 63 && PER <= 64, "vmcnt cap");
-    static_assert(PAT == 0 || PER == 45, "park tiles are 45 requests");
+    static_assert(PAT != 1 || PER == 45, "park tiles are 45 requests");
+    // PAT 2 / 3: the staged kernel's pattern at B = 4096 -- chunk = 64
+    // pieces of L = 512 / 128 bytes, 4096 bytes apart (segment seg of 64
+    // consecutive 4 KiB blocks); PER = 64 L / 1024 requests
+    constexpr uint32_t L = PAT == 2 ? 512u : 128u, K = 4096u / L, UPP = L / 16u;
+    static_assert(PAT < 2 || PER * 1024 == 64 * L, "one chunk = 64 pieces");
     __shared__ __attribute__((aligned(16))) uint8_t buf[64 * 1024];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave >= NW) return;  // idle waves (a launch of more waves than streams)
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t chunk = PAT ? 64ull * 700 : (uint64_t)PER * 1024;
-    const uint64_t nch = bytes / chunk;
+    const uint64_t chunk = PAT == 1 ? 64ull * 700 : (uint64_t)PER * 1024;
+    const uint64_t nch = PAT >= 2 ? bytes / (64ull * 4096) * K : bytes / chunk;
     const uint32_t G = gridDim.x;
     uint32_t issued = 0;
 #pragma unroll 1
     for (uint64_t c = blockIdx.x + (uint64_t)G * wave; c < nch; c += (uint64_t)G * NW) {
+        const uint64_t at = PAT >= 2 ? (c / K) * (64ull * 4096) + (c % K) * L : c * chunk;
         const __amdgpu_buffer_rsrc_t r =
-            __builtin_amdgcn_make_buffer_rsrc((void *)(arena + rfl64(c * chunk)), (short)0, 0x7FFFFFFF, 0x00020000);
-        if constexpr (PAT != 0) {
+            __builtin_amdgcn_make_buffer_rsrc((void *)(arena + rfl64(at)), (short)0, 0x7FFFFFFF, 0x00020000);
+        if constexpr (PAT >= 2) {
+#pragma unroll
+            for (int i = 0; i < PER; i++) {
+                const uint32_t idx = 64u * i + lane;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(buf + 1024 * i),
+                                                         16, (idx / UPP) * 4096u + (idx % UPP) * 16u, 0, 0, 2);
+            }
+        } else if constexpr (PAT != 0) {
 #pragma unroll
             for (int i = 0; i < PER; i++)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(buf + 1024 * i),
@@ -1387,6 +1421,15 @@ static uint32_t park_grid(uint64_t total_blocks) {
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus, ntile));
 }
 
+// Persistent staged kernels: every resident workgroup (LDS-limited: 4 per CU
+// at 128-byte segments, 2 at 256) loops over the waves' 64-block groups.
+static dim3 staged_persist_grid(uint32_t seg, uint32_t nwg) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t per_cu = seg == 128 ? 4u : 2u;
+    return dim3(std::max(1u, std::min<uint32_t>(nwg, (uint32_t)cus * per_cu)));
+}
+
 hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const DevFile *files,
                              const uint32_t *wg_file, uint64_t total_blocks, uint32_t nwg, bool aligned,
                              uint32_t max_blen, uint32_t seed, uint8_t *out, uint32_t *scratch,
@@ -1482,6 +1525,14 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             case 38: hipLaunchKernelGGL((diag_stream_rw<1, 16>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
             case 39: hipLaunchKernelGGL((diag_stream_rw<1, 32>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
             case 40: hipLaunchKernelGGL((diag_stream_rw<0, 8>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
+            case 52: hipLaunchKernelGGL((block_sums_staged<2011>), staged_persist_grid(128, nwg), block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
+            case 53: hipLaunchKernelGGL((block_sums_staged<2001>), staged_persist_grid(256, nwg), block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
+            case 46: hipLaunchKernelGGL((diag_stream_read<3, 32, 1, 0>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 47: hipLaunchKernelGGL((diag_stream_read<3, 32, 1, 2>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 48: hipLaunchKernelGGL((diag_stream_read<3, 8, 3, 3>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 49: hipLaunchKernelGGL((diag_stream_read<8, 32, 1, 2>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 50: hipLaunchKernelGGL((diag_stream_read<8, 8, 3, 3>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 51: hipLaunchKernelGGL((diag_stream_read<8, 32, 1, 0>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
             case 43: hipLaunchKernelGGL((block_sums_staged<1011>), grid, block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
             case 44: hipLaunchKernelGGL((block_sums_staged<1001>), grid, block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
             case 45: hipLaunchKernelGGL((block_sums_staged<11>), grid, block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
@@ -1535,7 +1586,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || v == 8 || v == 9)) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || (v >= 8 && v <= 11))) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
     if ((v == 2 || v == 7) && max_blen > kRegMaxBytes) v = 1;
     if (v == 7 && !aligned) v = 0;
@@ -1571,6 +1622,14 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 8:  // 128-byte segments, two slabs per wave
             hipLaunchKernelGGL((block_sums_staged<1010>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
                                total_blocks, seed, out);
+            break;
+        case 10:  // 128-byte segments, persistent workgroups
+            hipLaunchKernelGGL((block_sums_staged<2010>), staged_persist_grid(128, nwg), block, 0, stream, arena,
+                               arena_bytes, files, wg_file, total_blocks, seed, out);
+            break;
+        case 11:  // 256-byte segments, persistent workgroups
+            hipLaunchKernelGGL((block_sums_staged<2000>), staged_persist_grid(256, nwg), block, 0, stream, arena,
+                               arena_bytes, files, wg_file, total_blocks, seed, out);
             break;
         case 9:  // 256-byte segments, two slabs per wave
             hipLaunchKernelGGL((block_sums_staged<1000>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,

@@ -134,7 +134,7 @@ def _run(eng, unaligned, variant, B, seed=cases.SEED):
 
 
 @pytest.mark.parametrize("variant,B", [(-1, 700), (2, 700), (7, 700), (1, 700), (4, 700), (4, 1024), (1, 131072),
-                                       (-1, 131072), (5, 4096), (8, 4096), (9, 131072)])
+                                       (-1, 131072), (5, 4096), (8, 4096), (9, 131072), (10, 4096), (11, 131072)])
 def test_aligned_arena_past_4gib(eng, variant, B):
     """Aligned batch on a 5 GiB arena: park (regular and irregular tiles) and
     the staged kernels, every checked record equal to the oracle's and not one
