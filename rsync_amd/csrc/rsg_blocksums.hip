@@ -1382,6 +1382,232 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     }
 }
 
+// ------------------------------------------------------------- long park
+// Park's streaming ring for blocks longer than a slot (B > 703, variant 12).
+// The staged kernel reads such blocks 128 or 256 bytes of each of a wave's 64
+// blocks at a time, and at B = 4096 those short pieces bound it (0.22 ms per
+// GiB; a bare reader with 512-byte pieces of the same 64 blocks 4 KiB apart
+// takes 0.149, profiles/r05y_b4096_stream_patterns.jsonl).  Here a tile is
+// segment s (704 bytes: 11 chunks) of each of a 64-block group's blocks,
+// streamed through park's three LDS slots by its three loader waves; a
+// hasher copies its lane's 704 bytes out as park's do.  A block's MD4 state
+// crosses tiles in LDS: a workgroup keeps kLpGroups groups in flight, and
+// its tickets run segment-major over them (batch b, segment s, group slot q:
+// k = (b S + s) kLpGroups + q), so consecutive tickets are different groups
+// and the hasher of (q, s) waits only for (q, s - 1), finished kLpGroups
+// tickets earlier (done[q] counts the slot's finished tickets).  S =
+// segments of the batch's longest block (max_blen): tiles of shorter blocks
+// request no bytes past them and hash nothing.  A group of several files'
+// blocks takes per-lane offsets (ds_bpermute per request, as park's
+// irregular tiles); only a partial last group, or one whose span does not
+// fit a buffer offset, takes the per-lane path at its segment 0.
+constexpr uint32_t kLpSeg = 64 * kRegChunks;  // 704 bytes of each block per tile
+constexpr uint32_t kLpGroups = 6;
+struct LpShared {
+    uint8_t tile[kPkSlots][kPkTile];
+    uint32_t rec[kPkWaves - 3][320];        // hashers' record staging (store_tile_records)
+    uint32_t st[kLpGroups][6][64];          // per group slot: h0..h3, s1, t of each lane's block
+    uint32_t n[kPkSlots][64];
+    uint32_t full[kPkSlots], freeq[kPkSlots], kind[kPkSlots];
+    uint32_t done[kLpGroups];
+    uint32_t ticket;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(kPkThreads) void block_sums_lpark(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint32_t nwg256, uint64_t total_blocks, uint32_t max_blen, uint32_t seed,
+    uint8_t *__restrict__ out) {
+    constexpr uint32_t NL = 3;
+    __shared__ __attribute__((aligned(16))) LpShared sh;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x < kPkSlots) {
+        sh.full[threadIdx.x] = ~0u;
+        sh.freeq[threadIdx.x] = threadIdx.x;
+    }
+    if (threadIdx.x < kLpGroups) sh.done[threadIdx.x] = 0;
+    if (threadIdx.x == 0) sh.ticket = 0;
+    __syncthreads();
+    const uint64_t ngroups = (total_blocks + 63) / 64;
+    const uint32_t G = gridDim.x;
+    // this workgroup's groups: gw = blockIdx.x + G m, m < M
+    const uint64_t M = ngroups > blockIdx.x ? (ngroups - blockIdx.x + G - 1) / G : 0;
+    const uint32_t S = (max_blen >> 6) / kRegChunks + 1;  // segments through the longest block's tail chunk
+    const uint64_t nbatch = (M + kLpGroups - 1) / kLpGroups;
+    const uint64_t ntk = nbatch * S * kLpGroups;
+    auto decode = [&](uint64_t k, uint32_t &sg, uint32_t &q, uint64_t &m, uint64_t &b) {
+        b = k / ((uint64_t)S * kLpGroups);
+        const uint32_t r = (uint32_t)(k - b * S * kLpGroups);
+        sg = r / kLpGroups;
+        q = r - sg * kLpGroups;
+        m = b * kLpGroups + q;
+    };
+
+    if (wave < NL) {
+        __builtin_amdgcn_s_setprio(3);
+        // loader L fills slot L with the tickets k = L mod 3.  The next
+        // ticket's descriptor (pk_locate: a chain of scalar loads, a few us)
+        // is built while this ticket's DMA is in flight, as park's loaders do.
+        auto prepare = [&](uint64_t k, PkDesc &d, uint32_t &kind, uint32_t &sg) {
+            uint32_t q;
+            uint64_t m, b;
+            decode(k, sg, q, m, b);
+            kind = 2;  // nothing to load or hash
+            d.n = 0;
+            if (m < M) {
+                const uint64_t gw = blockIdx.x + (uint64_t)G * m;
+                pk_locate(gw, d, lane, files, wg_file, nwg256, total_blocks, arena_bytes);
+                const bool full = gw * 64 + 64 <= total_blocks;
+                bool ok;
+                // every 16-byte request inside the arena: a block's last
+                // request may run up to 15 bytes past its end
+                if (d.regular) {
+                    const uint32_t n63 = d.jl == 63 ? d.nl : d.B;  // lane 63's block: the file's last, or a whole one
+                    ok = full && (uint64_t)d.B * 64 <= 0x7FFFFFFFull &&
+                         d.base + (uint64_t)d.B * 63 + ((n63 + 15u) & ~15u) <= arena_bytes;
+                } else {
+                    // blocks of several files: per-lane offsets (pk_locate's base is the lowest)
+                    const uint64_t top = rfl64(wave_max_u64(d.n ? d.off + ((d.n + 15u) & ~15u) : 0));
+                    ok = full && top <= arena_bytes && top - d.base <= 0x7FFFFFFFull;
+                }
+                kind = ok ? 1u : (sg == 0 ? 0u : 2u);
+            }
+        };
+        // request i, lane l: block j = (64 i + l) / 45, 16-byte unit u (44 = the pad)
+        uint32_t jj[kPkDma], uu[kPkDma];
+#pragma unroll
+        for (uint32_t i = 0; i < kPkDma; i++) {
+            const uint32_t idx = 64u * i + lane;
+            jj[i] = idx / 45u;
+            const uint32_t u = idx - 45u * jj[i];
+            uu[i] = u < 44u ? 16u * u : 0x40000000u;  // past every block length
+        }
+        uint64_t k = wave;
+        PkDesc cur, nxt;
+        uint32_t kind = 2, sg = 0;
+        if (k < ntk) prepare(k, cur, kind, sg);
+#pragma unroll 1
+        while (k < ntk) {
+            const uint32_t slot = (uint32_t)(k % kPkSlots);
+            while (pk_load(&sh.freeq[slot]) != (uint32_t)k) __builtin_amdgcn_s_sleep(1);
+            sh.n[slot][lane] = cur.n;
+            if (lane == 0) sh.kind[slot] = kind;
+            if (kind == 1 && MODE != 2) {
+                // segment sg of block j: bytes [sg 704, +704) of the block, none past its end
+                const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                    (void *)(arena + cur.base + (uint64_t)sg * kLpSeg), (short)0, 0x7FFFFFFF, 0x00020000);
+                const uint32_t so = sg * kLpSeg;
+                const int rel = (int)(uint32_t)(cur.off - cur.base);
+                if (cur.regular) {
+                    // the bytes of block j left from segment sg on (0 past its end)
+                    const uint32_t nB = cur.B > so ? cur.B - so : 0u, nL = cur.nl > so ? cur.nl - so : 0u;
+#pragma unroll
+                    for (uint32_t i = 0; i < kPkDma; i++) {
+                        const uint32_t left = jj[i] == cur.jl ? nL : nB;
+                        const uint32_t vo = uu[i] < left ? cur.B * jj[i] + uu[i] : 0x80000000u;
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                            rsrc, (__attribute__((address_space(3))) void *)(&sh.tile[slot][0] + 1024u * i), 16, vo, 0, 0, 2);
+                    }
+                } else {
+#pragma unroll 1
+                    for (uint32_t i = 0; i < kPkDma; i++) {
+                        const uint32_t rj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * jj[i]), rel);
+                        const uint32_t nj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * jj[i]), (int)cur.n);
+                        const uint32_t vo = (uu[i] < 0x40000000u && so + uu[i] < nj) ? rj + uu[i] : 0x80000000u;
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                            rsrc, (__attribute__((address_space(3))) void *)(&sh.tile[slot][0] + 1024u * i), 16, vo, 0, 0, 2);
+                    }
+                }
+            }
+            const uint64_t kn = k + kPkSlots;
+            uint32_t kind_n = 2, sg_n = 0;
+            if (kn < ntk) prepare(kn, nxt, kind_n, sg_n);
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            if (lane == 0) pk_store(&sh.full[slot], (uint32_t)k);
+            k = kn;
+            cur = nxt;
+            kind = kind_n;
+            sg = sg_n;
+        }
+        return;
+    }
+
+    // ---------------------------------------------------------------- hashers
+    uint32_t *rec = &sh.rec[wave - NL][0];
+#pragma unroll 1
+    for (;;) {
+        uint32_t kk = 0;
+        if (lane == 0) kk = __hip_atomic_fetch_add(&sh.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint64_t k = __builtin_amdgcn_readfirstlane(kk);
+        if (k >= ntk) break;
+        const uint32_t slot = (uint32_t)(k % kPkSlots);
+        uint32_t sg, q;
+        uint64_t m, b;
+        decode(k, sg, q, m, b);
+        while (pk_load(&sh.full[slot]) != (uint32_t)k) __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_setprio(3);
+        const uint32_t n = sh.n[slot][lane];
+        const uint32_t kind = __builtin_amdgcn_readfirstlane(sh.kind[slot]);
+        uint32_t R[16 * kRegChunks];
+        if (kind == 1) {
+            const uint8_t *mine = &sh.tile[slot][0] + lane * kPkPiece;
+#pragma unroll
+            for (uint32_t qd = 0; qd < 4 * kRegChunks; qd++) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * qd);
+                R[4 * qd + 0] = v.x; R[4 * qd + 1] = v.y; R[4 * qd + 2] = v.z; R[4 * qd + 3] = v.w;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        if (lane == 0) pk_store(&sh.freeq[slot], (uint32_t)k + kPkSlots);
+        __builtin_amdgcn_s_setprio(0);
+        // this group slot's previous ticket (its segment sg - 1, or the last
+        // segment of the slot's previous group) must be done
+        const uint32_t want = (uint32_t)(b * S + sg);
+        while (pk_load(&sh.done[q]) != want) __builtin_amdgcn_s_sleep(1);
+        const uint64_t gw = blockIdx.x + (uint64_t)G * m;
+        if (kind == 1) {
+            uint32_t h[4];
+            int32_t s1;
+            uint32_t tw;
+            if (sg == 0) {
+                md4_init(h);
+                s1 = 0;
+                tw = 0;
+            } else {
+                h[0] = sh.st[q][0][lane]; h[1] = sh.st[q][1][lane]; h[2] = sh.st[q][2][lane]; h[3] = sh.st[q][3][lane];
+                s1 = (int32_t)sh.st[q][4][lane];
+                tw = sh.st[q][5][lane];
+            }
+            const uint32_t nfull = n >> 6;
+            if (MODE == 1) {
+#pragma unroll
+                for (int qd = 0; qd < 16 * (int)kRegChunks; qd++) h[qd & 3] ^= R[qd];
+            } else {
+#pragma unroll
+                for (uint32_t c0 = 0; c0 < kRegChunks; c0++) {
+                    const uint32_t c = sg * kRegChunks + c0;
+                    if (c < nfull) hash_chunk<true>(R + 16 * c0, 0u, 0u, c, h, s1, tw);
+                    else if (c == nfull) hash_tail<true>(R + 16 * c0, 0u, 0u, n, seed, h, s1, tw);
+                }
+            }
+            if (sg + 1 == S) {
+                store_tile_records<2>(out, gw, lane, rec, n, s1, tw, h);
+            } else {
+                sh.st[q][0][lane] = h[0]; sh.st[q][1][lane] = h[1]; sh.st[q][2][lane] = h[2]; sh.st[q][3][lane] = h[3];
+                sh.st[q][4][lane] = (uint32_t)s1;
+                sh.st[q][5][lane] = tw;
+            }
+        } else if (kind == 0) {
+            if (MODE == 0 && lane == 0 && gw * 64 + 64 <= total_blocks) count_fallback(1);
+            const uint64_t g = gw * 64 + lane;
+            if (g < total_blocks) pk_direct(arena, arena_bytes, files, wg_file, nwg256, g, seed, out);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the state stores land before the hand-on
+        if (lane == 0) pk_store(&sh.done[q], want + 1);
+    }
+}
+
 // Kernel variants (rsg_set_block_sums_kernel; identical results, only speed
 // differs): -1 = automatic, 0 = direct per-lane loads, 1 = staged LDS-DMA
 // slabs (256-byte segments), 2 = park (three loader waves + five hashers with
@@ -1525,6 +1751,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             case 38: hipLaunchKernelGGL((diag_stream_rw<1, 16>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
             case 39: hipLaunchKernelGGL((diag_stream_rw<1, 32>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
             case 40: hipLaunchKernelGGL((diag_stream_rw<0, 8>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
+            case 54: hipLaunchKernelGGL((block_sums_lpark<1>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file, nwg, total_blocks, max_blen, seed, out); break;
             case 52: hipLaunchKernelGGL((block_sums_staged<2011>), staged_persist_grid(128, nwg), block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
             case 53: hipLaunchKernelGGL((block_sums_staged<2001>), staged_persist_grid(256, nwg), block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
             case 46: hipLaunchKernelGGL((diag_stream_read<3, 32, 1, 0>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
@@ -1586,7 +1813,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || (v >= 8 && v <= 11))) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || (v >= 8 && v <= 12))) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
     if ((v == 2 || v == 7) && max_blen > kRegMaxBytes) v = 1;
     if (v == 7 && !aligned) v = 0;
@@ -1622,6 +1849,11 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         case 8:  // 128-byte segments, two slabs per wave
             hipLaunchKernelGGL((block_sums_staged<1010>), grid, block, 0, stream, arena, arena_bytes, files, wg_file,
                                total_blocks, seed, out);
+            break;
+        case 12:  // long park: 704-byte segments of 64-block groups through park's ring
+            if (aligned)
+                hipLaunchKernelGGL((block_sums_lpark<0>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file,
+                                   nwg, total_blocks, max_blen, seed, out);
             break;
         case 10:  // 128-byte segments, persistent workgroups
             hipLaunchKernelGGL((block_sums_staged<2010>), staged_persist_grid(128, nwg), block, 0, stream, arena,

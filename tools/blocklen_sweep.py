@@ -34,13 +34,14 @@ SHAPES = [  # (files, file bytes, block length, arenas)
     (1, 1 << 30, 32768, 2),       # 8: one 1 GiB file at the reference's sizing (B = sqrt(len) = 32768)
 ]
 VARIANTS = {1: "staged", 4: "staged_seg128", 5: "staged_seg512", 8: "staged_seg128_db", 9: "staged_db", 10: "staged_seg128_persist",
-            11: "staged_persist", 2: "park",
+            11: "staged_persist", 12: "lpark", 2: "park",
             3: "long_deep_prefetch"}
 DIAGS = {1: "diag_staged_memory_only", 45: "diag_staged_seg128_memory_only", 43: "diag_staged_seg128_db_memory_only",
          44: "diag_staged_db_memory_only", 2: "diag_staged_hash_only", 6: "diag_linear_read_ldsdma",
          46: "diag_stream3_contig32k", 47: "diag_stream3_strided512", 48: "diag_stream3_strided128",
          51: "diag_stream8_contig32k", 49: "diag_stream8_strided512", 50: "diag_stream8_strided128",
-         52: "diag_staged_seg128_persist_memory_only", 53: "diag_staged_persist_memory_only"}
+         52: "diag_staged_seg128_persist_memory_only", 53: "diag_staged_persist_memory_only",
+         54: "diag_lpark_memory_only"}
 
 
 def main():
