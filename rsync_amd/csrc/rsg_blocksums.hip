@@ -1432,13 +1432,14 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_lpark(
     const uint64_t ngroups = (total_blocks + 63) / 64;
     const uint32_t G = gridDim.x;
     // this workgroup's groups: gw = blockIdx.x + G m, m < M
-    const uint64_t M = ngroups > blockIdx.x ? (ngroups - blockIdx.x + G - 1) / G : 0;
+    // 32-bit ticket arithmetic: the launch checks that every count fits
+    const uint32_t M = ngroups > blockIdx.x ? (uint32_t)((ngroups - blockIdx.x + G - 1) / G) : 0u;
     const uint32_t S = (max_blen >> 6) / kRegChunks + 1;  // segments through the longest block's tail chunk
-    const uint64_t nbatch = (M + kLpGroups - 1) / kLpGroups;
-    const uint64_t ntk = nbatch * S * kLpGroups;
-    auto decode = [&](uint64_t k, uint32_t &sg, uint32_t &q, uint64_t &m, uint64_t &b) {
-        b = k / ((uint64_t)S * kLpGroups);
-        const uint32_t r = (uint32_t)(k - b * S * kLpGroups);
+    const uint32_t SG = S * kLpGroups;
+    const uint32_t ntk = (M + kLpGroups - 1) / kLpGroups * SG;
+    auto decode = [&](uint32_t k, uint32_t &sg, uint32_t &q, uint32_t &m, uint32_t &b) {
+        b = k / SG;
+        const uint32_t r = k - b * SG;
         sg = r / kLpGroups;
         q = r - sg * kLpGroups;
         m = b * kLpGroups + q;
@@ -1449,9 +1450,8 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_lpark(
         // loader L fills slot L with the tickets k = L mod 3.  The next
         // ticket's descriptor (pk_locate: a chain of scalar loads, a few us)
         // is built while this ticket's DMA is in flight, as park's loaders do.
-        auto prepare = [&](uint64_t k, PkDesc &d, uint32_t &kind, uint32_t &sg) {
-            uint32_t q;
-            uint64_t m, b;
+        auto prepare = [&](uint32_t k, PkDesc &d, uint32_t &kind, uint32_t &sg) {
+            uint32_t q, m, b;
             decode(k, sg, q, m, b);
             kind = 2;  // nothing to load or hash
             d.n = 0;
@@ -1483,14 +1483,14 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_lpark(
             const uint32_t u = idx - 45u * jj[i];
             uu[i] = u < 44u ? 16u * u : 0x40000000u;  // past every block length
         }
-        uint64_t k = wave;
+        uint32_t k = wave;
         PkDesc cur, nxt;
         uint32_t kind = 2, sg = 0;
         if (k < ntk) prepare(k, cur, kind, sg);
 #pragma unroll 1
         while (k < ntk) {
-            const uint32_t slot = (uint32_t)(k % kPkSlots);
-            while (pk_load(&sh.freeq[slot]) != (uint32_t)k) __builtin_amdgcn_s_sleep(1);
+            const uint32_t slot = k % kPkSlots;
+            while (pk_load(&sh.freeq[slot]) != k) __builtin_amdgcn_s_sleep(1);
             sh.n[slot][lane] = cur.n;
             if (lane == 0) sh.kind[slot] = kind;
             if (kind == 1 && MODE != 2) {
@@ -1510,7 +1510,8 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_lpark(
                             rsrc, (__attribute__((address_space(3))) void *)(&sh.tile[slot][0] + 1024u * i), 16, vo, 0, 0, 2);
                     }
                 } else {
-#pragma unroll 1
+                    // (unrolled: a dynamically indexed jj / uu would live in scratch memory)
+#pragma unroll
                     for (uint32_t i = 0; i < kPkDma; i++) {
                         const uint32_t rj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * jj[i]), rel);
                         const uint32_t nj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * jj[i]), (int)cur.n);
@@ -1520,11 +1521,11 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_lpark(
                     }
                 }
             }
-            const uint64_t kn = k + kPkSlots;
+            const uint32_t kn = k + kPkSlots;
             uint32_t kind_n = 2, sg_n = 0;
             if (kn < ntk) prepare(kn, nxt, kind_n, sg_n);
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            if (lane == 0) pk_store(&sh.full[slot], (uint32_t)k);
+            if (lane == 0) pk_store(&sh.full[slot], k);
             k = kn;
             cur = nxt;
             kind = kind_n;
@@ -1539,13 +1540,12 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_lpark(
     for (;;) {
         uint32_t kk = 0;
         if (lane == 0) kk = __hip_atomic_fetch_add(&sh.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint64_t k = __builtin_amdgcn_readfirstlane(kk);
+        const uint32_t k = __builtin_amdgcn_readfirstlane(kk);
         if (k >= ntk) break;
-        const uint32_t slot = (uint32_t)(k % kPkSlots);
-        uint32_t sg, q;
-        uint64_t m, b;
+        const uint32_t slot = k % kPkSlots;
+        uint32_t sg, q, m, b;
         decode(k, sg, q, m, b);
-        while (pk_load(&sh.full[slot]) != (uint32_t)k) __builtin_amdgcn_s_sleep(1);
+        while (pk_load(&sh.full[slot]) != k) __builtin_amdgcn_s_sleep(1);
         __builtin_amdgcn_s_setprio(3);
         const uint32_t n = sh.n[slot][lane];
         const uint32_t kind = __builtin_amdgcn_readfirstlane(sh.kind[slot]);
@@ -1559,11 +1559,11 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_lpark(
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
-        if (lane == 0) pk_store(&sh.freeq[slot], (uint32_t)k + kPkSlots);
+        if (lane == 0) pk_store(&sh.freeq[slot], k + kPkSlots);
         __builtin_amdgcn_s_setprio(0);
         // this group slot's previous ticket (its segment sg - 1, or the last
         // segment of the slot's previous group) must be done
-        const uint32_t want = (uint32_t)(b * S + sg);
+        const uint32_t want = b * S + sg;
         while (pk_load(&sh.done[q]) != want) __builtin_amdgcn_s_sleep(1);
         const uint64_t gw = blockIdx.x + (uint64_t)G * m;
         if (kind == 1) {
@@ -1851,7 +1851,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                                total_blocks, seed, out);
             break;
         case 12:  // long park: 704-byte segments of 64-block groups through park's ring
-            if (aligned)
+            // (its ticket counts are 32-bit: per workgroup groups x segments)
+            if (aligned && ((total_blocks + 63) / 64 / pgrid.x + kLpGroups) * ((max_blen >> 6) / kRegChunks + 1) * kLpGroups <
+                               (1ull << 31))
                 hipLaunchKernelGGL((block_sums_lpark<0>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file,
                                    nwg, total_blocks, max_blen, seed, out);
             break;
