@@ -154,12 +154,14 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
  * 7 = park with register-staged loaders, 8 / 9 = staged with 128- / 256-byte
  * segments and two slabs per wave (a segment's DMA issues two segments
  * ahead), 10 / 11 = staged with 128- / 256-byte segments in persistent
- * workgroups (each wave loops over 64-block groups).  Automatic: aligned batches take 2 when 512 <= the largest block
+ * workgroups (each wave loops over 64-block groups), 12 = long park (park's
+ * ring streaming 704-byte segments of 64-block groups, MD4 states kept in
+ * LDS across segments).  Automatic: aligned batches take 2 when 512 <= the largest block
  * <= 703 bytes, 4 when it is 704..4096 bytes, else 1; unaligned batches (a
  * block not 4-byte aligned) take 6 (3 for blocks >= 8 KiB, else 0, when the
- * arena itself is not 4-byte aligned; 1, 2, 4, 5 and 7-11 fall back to 0
+ * arena itself is not 4-byte aligned; 1, 2, 4, 5 and 7-12 fall back to 0
  * there).  The environment variable RSG_BLOCKSUMS_KERNEL sets a new
- * context's initial value.  Returns RSG_ERR_INVALID outside -1..11.  (Timing
+ * context's initial value.  Returns RSG_ERR_INVALID outside -1..12.  (Timing
  * diagnostics that write meaningless records live in include/rsg_testing.h,
  * not here.) */
 rsg_status rsg_set_block_sums_kernel(rsg_ctx *ctx, int32_t variant);
