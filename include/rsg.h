@@ -156,8 +156,9 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
  * ahead), 10 / 11 = staged with 128- / 256-byte segments in persistent
  * workgroups (each wave loops over 64-block groups), 12 = long park (park's
  * ring streaming 704-byte segments of 64-block groups, MD4 states kept in
- * LDS across segments).  Automatic: aligned batches take 2 when 512 <= the largest block
- * <= 703 bytes, 4 when it is 704..4096 bytes, else 1; unaligned batches (a
+ * LDS across segments).  Automatic: aligned batches take 2 when 512 <= the
+ * largest block <= 703 bytes, 4 when it is 704..2048 bytes, 10 when it is
+ * 2049..4096, else 1; unaligned batches (a
  * block not 4-byte aligned) take 6 (3 for blocks >= 8 KiB, else 0, when the
  * arena itself is not 4-byte aligned; 1, 2, 4, 5 and 7-12 fall back to 0
  * there).  The environment variable RSG_BLOCKSUMS_KERNEL sets a new

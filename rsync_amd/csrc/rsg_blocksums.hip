@@ -1613,11 +1613,13 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_lpark(
 // slabs (256-byte segments), 2 = park (three loader waves + five hashers with
 // register-parked blocks, blocks <= 703 bytes), 3 = long blocks with deep
 // per-lane prefetch, 4 / 5 = staged with 128- / 512-byte segments, 6 = staged
-// for blocks at any byte offset (funnel-shifted pieces).
+// for blocks at any byte offset (funnel-shifted pieces), 7 = park with
+// register-staged loaders, 8 / 9 = staged with two slabs per wave, 10 / 11 =
+// staged in persistent workgroups, 12 = long park (rsg.h has the details).
 // Automatic (launch_block_sums below): aligned batches take park when
-// 512 <= max block <= 703, 4 when the max block is 704..4096, else 1;
-// unaligned batches take 6 (3 for blocks >= 8 KiB, else 0, when the arena
-// itself is not 4-byte aligned).
+// 512 <= max block <= 703, 4 when the max block is 704..2048, 10 up to
+// 4096, else 1; unaligned batches take 6 (3 for blocks >= 8 KiB, else 0,
+// when the arena itself is not 4-byte aligned).
 //
 // Timing diagnostics (rsg_testing_block_sums_diagnostic, a test-only knob of
 // one context, so the product knob can never select one; their "records" are
@@ -1804,12 +1806,15 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     // Aligned: park for 512..703-byte blocks, 128-byte segments up to 4096
     // (B = 1024: 0.197-0.204 ms against 0.207-0.224 for 256-byte segments in
     // three sweeps; B = 2048 0.186 against 0.197, B = 4096 equal,
-    // profiles/r04x_blocklen_sweep.jsonl), 256-byte segments beyond (12 %
-    // better at 128 KiB).  Unaligned: the staged kernel wins at every block
-    // length measured.
+    // profiles/r04x_blocklen_sweep.jsonl), in persistent workgroups above
+    // 2048 (B = 4096: 0.215-0.216 ms against 0.222-0.223, but B = 1024 / 2048
+    // slower, profiles/r05af_blocklen_lpark.jsonl and the r05aa sweep),
+    // 256-byte segments beyond 4096 (12 % better at 128 KiB).  Unaligned: the
+    // staged kernel wins at every block length measured.
     if (v == -1)
-        v = aligned ? ((max_blen <= kRegMaxBytes && max_blen >= kParkMinBytes) ? 2
-                                                                               : (max_blen > kRegMaxBytes && max_blen <= 4096 ? 4 : 1))
+        v = aligned ? ((max_blen <= kRegMaxBytes && max_blen >= kParkMinBytes)
+                           ? 2
+                           : (max_blen > kRegMaxBytes && max_blen <= 4096 ? (max_blen > 2048 ? 10 : 4) : 1))
                     : 6;
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena

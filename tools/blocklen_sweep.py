@@ -33,7 +33,7 @@ SHAPES = [  # (files, file bytes, block length, arenas)
     (256, 4 << 20, 4112, 2),
     (1, 1 << 30, 32768, 2),       # 8: one 1 GiB file at the reference's sizing (B = sqrt(len) = 32768)
 ]
-VARIANTS = {1: "staged", 4: "staged_seg128", 5: "staged_seg512", 8: "staged_seg128_db", 9: "staged_db", 10: "staged_seg128_persist",
+VARIANTS = {-1: "automatic", 1: "staged", 4: "staged_seg128", 5: "staged_seg512", 8: "staged_seg128_db", 9: "staged_db", 10: "staged_seg128_persist",
             11: "staged_persist", 12: "lpark", 2: "park",
             3: "long_deep_prefetch"}
 DIAGS = {1: "diag_staged_memory_only", 45: "diag_staged_seg128_memory_only", 43: "diag_staged_seg128_db_memory_only",
