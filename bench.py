@@ -195,8 +195,7 @@ def main():
                  (1, 37): "diag_stream_rw_contiguous_4tiles", (1, 38): "diag_stream_rw_contiguous_16tiles",
                  (1, 39): "diag_stream_rw_contiguous_32tiles", (1, 40): "diag_stream_rw_interleaved_8tiles",
                  (1, 41): "park_rec6_ring8", (1, 42): "diag_park_rec6_memory_only",
-                 (12, 0): "lpark", (1, 54): "diag_lpark_memory_only",
-                 (1, 55): "park_rec7_burst3", (1, 56): "diag_park_rec7_memory_only"}
+                 (12, 0): "lpark", (1, 54): "diag_lpark_memory_only"}
         only = os.environ.get("AB_ONLY")  # comma-separated substrings: A/B only the matching entries
         if only:
             names = {v: n for v, n in names.items() if any(o in n for o in only.split(","))}

@@ -1315,32 +1315,6 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
     }
 
     // ---------------------------------------------------------------- hashers
-    // REC 7: a hasher's records leave in bursts of kRecBurst tiles (its own
-    // area of the ring, kRecBurst tiles' records staged in LDS)
-    constexpr uint32_t kRecBurst = 3;
-    uint32_t nburst = 0;
-    uint64_t bt0 = 0, bt1 = 0, bt2 = 0;
-    uint32_t *brec = &sh.rec[320u * kRecBurst * (wave - NL)];
-    auto flush_burst = [&]() {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (uint32_t i = 0; i < kRecBurst; i++) {
-            if (i >= nburst) break;
-            const uint64_t tt = i == 0 ? bt0 : (i == 1 ? bt1 : bt2);
-            const u32x4v *src = reinterpret_cast<const u32x4v *>(brec + 320u * i);
-            u32x4a4 *dst = reinterpret_cast<u32x4a4 *>(out + tt * (64ull * kRecordBytes));
-            const u32x4v a = src[lane];
-            __builtin_nontemporal_store(u32x4a4{a.x, a.y, a.z, a.w}, dst + lane);
-            if (lane < 16) {
-                const u32x4v b = src[64 + lane];
-                __builtin_nontemporal_store(u32x4a4{b.x, b.y, b.z, b.w}, dst + 64 + lane);
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the area is rewritten by the next burst
-        nburst = 0;
-    };
 #pragma unroll 1
     for (;;) {
         uint32_t k = 0;
@@ -1386,19 +1360,6 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
                 // diagnostic: no record stores
             } else if (REC == 6) {
                 pk_ring_put(sh, k, t, G, ntiles, lane, n, s1, tw, h, out, true);
-            } else if (REC == 7) {
-                const uint32_t s2 = n * (uint32_t)s1 - tw;
-                uint32_t *r = brec + 320u * nburst + 5u * lane;
-                r[0] = ((uint32_t)s1 & 0xffffu) | (s2 << 16);  // rsyncchecksum.go:50
-                r[1] = h[0];
-                r[2] = h[1];
-                r[3] = h[2];
-                r[4] = h[3];
-                if (nburst == 0) bt0 = t;
-                else if (nburst == 1) bt1 = t;
-                else bt2 = t;
-                nburst++;
-                if (nburst == kRecBurst) flush_burst();
             } else if (REC == 3) {
                 store_record_nt(out, g, n, s1, tw, h);
             } else if (REC >= 1) {
@@ -1419,7 +1380,6 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
             }
         }
     }
-    if (REC == 7 && nburst) flush_burst();
 }
 
 // ------------------------------------------------------------- long park
@@ -1793,15 +1753,6 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             case 38: hipLaunchKernelGGL((diag_stream_rw<1, 16>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
             case 39: hipLaunchKernelGGL((diag_stream_rw<1, 32>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
             case 40: hipLaunchKernelGGL((diag_stream_rw<0, 8>), pgrid, dim3(512), 0, stream, arena, arena_bytes, out); break;
-            case 55:
-            case 56:
-                if (max_blen <= kRegMaxBytes) {
-                    auto kern = diag == 55 ? block_sums_park<0, kParkLoaders, 2, 3, 0, 7>
-                                           : block_sums_park<1, kParkLoaders, 2, 3, 0, 7>;
-                    hipLaunchKernelGGL(kern, pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file, nwg,
-                                       total_blocks, seed, out);
-                }
-                break;
             case 54: hipLaunchKernelGGL((block_sums_lpark<1>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file, nwg, total_blocks, max_blen, seed, out); break;
             case 52: hipLaunchKernelGGL((block_sums_staged<2011>), staged_persist_grid(128, nwg), block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
             case 53: hipLaunchKernelGGL((block_sums_staged<2001>), staged_persist_grid(256, nwg), block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
