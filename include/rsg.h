@@ -156,13 +156,17 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
  * ahead), 10 / 11 = staged with 128- / 256-byte segments in persistent
  * workgroups (each wave loops over 64-block groups), 12 = long park (park's
  * ring streaming 704-byte segments of 64-block groups, MD4 states kept in
- * LDS across segments).  Automatic: aligned batches take 2 when 512 <= the
- * largest block <= 703 bytes, 4 when it is 704..2048 bytes, 10 when it is
- * 2049..4096, else 1; unaligned batches (a
+ * LDS across segments), 13 / 14 / 15 = persistent staged with 128- / 512- /
+ * 256-byte segments where each wave requests its next group's first segment
+ * before hashing the current group's last one.  Automatic: aligned batches
+ * take 2 when 512 <= the largest block <= 703 bytes; when it is 704..8192
+ * bytes, 4 for multiples of 128 up to 2048, else 14 unless 512-byte
+ * segments through the block's tail chunk read over 1.2x its length (then
+ * 1); 1 for all other lengths; unaligned batches (a
  * block not 4-byte aligned) take 6 (3 for blocks >= 8 KiB, else 0, when the
- * arena itself is not 4-byte aligned; 1, 2, 4, 5 and 7-12 fall back to 0
+ * arena itself is not 4-byte aligned; 1, 2, 4, 5 and 7-15 fall back to 0
  * there).  The environment variable RSG_BLOCKSUMS_KERNEL sets a new
- * context's initial value.  Returns RSG_ERR_INVALID outside -1..12.  (Timing
+ * context's initial value.  Returns RSG_ERR_INVALID outside -1..15.  (Timing
  * diagnostics that write meaningless records live in include/rsg_testing.h,
  * not here.) */
 rsg_status rsg_set_block_sums_kernel(rsg_ctx *ctx, int32_t variant);

@@ -413,6 +413,56 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     }
     return v;
 }
+// A 64-block group's layout, wave-uniform when the whole group lies in one
+// file (every lane's block full-length except perhaps lane 63's, the file's
+// last): the file is found with g = the group's first block, so the loads
+// are uniform (scalar loads: no wait on the vector-memory counter, which
+// the in-flight DMA also holds).  Otherwise (the group spans files or runs
+// past the batch) the lanes locate their own blocks (locate_block).
+struct GroupDesc {
+    uint64_t off;   // this lane's block
+    uint32_t n;
+    uint64_t base;  // lane 0's block (uniform)
+    uint32_t S;     // segments through the longest block's tail chunk (uniform)
+    bool staged;    // the staged path applies (uniform)
+};
+
+template <uint32_t SEG>
+__device__ __forceinline__ void locate_group(const uint8_t *arena, uint64_t arena_bytes,
+                                             const DevFile *__restrict__ files, const uint32_t *__restrict__ wg_file,
+                                             uint64_t total_blocks, uint64_t wave_first, uint32_t lane, GroupDesc &d) {
+    constexpr uint32_t kChunks = SEG / 64;
+    (void)arena;
+    const uint64_t wg = wave_first / kBlockSumThreads;
+    uint32_t lo = rfl32(wg_file[wg]), hi = rfl32(wg_file[wg + 1]);
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (files[mid].first_block <= wave_first) lo = mid; else hi = mid - 1;
+    }
+    const uint64_t F_off = rfl64(files[lo].offset), F_len = rfl64(files[lo].len), F_first = rfl64(files[lo].first_block);
+    const uint32_t F_blen = rfl32(files[lo].blen), F_nb = rfl32(files[lo].nblocks);
+    const bool full = wave_first + 63 < total_blocks;
+    if (full && wave_first + 63 - F_first < F_nb) {
+        const uint64_t bi = wave_first + lane - F_first, boff = bi * F_blen, left = F_len - boff;
+        d.n = left < F_blen ? (uint32_t)left : F_blen;
+        d.off = F_off + boff;
+        d.base = F_off + (wave_first - F_first) * F_blen;
+        d.S = (F_blen >> 6) / kChunks + 1;
+        const uint64_t top = d.base + 63ull * F_blen + (uint64_t)SEG * d.S;
+        d.staged = top <= arena_bytes && (top - d.base) <= 0x7FFFFFFFull;
+        return;
+    }
+    const uint64_t g = wave_first + lane;
+    d.off = 0;
+    d.n = 0;
+    if (g < total_blocks) locate_block(files, wg_file, g, d.off, d.n, wg);
+    const uint32_t nseg = d.n ? (d.n >> 6) / kChunks + 1 : 0;
+    d.S = rfl32((uint32_t)wave_max_u64(nseg));
+    d.base = rfl64(wave_min_u64(d.n ? d.off : ~0ull));
+    const uint64_t top = rfl64(wave_max_u64(d.n ? d.off + (uint64_t)SEG * d.S : 0));
+    d.staged = full && top <= arena_bytes && (top - d.base) <= 0x7FFFFFFFull;
+}
+
 // KIND % 10: 0 = the product kernel; timing diagnostics (outputs
 // meaningless): 1 = DMA + LDS reads only (the memory cost of this access
 // pattern), 2 = hashing only, no DMA (the compute cost).  (KIND / 10) % 10
@@ -593,6 +643,177 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     }
 }
 
+// Variants 13 / 14 (round 5): the persistent staged kernel with each wave's
+// group boundary hidden.  Diagnostics showed the staged pattern's cost is
+// its temporal order, not the piece length alone (`diag_stream_read` PAT 4 /
+// 5), and that a persistent wave pays a full memory round trip plus the
+// block lookup at every group start with nothing of its own in flight.  Here
+// the next group is located (uniform loads) while the current group's last
+// segment is in flight, its segment 0 is requested as soon as the slab is
+// free (before the current group's last segment is hashed), and the current
+// group's records leave after the next group's first segment has landed.
+// KIND % 10: 0 product, 1 memory only (outputs meaningless); (KIND / 10) % 10
+// picks the segment as the staged kernel does (0 = 256, 1 = 128, 2 = 512).
+// Measured (profiles/r05am, r05ao sweeps, ms per GiB): memory only 0.179
+// against the staged kernel's 0.200 at B = 1024 (0.180 / 0.186 at 2048,
+// 0.218 / 0.219 at 4096); the product holds 153 VGPRs (3 waves per SIMD
+// against staged's 4), so it gains only at B = 4096: 0.212-0.214 against
+// 0.214-0.216.  Held to 4 waves per SIMD it spills (0.236 at B = 1024).
+// With 512-byte segments (variant 14: one wave per SIMD, LDS-bound anyway)
+// it is the automatic choice for most lengths from 704 to 8192 bytes (see
+// launch_block_sums).
+template <int KIND>
+__device__ __forceinline__ void pipe_body(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
+    constexpr int MODE = KIND % 10;
+    constexpr uint32_t SEG = (KIND % 100) >= 20 ? 512u : ((KIND % 100) >= 10 ? 128u : 256u);
+    constexpr uint32_t kUnits = Seg<SEG>::kUnits, kPiece = Seg<SEG>::kPiece;
+    constexpr uint32_t kWaveSlab = Seg<SEG>::kWaveSlab, kDmaPerSeg = Seg<SEG>::kDmaPerSeg;
+    constexpr uint32_t kChunks = Seg<SEG>::kChunks;
+    constexpr int DMA_AUX = 2;
+    __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * kWaveSlab];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t *slab = slab_all + wave * kWaveSlab;
+    const uint8_t *mine = slab + lane * kPiece;
+    const uint64_t groups = (total_blocks + 63) / 64, stride = (uint64_t)gridDim.x * (kBlockSumThreads / 64);
+    uint64_t gw = (uint64_t)blockIdx.x * (kBlockSumThreads / 64) + wave;
+    if (gw >= groups) return;
+    uint32_t voff[Seg<512>::kDmaPerSeg];  // fixed bound (see block_sums_staged)
+    __amdgpu_buffer_rsrc_t rsrc;
+    // the lane offsets and buffer of group d's DMA (valid until the next call)
+    auto point = [&](const GroupDesc &d) {
+        rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(arena + d.base), (short)0, 0x7FFFFFFF, 0x00020000);
+        const uint32_t rel = (uint32_t)(d.off - d.base);
+#pragma unroll
+        for (uint32_t i = 0; i < kDmaPerSeg; i++) {
+            const uint32_t idx = 64u * i + lane;
+            const uint32_t j = idx / kUnits, u = idx - kUnits * j;
+            const uint32_t v = (uint32_t)__shfl((int)rel, (int)j, 64) + 16u * u;
+            voff[i] = u + 1 < kUnits ? v : 0x80000000u;
+        }
+    };
+    auto dma = [&](uint32_t s) {
+#pragma unroll
+        for (uint32_t i = 0; i < kDmaPerSeg; i++)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(slab + 1024u * i),
+                                                     16, voff[i], SEG * s, 0, DMA_AUX);
+    };
+    uint32_t R[Seg<512>::kSegBytes / 4 + 4];
+    auto read_segment = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < (int)(SEG / 16); q++) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
+            R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+    GroupDesc cur, nxt;
+    locate_group<SEG>(arena, arena_bytes, files, wg_file, total_blocks, gw * 64, lane, cur);
+    if (cur.staged) {
+        point(cur);
+        if (MODE != 2) dma(0);
+    }
+    // the previous group's records, stored once the next group's first
+    // segment has landed (the slab is free then)
+    bool pend = false;
+    uint64_t pend_tile = 0;
+    uint32_t pn = 0, ph[4] = {0, 0, 0, 0}, pt = 0;
+    int32_t ps1 = 0;
+#pragma unroll 1
+    for (;;) {
+        const uint64_t nw = gw + stride;
+        const bool has_next = nw < groups;
+        uint32_t h[4];
+        md4_init(h);
+        int32_t s1 = 0;
+        uint32_t t = 0;
+        const uint32_t n = cur.n, nfull = n >> 6;
+        bool next_located = false;
+        if (!cur.staged) {
+            if (pend) {
+                store_record(out, pend_tile * 64 + lane, pn, ps1, pt, ph);
+                pend = false;
+            }
+            if (n) {
+                hash_block_direct<true>(arena, (uintptr_t)(arena + arena_bytes), cur.off, n, seed, h, s1, t);
+                store_record(out, gw * 64 + lane, n, s1, t, h);
+            }
+            if (!has_next) break;
+            gw = nw;
+            locate_group<SEG>(arena, arena_bytes, files, wg_file, total_blocks, gw * 64, lane, cur);
+            if (cur.staged) {
+                point(cur);
+                dma(0);
+            }
+            continue;
+        }
+        read_segment();
+        if (pend) {
+            if (MODE == 0) store_tile_records<2>(out, pend_tile, lane, reinterpret_cast<uint32_t *>(slab), pn, ps1, pt, ph);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads done before the slab is refilled
+            pend = false;
+        }
+        const uint32_t S = cur.S;
+        if (S == 1 && has_next) {
+            locate_group<SEG>(arena, arena_bytes, files, wg_file, total_blocks, nw * 64, lane, nxt);
+            next_located = true;
+        }
+#pragma unroll 1
+        for (uint32_t cs = 0; cs < S; cs++) {
+            const bool more = cs + 1 < S;
+            if (more) {
+                dma(cs + 1);
+            } else if (next_located && nxt.staged) {
+                point(nxt);  // the slab is free: segment cs is in R
+                dma(0);
+            }
+            if (MODE == 1) {
+#pragma unroll
+                for (int q = 0; q < (int)(SEG / 4); q++) h[q & 3] ^= R[q];
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < kChunks; i++) {
+                    const uint32_t c = kChunks * cs + i;
+                    if (c < nfull) hash_chunk<true>(R + 16 * i, R[16 * i + 16], 0, c, h, s1, t);
+                    else if (c == nfull) hash_tail<true>(R + 16 * i, R[16 * i + 16], 0, n, seed, h, s1, t);
+                }
+            }
+            if (more) {
+                if (cs + 2 == S && has_next) {
+                    // the wave would wait for segment cs + 1 here anyway
+                    locate_group<SEG>(arena, arena_bytes, files, wg_file, total_blocks, nw * 64, lane, nxt);
+                    next_located = true;
+                }
+                read_segment();
+            }
+        }
+        pend = true;
+        pend_tile = gw;
+        pn = n;
+        ps1 = s1;
+        pt = t;
+#pragma unroll
+        for (int k = 0; k < 4; k++) ph[k] = h[k];
+        if (!has_next) break;
+        gw = nw;
+        cur = nxt;  // if staged, its segment 0 is in flight (pointed above)
+    }
+    if (pend) {
+        // no DMA in flight: the slab is free
+        if (MODE == 0) store_tile_records<2>(out, pend_tile, lane, reinterpret_cast<uint32_t *>(slab), pn, ps1, pt, ph);
+        else store_record(out, pend_tile * 64 + lane, pn, ps1, pt, ph);
+    }
+}
+template <int KIND>
+__global__ __launch_bounds__(kBlockSumThreads) void block_sums_pipe(
+    const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
+    const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
+    pipe_body<KIND>(arena, arena_bytes, files, wg_file, total_blocks, seed, out);
+}
+
 // ---------------------------------------------------------------- read ceilings
 // Timing diagnostics only: the fastest way to read the same arena with no
 // hashing, i.e. the empirical HBM-read roofline of this box for DESIGN.md.
@@ -651,8 +872,12 @@ __global__ __launch_bounds__(512) void diag_stream_read(const uint8_t *__restric
     static_assert(PAT != 1 || PER == 45, "park tiles are 45 requests");
     // PAT 2 / 3: the staged kernel's pattern at B = 4096 -- chunk = 64
     // pieces of L = 512 / 128 bytes, 4096 bytes apart (segment seg of 64
-    // consecutive 4 KiB blocks); PER = 64 L / 1024 requests
-    constexpr uint32_t L = PAT == 2 ? 512u : 128u, K = 4096u / L, UPP = L / 16u;
+    // consecutive 4 KiB blocks); PER = 64 L / 1024 requests.  Chunks are
+    // dealt round-robin over the chip, so a group's K segments are read at
+    // once by K waves.  PAT 4 / 5: the same pieces, but each wave walks one
+    // group's segments in order (the staged kernel's temporal order).
+    constexpr bool SEQ = PAT >= 4;
+    constexpr uint32_t L = (PAT == 2 || PAT == 4) ? 512u : 128u, K = 4096u / L, UPP = L / 16u;
     static_assert(PAT < 2 || PER * 1024 == 64 * L, "one chunk = 64 pieces");
     __shared__ __attribute__((aligned(16))) uint8_t buf[64 * 1024];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -663,7 +888,10 @@ __global__ __launch_bounds__(512) void diag_stream_read(const uint8_t *__restric
     const uint32_t G = gridDim.x;
     uint32_t issued = 0;
 #pragma unroll 1
-    for (uint64_t c = blockIdx.x + (uint64_t)G * wave; c < nch; c += (uint64_t)G * NW) {
+    for (uint64_t it = 0;; it++) {
+        const uint64_t W = blockIdx.x + (uint64_t)G * wave, T = (uint64_t)G * NW;
+        const uint64_t c = SEQ ? (W + T * (it / K)) * K + it % K : W + T * it;
+        if (c >= nch) break;
         const uint64_t at = PAT >= 2 ? (c / K) * (64ull * 4096) + (c % K) * L : c * chunk;
         const __amdgpu_buffer_rsrc_t r =
             __builtin_amdgcn_make_buffer_rsrc((void *)(arena + rfl64(at)), (short)0, 0x7FFFFFFF, 0x00020000);
@@ -1650,11 +1878,11 @@ static uint32_t park_grid(uint64_t total_blocks) {
 }
 
 // Persistent staged kernels: every resident workgroup (LDS-limited: 4 per CU
-// at 128-byte segments, 2 at 256) loops over the waves' 64-block groups.
+// at 128-byte segments, 2 at 256, 1 at 512) loops over the waves' 64-block groups.
 static dim3 staged_persist_grid(uint32_t seg, uint32_t nwg) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint32_t per_cu = seg == 128 ? 4u : 2u;
+    const uint32_t per_cu = seg == 128 ? 4u : (seg == 256 ? 2u : 1u);
     return dim3(std::max(1u, std::min<uint32_t>(nwg, (uint32_t)cus * per_cu)));
 }
 
@@ -1762,6 +1990,15 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             case 49: hipLaunchKernelGGL((diag_stream_read<8, 32, 1, 2>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
             case 50: hipLaunchKernelGGL((diag_stream_read<8, 8, 3, 3>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
             case 51: hipLaunchKernelGGL((diag_stream_read<8, 32, 1, 0>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 55: hipLaunchKernelGGL((diag_stream_read<8, 32, 1, 4>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 56: hipLaunchKernelGGL((diag_stream_read<8, 8, 3, 5>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 57: hipLaunchKernelGGL((diag_stream_read<3, 32, 1, 4>), pgrid, dim3(512), 0, stream, arena, arena_bytes, (uint32_t *)out); break;
+            case 58: hipLaunchKernelGGL((block_sums_staged<21>), grid, block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
+            case 59: hipLaunchKernelGGL((block_sums_staged<2021>), staged_persist_grid(512, nwg), block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
+            case 60: hipLaunchKernelGGL((block_sums_staged<2020>), staged_persist_grid(512, nwg), block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
+            case 61: hipLaunchKernelGGL((block_sums_pipe<11>), staged_persist_grid(128, nwg), block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
+            case 62: hipLaunchKernelGGL((block_sums_pipe<21>), staged_persist_grid(512, nwg), block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
+            case 63: hipLaunchKernelGGL((block_sums_pipe<1>), staged_persist_grid(256, nwg), block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
             case 43: hipLaunchKernelGGL((block_sums_staged<1011>), grid, block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
             case 44: hipLaunchKernelGGL((block_sums_staged<1001>), grid, block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
             case 45: hipLaunchKernelGGL((block_sums_staged<11>), grid, block, 0, stream, arena, arena_bytes, files, wg_file, total_blocks, seed, out); break;
@@ -1803,22 +2040,39 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         return hipGetLastError();
     }
     int v = variant;
-    // Aligned: park for 512..703-byte blocks, 128-byte segments up to 4096
+    // Aligned: park for 512..703-byte blocks, 128-byte segments for multiples
+    // of 128 up to 2048, otherwise (below) 512-byte pipelined segments up to
+    // 8192 bytes.  History: 128-byte segments up to 4096
     // (B = 1024: 0.197-0.204 ms against 0.207-0.224 for 256-byte segments in
     // three sweeps; B = 2048 0.186 against 0.197, B = 4096 equal,
     // profiles/r04x_blocklen_sweep.jsonl), in persistent workgroups above
     // 2048 (B = 4096: 0.215-0.216 ms against 0.222-0.223, but B = 1024 / 2048
-    // slower, profiles/r05af_blocklen_lpark.jsonl and the r05aa sweep),
+    // slower, profiles/r05af_blocklen_lpark.jsonl and the r05aa sweep), with
+    // each wave's next group requested early (variant 13: 0.212-0.214 at
+    // B = 4096, profiles/r05ao_blocklen_sweep_pipe.jsonl),
     // 256-byte segments beyond 4096 (12 % better at 128 KiB).  Unaligned: the
     // staged kernel wins at every block length measured.
-    if (v == -1)
-        v = aligned ? ((max_blen <= kRegMaxBytes && max_blen >= kParkMinBytes)
-                           ? 2
-                           : (max_blen > kRegMaxBytes && max_blen <= 4096 ? (max_blen > 2048 ? 10 : 4) : 1))
-                    : 6;
+    // Block lengths that are not multiples of 128 (most SumSizesSqroot
+    // lengths: sqrt(len) rounded to 8) put most 128-byte pieces across two
+    // 128-byte lines: there 512-byte segments with the group boundary hidden
+    // (variant 14) win at every length measured from 1000 to 8000 bytes,
+    // unless the segments through a block's tail chunk over-read it by more
+    // than a fifth (B = 1224: 1536 bytes; then 256-byte segments)
+    // (profiles/r05aq_blocklen_sweep_realistic.jsonl: B = 1000 0.240 ms
+    // against 0.340 for 128-byte segments, B = 4000 0.227 against 0.300).
+    if (v == -1) {
+        const uint64_t seg512_bytes = (uint64_t)((max_blen >> 6) / 8 + 1) * 512;  // read per block
+        if (!aligned) v = 6;
+        else if (max_blen >= kParkMinBytes && max_blen <= kRegMaxBytes) v = 2;
+        else if (max_blen > kRegMaxBytes && max_blen <= 8192) {
+            if (max_blen % 128 == 0 && max_blen <= 2048) v = 4;
+            else if (seg512_bytes * 5 <= (uint64_t)max_blen * 6) v = 14;
+            else v = 1;
+        } else v = 1;
+    }
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
     // staged kernel (6) needs a 4-byte aligned arena
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || (v >= 8 && v <= 12))) v = 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 5 || (v >= 8 && v <= 15))) v = 0;
     if (v == 6 && ((uintptr_t)arena & 3u)) v = max_blen >= kLongBlockBytes ? 3 : 0;
     if ((v == 2 || v == 7) && max_blen > kRegMaxBytes) v = 1;
     if (v == 7 && !aligned) v = 0;
@@ -1861,6 +2115,21 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                                (1ull << 31))
                 hipLaunchKernelGGL((block_sums_lpark<0>), pgrid, pblock, 0, stream, arena, arena_bytes, files, wg_file,
                                    nwg, total_blocks, max_blen, seed, out);
+            else
+                hipLaunchKernelGGL((block_sums_staged<2010>), staged_persist_grid(128, nwg), block, 0, stream, arena,
+                                   arena_bytes, files, wg_file, total_blocks, seed, out);
+            break;
+        case 13:  // persistent, group boundaries hidden: 128 / 512 / 256-byte segments
+            hipLaunchKernelGGL((block_sums_pipe<10>), staged_persist_grid(128, nwg), block, 0, stream, arena,
+                               arena_bytes, files, wg_file, total_blocks, seed, out);
+            break;
+        case 14:
+            hipLaunchKernelGGL((block_sums_pipe<20>), staged_persist_grid(512, nwg), block, 0, stream, arena,
+                               arena_bytes, files, wg_file, total_blocks, seed, out);
+            break;
+        case 15:
+            hipLaunchKernelGGL((block_sums_pipe<0>), staged_persist_grid(256, nwg), block, 0, stream, arena,
+                               arena_bytes, files, wg_file, total_blocks, seed, out);
             break;
         case 10:  // 128-byte segments, persistent workgroups
             hipLaunchKernelGGL((block_sums_staged<2010>), staged_persist_grid(128, nwg), block, 0, stream, arena,

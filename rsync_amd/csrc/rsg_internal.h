@@ -37,8 +37,8 @@ inline uint64_t block_sums_scratch_bytes(uint64_t total_blocks) { return 8 + 4 *
 // register-staged loaders) and timing
 // diagnostics (0 off, 1..kBlockSumsDiagMax; outputs meaningless),
 // rsg_blocksums.hip; both per context (rsg_ctx::bs_variant / bs_diag).
-constexpr int kBlockSumsVariantMax = 12;
-constexpr int kBlockSumsDiagMax = 54;
+constexpr int kBlockSumsVariantMax = 15;
+constexpr int kBlockSumsDiagMax = 63;
 // RSG_BLOCKSUMS_KERNEL (read once): a context's initial variant.
 int block_sums_variant_env();
 // Fallback census of the current device: [0] staged waves, [1] park tiles

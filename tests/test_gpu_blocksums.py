@@ -184,7 +184,7 @@ def test_generate_and_send_sums_wire(eng):
     assert bytes(conn.buf) == want
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("blen", [700, 64, 1024, 1400, 1773, 4096, 131072])
 def test_kernel_variants_match(eng, variant, blen):
     """Every kernel variant (direct / staged / park / long / staged with 128-
@@ -257,7 +257,43 @@ def test_variants_long_blocks_full_waves(eng, variant):
     assert got == want
 
 
-@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("variant", [10, 11, 13, 14, 15])
+@pytest.mark.parametrize("blen", [64, 1400])
+def test_persistent_waves_many_groups(eng, variant, blen):
+    """The persistent staged kernels with several 64-block groups per wave
+    (more groups than resident waves), so the pipelined variants (13-15)
+    hand each group over to the next: files of ragged lengths straddling
+    groups, one ending exactly at the arena end (the last group takes the
+    per-lane path after staged ones)."""
+    rng = np.random.default_rng(blen)
+    # B = 64: 6 k groups, more than the resident waves of every variant (4096
+    # at 128-byte segments); B = 1400: 3.7 k groups (more than 2048 / 1024
+    # resident waves at 256 / 512-byte segments).  B = 4096 on a 5 GiB arena:
+    # tests/test_gpu_large.py
+    total = (24 << 20) if blen == 64 else (320 << 20)
+    lens = []
+    while sum(lens) < total:
+        lens.append(int(rng.integers(1, 6 << 20)))
+    offs, o = [], 0
+    for n in lens:
+        offs.append(o)
+        o += (n + 15) & ~15
+    arena_bytes = offs[-1] + lens[-1]
+    host = np.zeros(arena_bytes, np.uint8)
+    host[:] = cases.splitmix64_bytes(31337, arena_bytes)
+    want = b"".join(orc.block_sums(host[o:o + n], blen, cases.SEED) for o, n in zip(offs, lens))
+    arena = eng.alloc(arena_bytes)
+    arena.upload(host)
+    try:
+        eng.set_block_sums_kernel(variant)
+        recs, total_recs = eng.block_sums_device(arena, [(o, n, blen) for o, n in zip(offs, lens)], cases.SEED)
+        got = recs.download(total_recs * 20).tobytes()
+    finally:
+        eng.set_block_sums_kernel(-1)
+    assert got == want
+
+
+@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 def test_variants_device_aligned_arena(eng, variant):
     """Aligned device arena (the staged / park fast paths), files straddling
     waves and tiles, a file ending exactly at the arena end (park's direct

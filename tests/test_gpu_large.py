@@ -135,7 +135,8 @@ def _run(eng, unaligned, variant, B, seed=cases.SEED):
 
 @pytest.mark.parametrize("variant,B", [(-1, 700), (2, 700), (7, 700), (1, 700), (4, 700), (4, 1024), (1, 131072),
                                        (-1, 131072), (5, 4096), (8, 4096), (9, 131072), (10, 4096), (11, 131072), (12, 700), (12, 1024),
-                                       (12, 4096), (12, 131072)])
+                                       (12, 4096), (12, 131072),
+                                       (13, 1024), (13, 4096), (14, 4096), (15, 4096), (14, 131072)])
 def test_aligned_arena_past_4gib(eng, variant, B):
     """Aligned batch on a 5 GiB arena: park (regular and irregular tiles) and
     the staged kernels, every checked record equal to the oracle's and not one

@@ -34,14 +34,17 @@ SHAPES = [  # (files, file bytes, block length, arenas)
     (1, 1 << 30, 32768, 2),       # 8: one 1 GiB file at the reference's sizing (B = sqrt(len) = 32768)
 ]
 VARIANTS = {-1: "automatic", 1: "staged", 4: "staged_seg128", 5: "staged_seg512", 8: "staged_seg128_db", 9: "staged_db", 10: "staged_seg128_persist",
-            11: "staged_persist", 12: "lpark", 2: "park",
+            11: "staged_persist", 12: "lpark", 13: "pipe_seg128", 14: "pipe_seg512", 15: "pipe", 2: "park",
             3: "long_deep_prefetch"}
 DIAGS = {1: "diag_staged_memory_only", 45: "diag_staged_seg128_memory_only", 43: "diag_staged_seg128_db_memory_only",
          44: "diag_staged_db_memory_only", 2: "diag_staged_hash_only", 6: "diag_linear_read_ldsdma",
          46: "diag_stream3_contig32k", 47: "diag_stream3_strided512", 48: "diag_stream3_strided128",
          51: "diag_stream8_contig32k", 49: "diag_stream8_strided512", 50: "diag_stream8_strided128",
          52: "diag_staged_seg128_persist_memory_only", 53: "diag_staged_persist_memory_only",
-         54: "diag_lpark_memory_only"}
+         54: "diag_lpark_memory_only", 55: "diag_stream8_strided512_seq", 56: "diag_stream8_strided128_seq",
+         57: "diag_stream3_strided512_seq", 58: "diag_staged_seg512_memory_only",
+         59: "diag_staged_seg512_persist_memory_only", 60: "staged_seg512_persist",
+         61: "diag_pipe_seg128_memory_only", 62: "diag_pipe_seg512_memory_only", 63: "diag_pipe_memory_only"}
 
 
 def main():
@@ -56,7 +59,11 @@ def main():
     # SWEEP_SHAPES="1,2": only those entries of SHAPES; SWEEP_ROUNDS: interleaved rounds
     pick = os.environ.get("SWEEP_SHAPES")
     shapes = [SHAPES[int(k)] for k in pick.split(",")] if pick else SHAPES
+    # SWEEP_BLENS="1000,4000": 256 x 4 MiB files at each of those block lengths instead
+    if os.environ.get("SWEEP_BLENS"):
+        shapes = [(256, 4 << 20, int(b), 2) for b in os.environ["SWEEP_BLENS"].split(",")]
     rounds = int(os.environ.get("SWEEP_ROUNDS", "1"))
+    only = os.environ.get("SWEEP_ONLY")  # comma-separated variant / diagnostic names
     for nf, fb, blen, narena in shapes:
         total = nf * fb
         arenas = [eng.alloc(total) for _ in range(narena)]
@@ -68,6 +75,8 @@ def main():
         eng.synchronize(sp)
         res = {}
         runs = [(v, 0, name) for v, name in VARIANTS.items()] + [(1, d, name) for d, name in DIAGS.items()]
+        if only:
+            runs = [r for r in runs if r[2] in only.split(",")]
         if total >= (4 << 30):  # the linear-read ceilings run on <= 4 GiB arenas only
             runs = [r for r in runs if r[1] not in (5, 6)]
         # the memory clock ramps up over the first ~15 ms of launches: warm up
