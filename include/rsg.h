@@ -160,7 +160,7 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
  * 256-byte segments where each wave requests its next group's first segment
  * before hashing the current group's last one.  Automatic: aligned batches
  * take 2 when 512 <= the largest block <= 703 bytes; when it is 704..8192
- * bytes, 4 for multiples of 128 up to 2048, else 14 unless 512-byte
+ * bytes, 4 for multiples of 128 but 4096, else 14 unless 512-byte
  * segments through the block's tail chunk read over 1.2x its length (then
  * 1); 1 for all other lengths; unaligned batches (a
  * block not 4-byte aligned) take 6 (3 for blocks >= 8 KiB, else 0, when the

@@ -2041,8 +2041,8 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     }
     int v = variant;
     // Aligned: park for 512..703-byte blocks, 128-byte segments for multiples
-    // of 128 up to 2048, otherwise (below) 512-byte pipelined segments up to
-    // 8192 bytes.  History: 128-byte segments up to 4096
+    // of 128 up to 8192 but 4096, otherwise (below) 512-byte pipelined
+    // segments up to 8192 bytes.  History: 128-byte segments up to 4096
     // (B = 1024: 0.197-0.204 ms against 0.207-0.224 for 256-byte segments in
     // three sweeps; B = 2048 0.186 against 0.197, B = 4096 equal,
     // profiles/r04x_blocklen_sweep.jsonl), in persistent workgroups above
@@ -2057,7 +2057,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     // 128-byte lines: there 512-byte segments with the group boundary hidden
     // (variant 14) win at every length measured from 1000 to 8000 bytes,
     // unless the segments through a block's tail chunk over-read it by more
-    // than a fifth (B = 1224: 1536 bytes; then 256-byte segments)
+    // than a fifth (B = 1224: 1536 bytes; then 256-byte segments).  Whole
+    // multiples of 128 keep 128-byte segments (B = 2176..8192: 0.184-0.203
+    // ms against 0.196-0.228 for variant 14, r05av), except B = 4096 (0.223
+    // against 0.215)
     // (profiles/r05aq_blocklen_sweep_realistic.jsonl: B = 1000 0.240 ms
     // against 0.340 for 128-byte segments, B = 4000 0.227 against 0.300).
     if (v == -1) {
@@ -2065,7 +2068,7 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         if (!aligned) v = 6;
         else if (max_blen >= kParkMinBytes && max_blen <= kRegMaxBytes) v = 2;
         else if (max_blen > kRegMaxBytes && max_blen <= 8192) {
-            if (max_blen % 128 == 0 && max_blen <= 2048) v = 4;
+            if (max_blen % 128 == 0 && max_blen != 4096) v = 4;
             else if (seg512_bytes * 5 <= (uint64_t)max_blen * 6) v = 14;
             else v = 1;
         } else v = 1;
