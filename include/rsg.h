@@ -162,7 +162,9 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
  * take 2 when 512 <= the largest block <= 703 bytes; when it is 704..8192
  * bytes, 4 for multiples of 128 but 4096, else 14 unless 512-byte
  * segments through the block's tail chunk read over 1.2x its length (then
- * 1); 1 for all other lengths; unaligned batches (a
+ * 1); for 8193..24576 bytes not a multiple of 128, 14 when the
+ * persistent grid's rounds over the batch's 64-block groups are at least
+ * 60 % full, else 1; 1 for all other lengths; unaligned batches (a
  * block not 4-byte aligned) take 6 (3 for blocks >= 8 KiB, else 0, when the
  * arena itself is not 4-byte aligned; 1, 2, 4, 5 and 7-15 fall back to 0
  * there).  The environment variable RSG_BLOCKSUMS_KERNEL sets a new

@@ -2060,7 +2060,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     // than a fifth (B = 1224: 1536 bytes; then 256-byte segments).  Whole
     // multiples of 128 keep 128-byte segments (B = 2176..8192: 0.184-0.203
     // ms against 0.196-0.228 for variant 14, r05av), except B = 4096 (0.223
-    // against 0.215)
+    // against 0.215).  Above 8192 (to 24576) variant 14 also wins unless the
+    // persistent grid's rounds run mostly empty (r05as: B = 9000 0.214
+    // against 0.246, 20000 0.224 against 0.253; 16000 0.292 against 0.275)
     // (profiles/r05aq_blocklen_sweep_realistic.jsonl: B = 1000 0.240 ms
     // against 0.340 for 128-byte segments, B = 4000 0.227 against 0.300).
     if (v == -1) {
@@ -2071,6 +2073,14 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
             if (max_blen % 128 == 0 && max_blen != 4096) v = 4;
             else if (seg512_bytes * 5 <= (uint64_t)max_blen * 6) v = 14;
             else v = 1;
+        } else if (max_blen > 8192 && max_blen <= 24576 && max_blen % 128 != 0) {
+            // longer groups: the persistent grid's last round can run nearly
+            // empty (B = 16000 on 256 x 4 MiB: 1052 groups on 1024 waves),
+            // so variant 14 only when the rounds are at least 60 % full
+            const uint64_t waves = (uint64_t)staged_persist_grid(512, nwg).x * (kBlockSumThreads / 64);
+            const uint64_t groups = (total_blocks + 63) / 64;
+            const uint64_t rounds = (groups + waves - 1) / waves;
+            v = groups * 5 >= rounds * waves * 3 ? 14 : 1;
         } else v = 1;
     }
     // the aligned LDS-DMA kernels need 4-byte aligned blocks; the unaligned
