@@ -109,7 +109,7 @@ rsg_status build_plan(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, uint
     plan.files.resize(nfiles);
     plan.max_blen = 0;
     uint64_t total = 0, off = 0;
-    bool aligned = true;
+    bool aligned = true, lines128 = true;
     for (uint64_t i = 0; i < nfiles; i++) {
         rsg_sum_head h;
         if (!head_for((int64_t)files[i].len, files[i].block_len, &h))
@@ -124,7 +124,7 @@ rsg_status build_plan(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, uint
                             (unsigned long long)files[i].len, (unsigned long long)arena_bytes);
         } else {
             f.offset = off;
-            off += (files[i].len + 15) & ~15ull;
+            off += rsg::pack_round(files[i].len);
         }
         f.len = files[i].len;
         f.first_block = total;
@@ -134,11 +134,13 @@ rsg_status build_plan(rsg_ctx *ctx, const rsg_file *files, uint64_t nfiles, uint
         if (h.count) {
             if (f.offset & 3) aligned = false;
             if (h.count > 1 && (f.blen & 3)) aligned = false;
+            if ((f.offset & 127) || (h.count > 1 && (f.blen & 127))) lines128 = false;
         }
         total += (uint64_t)h.count;
     }
     plan.total_blocks = total;
     plan.aligned = aligned;
+    plan.lines128 = lines128;
     plan.arena_bytes = use_offsets ? arena_bytes : off;
     const uint64_t nwg = (total + kBlockSumThreads - 1) / kBlockSumThreads;
     if (nwg >= 0x7FFFFFFFull) return fail(ctx, RSG_ERR_INVALID, "batch too large (%llu blocks)",
@@ -161,11 +163,12 @@ rsg_status launch_plan(rsg_ctx *ctx, const HostPlan &plan, const void *d_files, 
     if (plan.total_blocks == 0) return RSG_OK;
     if (!d_arena || !d_records) return fail(ctx, RSG_ERR_INVALID, "NULL device pointer");
     const bool aligned = plan.aligned && (((uintptr_t)d_arena & 3u) == 0);
+    const bool lines128 = plan.lines128 && (((uintptr_t)d_arena & 127u) == 0);
     RSG_HIP(ctx, rsg::launch_block_sums((const uint8_t *)d_arena, plan.arena_bytes, (const DevFile *)d_files,
                                         (const uint32_t *)d_wg, plan.total_blocks, plan.nwg, aligned,
                                         plan.max_blen, (uint32_t)seed, (uint8_t *)d_records,
                                         (uint32_t *)d_scratch, plan.lds_reserve, ctx->bs_variant, ctx->bs_diag,
-                                        stream));
+                                        stream, lines128));
     return RSG_OK;
 }
 
@@ -543,7 +546,7 @@ rsg_status rsg_block_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfi
             }
             const uint64_t start = b0 * B, end = std::min<uint64_t>((b0 + take) * B, files[i].len);
             bt->pieces.push_back({i, b0, b0 + take});
-            bt->bytes += ((end - start) + 15) & ~15ull;
+            bt->bytes += rsg::pack_round(end - start);
             bt->recs += take;
             rec += take;
             b0 += take;
@@ -606,7 +609,7 @@ rsg_status rsg_block_sums_host(rsg_ctx *ctx, const rsg_file *files, uint64_t nfi
             vf[j].offset = off;
             vf[j].len = end - start;
             vf[j].block_len = (int32_t)B;
-            off += ((end - start) + 15) & ~15ull;
+            off += rsg::pack_round(end - start);
         }
         // Pieces whose source already lies in page-locked memory (the
         // caller read the files into rsg_alloc_pinned buffers)

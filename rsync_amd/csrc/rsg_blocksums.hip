@@ -1889,7 +1889,7 @@ static dim3 staged_persist_grid(uint32_t seg, uint32_t nwg) {
 hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const DevFile *files,
                              const uint32_t *wg_file, uint64_t total_blocks, uint32_t nwg, bool aligned,
                              uint32_t max_blen, uint32_t seed, uint8_t *out, uint32_t *scratch,
-                             uint32_t lds_reserve, int variant, int diag, hipStream_t stream) {
+                             uint32_t lds_reserve, int variant, int diag, hipStream_t stream, bool lines128) {
     (void)scratch;
     if (total_blocks == 0) return hipSuccess;
     const dim3 block(kBlockSumThreads), grid(nwg);
@@ -2040,9 +2040,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         return hipGetLastError();
     }
     int v = variant;
-    // Aligned: park for 512..703-byte blocks, 128-byte segments for multiples
-    // of 128 up to 8192 but 4096, otherwise (below) 512-byte pipelined
-    // segments up to 8192 bytes.  History: 128-byte segments up to 4096
+    // Aligned: park for 512..703-byte blocks, 128-byte segments when every
+    // block starts on a 128-byte line up to 8192, otherwise (below) 512-byte
+    // pipelined segments up to 8192 bytes.  History: 128-byte segments up to 4096
     // (B = 1024: 0.197-0.204 ms against 0.207-0.224 for 256-byte segments in
     // three sweeps; B = 2048 0.186 against 0.197, B = 4096 equal,
     // profiles/r04x_blocklen_sweep.jsonl), in persistent workgroups above
@@ -2057,10 +2057,12 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     // 128-byte lines: there 512-byte segments with the group boundary hidden
     // (variant 14) win at every length measured from 1000 to 8000 bytes,
     // unless the segments through a block's tail chunk over-read it by more
-    // than a fifth (B = 1224: 1536 bytes; then 256-byte segments).  Whole
-    // multiples of 128 keep 128-byte segments (B = 2176..8192: 0.184-0.203
-    // ms against 0.196-0.228 for variant 14, r05av), except B = 4096 (0.223
-    // against 0.215).  Above 8192 (to 24576) variant 14 also wins unless the
+    // than a fifth (B = 1224: 1536 bytes; then 256-byte segments).  Blocks
+    // that all start on 128-byte lines (lines128: lengths and file offsets
+    // multiples of 128; the library packs its arenas so) keep 128-byte segments (B = 2176..8192: 0.184-0.203
+    // ms against 0.196-0.228 for variant 14, r05av; B = 4096 over files of
+    // mixed lengths 0.181 against 0.202, r05ay, though 4 MiB files 4 MiB apart
+    // favour variant 14, 0.215 against 0.223).  Above 8192 (to 24576) variant 14 also wins unless the
     // persistent grid's rounds run mostly empty (r05as: B = 9000 0.214
     // against 0.246, 20000 0.224 against 0.253; 16000 0.292 against 0.275)
     // (profiles/r05aq_blocklen_sweep_realistic.jsonl: B = 1000 0.240 ms
@@ -2070,10 +2072,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         if (!aligned) v = 6;
         else if (max_blen >= kParkMinBytes && max_blen <= kRegMaxBytes) v = 2;
         else if (max_blen > kRegMaxBytes && max_blen <= 8192) {
-            if (max_blen % 128 == 0 && max_blen != 4096) v = 4;
+            if (lines128) v = 4;
             else if (seg512_bytes * 5 <= (uint64_t)max_blen * 6) v = 14;
             else v = 1;
-        } else if (max_blen > 8192 && max_blen <= 24576 && max_blen % 128 != 0) {
+        } else if (max_blen > 8192 && max_blen <= 24576 && !lines128) {
             // longer groups: the persistent grid's last round can run nearly
             // empty (B = 16000 on 256 x 4 MiB: 1052 groups on 1024 waves),
             // so variant 14 only when the rounds are at least 60 % full

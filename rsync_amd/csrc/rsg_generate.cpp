@@ -48,7 +48,7 @@ constexpr uint32_t kMaxMessage = 256 * 1024;  // wire.go:46-47
 
 struct Piece {
     uint64_t file, b0, b1;  // blocks [b0, b1) of file
-    uint64_t stage_off;     // 16-byte aligned offset in the batch's staging arena
+    uint64_t stage_off;     // kPackAlign-aligned offset in the batch's staging arena
 };
 struct Batch {
     std::vector<Piece> pieces;
@@ -215,7 +215,7 @@ rsg_status generate_files_fd_impl(rsg_ctx *ctx, const rsg_fd_file *files, uint64
             }
             const uint64_t start = b0 * B, end = std::min<uint64_t>((b0 + take) * B, files[i].len);
             bt->pieces.push_back({i, b0, b0 + take, bt->bytes});
-            bt->bytes += ((end - start) + 15) & ~15ull;
+            bt->bytes += rsg::pack_round(end - start);
             bt->recs += take;
             b0 += take;
         }

@@ -100,6 +100,7 @@ struct HostPlan {
     uint64_t total_blocks = 0;
     uint32_t nwg = 0;
     bool aligned = true;      // every block start is 4-byte aligned (arena base aside)
+    bool lines128 = true;     // every block start is 128-byte aligned (arena base aside)
     uint32_t max_blen = 0;    // largest block length (picks blocks per lane)
     uint64_t arena_bytes = 0;
     uint32_t lds_reserve = 0;  // dynamic LDS per workgroup of the long-block kernel (keeps it off CUs

@@ -27,7 +27,12 @@ static_assert(sizeof(DevFile) == 32, "DevFile layout");
 hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const DevFile *files,
                              const uint32_t *wg_file, uint64_t total_blocks, uint32_t nwg, bool aligned,
                              uint32_t max_blen, uint32_t seed, uint8_t *out, uint32_t *scratch,
-                             uint32_t lds_reserve, int variant, int diag, hipStream_t stream);
+                             uint32_t lds_reserve, int variant, int diag, hipStream_t stream,
+                             bool lines128 = false);
+// Files packed into an arena by the library start at multiples of this, so
+// blocks whose length is a multiple of 128 start on 128-byte lines
+constexpr uint64_t kPackAlign = 128;
+inline uint64_t pack_round(uint64_t n) { return (n + kPackAlign - 1) & ~(kPackAlign - 1); }
 
 // Device scratch a block-sum launch needs: 4 + 4 * ceil(total_blocks / 64) bytes.
 inline uint64_t block_sums_scratch_bytes(uint64_t total_blocks) { return 8 + 4 * ((total_blocks + 63) / 64); }

@@ -107,12 +107,14 @@ def shard_layout(lengths: Sequence[int], world: int, nbatch: int = 1, block_len=
 
 def rank_arena(lengths: Sequence[int], layout: ShardLayout, rank: int) -> Tuple[dict, int]:
     """Arena placement of the files rank `rank` touches: whole files back to
-    back at 16-byte aligned offsets.  -> ({file: offset}, arena bytes)."""
+    back at 128-byte aligned offsets (as the library packs its own arenas, so
+    blocks whose length is a multiple of 128 start on 128-byte lines).
+    -> ({file: offset}, arena bytes)."""
     files = sorted({p.file for g in layout.batches[rank] for p in g})
     at, pos = 0, {}
     for f in files:
         pos[f] = at
-        at += (lengths[f] + 15) & ~15
+        at += (lengths[f] + 127) & ~127
     return pos, max(at, 16)
 
 
