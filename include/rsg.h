@@ -159,12 +159,12 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
  * LDS across segments), 13 / 14 / 15 = persistent staged with 128- / 512- /
  * 256-byte segments where each wave requests its next group's first segment
  * before hashing the current group's last one.  Automatic: aligned batches
- * take 2 when 512 <= the largest block <= 703 bytes; when it is 704..8192
- * bytes, 4 when every block starts on a 128-byte line (block length
+ * take 2 when 512 <= the largest block <= 703 bytes; 4 when it is
+ * 704..32768 bytes and every block starts on a 128-byte line (block length
  * and file offsets multiples of 128; the library's own packing keeps file
- * offsets so), else 14 unless 512-byte
+ * offsets so); otherwise for 704..8192 bytes 14 unless 512-byte
  * segments through the block's tail chunk read over 1.2x its length (then
- * 1); for 8193..24576 bytes not a multiple of 128, 14 when the
+ * 1); for 8193..24576 bytes (blocks not on 128-byte lines), 14 when the
  * persistent grid's rounds over the batch's 64-block groups are at least
  * 60 % full, else 1; 1 for all other lengths; unaligned batches (a
  * block not 4-byte aligned) take 6 (3 for blocks >= 8 KiB, else 0, when the

@@ -2062,7 +2062,8 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
     // multiples of 128; the library packs its arenas so) keep 128-byte segments (B = 2176..8192: 0.184-0.203
     // ms against 0.196-0.228 for variant 14, r05av; B = 4096 over files of
     // mixed lengths 0.181 against 0.202, r05ay, though 4 MiB files 4 MiB apart
-    // favour variant 14, 0.215 against 0.223).  Above 8192 (to 24576) variant 14 also wins unless the
+    // favour variant 14, 0.215 against 0.223), up to 32768 (B = 16384 0.172
+    // against 0.200, r05bb).  Above 8192 (to 24576) variant 14 also wins unless the
     // persistent grid's rounds run mostly empty (r05as: B = 9000 0.214
     // against 0.246, 20000 0.224 against 0.253; 16000 0.292 against 0.275)
     // (profiles/r05aq_blocklen_sweep_realistic.jsonl: B = 1000 0.240 ms
@@ -2071,11 +2072,10 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
         const uint64_t seg512_bytes = (uint64_t)((max_blen >> 6) / 8 + 1) * 512;  // read per block
         if (!aligned) v = 6;
         else if (max_blen >= kParkMinBytes && max_blen <= kRegMaxBytes) v = 2;
+        else if (max_blen > kRegMaxBytes && max_blen <= 32768 && lines128) v = 4;
         else if (max_blen > kRegMaxBytes && max_blen <= 8192) {
-            if (lines128) v = 4;
-            else if (seg512_bytes * 5 <= (uint64_t)max_blen * 6) v = 14;
-            else v = 1;
-        } else if (max_blen > 8192 && max_blen <= 24576 && !lines128) {
+            v = seg512_bytes * 5 <= (uint64_t)max_blen * 6 ? 14 : 1;
+        } else if (max_blen > 8192 && max_blen <= 24576) {
             // longer groups: the persistent grid's last round can run nearly
             // empty (B = 16000 on 256 x 4 MiB: 1052 groups on 1024 waves),
             // so variant 14 only when the rounds are at least 60 % full
