@@ -289,7 +289,8 @@ void rsg_ctx_destroy(rsg_ctx *c) {
     for (DevBuf *b : dbs)
         if (b->p) hipFree(b->p);
     for (SearchSlot &sl : c->search) {
-        DevBuf *sbs[] = {&sl.agg, &sl.prefix, &sl.counts, &sl.blob, &sl.src, &sl.res};
+        DevBuf *sbs[] = {&sl.agg, &sl.prefix, &sl.counts, &sl.blob, &sl.src, &sl.res,
+                         &sl.cfiles, &sl.cwg, &sl.cout, &sl.cfb};
         for (DevBuf *b : sbs)
             if (b->p) hipFree(b->p);
         if (sl.count.p) hipHostFree(sl.count.p);

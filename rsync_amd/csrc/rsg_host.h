@@ -51,6 +51,12 @@ struct SearchSlot {
     DevBuf res;                        // confirmation results (block index per window)
     PinBuf hres;                       // ... read back; the job's walk reads them on a worker thread
     PinBuf sel;                        // offsets of the windows a confirm_all batch confirms (the GPU plan reads them)
+    // Confirmation scratch of this slot's job (window descriptors, the plan's
+    // workgroup table, records, the kernel's fallback words).  Per slot, not
+    // per context: two jobs' confirmations run at once on different streams
+    // (the last job's beside job n-2's), and a job's later round trips run on
+    // a worker thread while the calling thread queues the next job's.
+    DevBuf cfiles, cwg, cout, cfb;
     hipEvent_t scanned = nullptr;      // prefix pass done (side stream)
     hipEvent_t tables_b = nullptr;     // the resolve tables' upload done (side stream)
     hipEvent_t rolled = nullptr;       // roll kernel + count read-back done
@@ -85,6 +91,7 @@ struct rsg_ctx {
         int kind;
     };
     bool timing = false;
+    std::mutex spans_mu;  // spans and stat_* (a search's tail records them from a worker thread)
     std::vector<TimedSpan> spans;
     // block-sum kernel knobs of this context (rsg_set_block_sums_kernel;
     // rsg_testing_block_sums_diagnostic): -1 = automatic; 0 = no diagnostic

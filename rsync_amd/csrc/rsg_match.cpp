@@ -62,6 +62,7 @@ void timed_end(rsg_ctx *ctx, hipEvent_t a, hipStream_t stream, int kind) {
         hipEventDestroy(a);
         return;
     }
+    std::lock_guard<std::mutex> g(ctx->spans_mu);
     ctx->spans.push_back({a, b, kind});
 }
 
@@ -231,31 +232,37 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
     rsg_status s;
     if ((s = need_resolve_tables(S)) != RSG_OK) return s;
     S.pt.mark("v.plan");
-    if ((s = ensure_dev(ctx, ctx->d_files, plan.files.size() * sizeof(DevFile) + 32)) != RSG_OK) return s;
-    if ((s = ensure_dev(ctx, ctx->d_wg, plan.wg_file.size() * sizeof(uint32_t) + 4)) != RSG_OK) return s;
-    if ((s = ensure_dev(ctx, ctx->d_out[0], plan.total_blocks * kRecordBytes)) != RSG_OK) return s;
-    RSG_HIP(ctx, hipMemcpyAsync(ctx->d_files.p, plan.files.data(), plan.files.size() * sizeof(DevFile),
+    // the slot's own confirmation scratch: this may run on a worker thread
+    // (a job's tail) while the calling thread queues another slot's
+    // confirmation; the slot's results buffers were consumed before the walk
+    SearchSlot &sl = *S.sl;
+    if ((s = ensure_dev(ctx, sl.cfiles, plan.files.size() * sizeof(DevFile) + 32)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, sl.cwg, plan.wg_file.size() * sizeof(uint32_t) + 4)) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, sl.cout, plan.total_blocks * kRecordBytes)) != RSG_OK) return s;
+    RSG_HIP(ctx, hipMemcpyAsync(sl.cfiles.p, plan.files.data(), plan.files.size() * sizeof(DevFile),
                                 hipMemcpyHostToDevice, S.cst));
-    RSG_HIP(ctx, hipMemcpyAsync(ctx->d_wg.p, plan.wg_file.data(), plan.wg_file.size() * sizeof(uint32_t),
+    RSG_HIP(ctx, hipMemcpyAsync(sl.cwg.p, plan.wg_file.data(), plan.wg_file.size() * sizeof(uint32_t),
                                 hipMemcpyHostToDevice, S.cst));
-    if ((s = ensure_dev(ctx, ctx->d_fb[0], rsg::block_sums_scratch_bytes(plan.total_blocks))) != RSG_OK) return s;
+    if ((s = ensure_dev(ctx, sl.cfb, rsg::block_sums_scratch_bytes(plan.total_blocks))) != RSG_OK) return s;
     hipEvent_t t0 = timed_begin(ctx, S.cst);
-    if (ctx->timing) ctx->stat_windows += idx.size();
-    if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, S.d_src, S.seed, ctx->d_out[0].p, ctx->d_fb[0].p,
-                         S.cst)) != RSG_OK)
+    if (ctx->timing) {
+        std::lock_guard<std::mutex> g(ctx->spans_mu);
+        ctx->stat_windows += idx.size();
+    }
+    if ((s = launch_plan(ctx, plan, sl.cfiles.p, sl.cwg.p, S.d_src, S.seed, sl.cout.p, sl.cfb.p, S.cst)) != RSG_OK)
         return s;
     // Each window resolves on the GPU to the first block in targets order with
     // equal Sum1, length and sum2[:s2len] (match.go:108-136); only the block
     // indices come back.
-    if ((s = ensure_dev(ctx, ctx->d_res, plan.total_blocks * 4)) != RSG_OK) return s;
-    RSG_HIP(ctx, rsg::launch_resolve((const uint8_t *)ctx->d_out[0].p, (const DevFile *)ctx->d_files.p,
+    if ((s = ensure_dev(ctx, sl.res, plan.total_blocks * 4)) != RSG_OK) return s;
+    RSG_HIP(ctx, rsg::launch_resolve((const uint8_t *)sl.cout.p, (const DevFile *)sl.cfiles.p,
                                      plan.total_blocks, S.d_groups, S.d_hi16, S.d_sum2,
                                      S.head.count, S.head.block_len, S.head.rem, S.head.s2len,
-                                     (int32_t *)ctx->d_res.p, S.cst));
+                                     (int32_t *)sl.res.p, S.cst));
     timed_end(ctx, t0, S.cst, 1);
-    if ((s = ensure_pin(ctx, ctx->h_out[0], plan.total_blocks * 4)) != RSG_OK) return s;
-    const int32_t *found = (const int32_t *)ctx->h_out[0].p;
-    RSG_HIP(ctx, hipMemcpyAsync(ctx->h_out[0].p, ctx->d_res.p, plan.total_blocks * 4, hipMemcpyDeviceToHost, S.cst));
+    if ((s = ensure_pin(ctx, sl.hres, plan.total_blocks * 4)) != RSG_OK) return s;
+    const int32_t *found = (const int32_t *)sl.hres.p;
+    RSG_HIP(ctx, hipMemcpyAsync(sl.hres.p, sl.res.p, plan.total_blocks * 4, hipMemcpyDeviceToHost, S.cst));
     if (!S.sl->confirmed) RSG_HIP(ctx, hipEventCreateWithFlags(&S.sl->confirmed, sync_event_flags()));
     RSG_HIP(ctx, hipEventRecord(S.sl->confirmed, S.cst));
     if ((s = run_hook(S, false)) != RSG_OK) return s;  // the next job's roll, if its tables are built
@@ -532,7 +539,10 @@ rsg_status queue_confirm(Search &S, const uint64_t *off, uint32_t m) {
     rsg_ctx *ctx = S.ctx;
     SearchSlot &sl = *S.sl;
     rsg_status s;
-    if (ctx->timing) ctx->stat_windows += m;
+    if (ctx->timing) {
+        std::lock_guard<std::mutex> g(ctx->spans_mu);
+        ctx->stat_windows += m;
+    }
     if (m) {
         HostPlan plan;
         plan.total_blocks = m;
@@ -549,19 +559,20 @@ rsg_status queue_confirm(Search &S, const uint64_t *off, uint32_t m) {
             memcpy(sl.sel.p, off, (size_t)m * 8);
             so = (const uint64_t *)sl.sel.p;
         }
-        if ((s = ensure_dev(ctx, ctx->d_files, (uint64_t)m * sizeof(DevFile) + 32)) != RSG_OK) return s;
-        if ((s = ensure_dev(ctx, ctx->d_wg, ((uint64_t)plan.nwg + 1) * sizeof(uint32_t) + 4)) != RSG_OK) return s;
-        if ((s = ensure_dev(ctx, ctx->d_out[0], (uint64_t)m * kRecordBytes)) != RSG_OK) return s;
-        if ((s = ensure_dev(ctx, ctx->d_fb[0], rsg::block_sums_scratch_bytes(m))) != RSG_OK) return s;
+        // the slot's own scratch: the last job's confirmation runs on the roll
+        // stream beside job n-2's on the confirmation stream (search_batch)
+        if ((s = ensure_dev(ctx, sl.cfiles, (uint64_t)m * sizeof(DevFile) + 32)) != RSG_OK) return s;
+        if ((s = ensure_dev(ctx, sl.cwg, ((uint64_t)plan.nwg + 1) * sizeof(uint32_t) + 4)) != RSG_OK) return s;
+        if ((s = ensure_dev(ctx, sl.cout, (uint64_t)m * kRecordBytes)) != RSG_OK) return s;
+        if ((s = ensure_dev(ctx, sl.cfb, rsg::block_sums_scratch_bytes(m))) != RSG_OK) return s;
         if ((s = ensure_dev(ctx, sl.res, (uint64_t)m * 4)) != RSG_OK) return s;
         if ((s = ensure_pin(ctx, sl.hres, (uint64_t)m * 4)) != RSG_OK) return s;
-        RSG_HIP(ctx, rsg::launch_confirm_plan(so, m, S.size, (uint32_t)S.head.block_len, (DevFile *)ctx->d_files.p,
-                                              (uint32_t *)ctx->d_wg.p, plan.nwg, S.cst));
+        RSG_HIP(ctx, rsg::launch_confirm_plan(so, m, S.size, (uint32_t)S.head.block_len, (DevFile *)sl.cfiles.p,
+                                              (uint32_t *)sl.cwg.p, plan.nwg, S.cst));
         hipEvent_t t0 = timed_begin(ctx, S.cst);
-        if ((s = launch_plan(ctx, plan, ctx->d_files.p, ctx->d_wg.p, S.d_src, S.seed, ctx->d_out[0].p, ctx->d_fb[0].p,
-                             S.cst)) != RSG_OK)
+        if ((s = launch_plan(ctx, plan, sl.cfiles.p, sl.cwg.p, S.d_src, S.seed, sl.cout.p, sl.cfb.p, S.cst)) != RSG_OK)
             return s;
-        RSG_HIP(ctx, rsg::launch_resolve((const uint8_t *)ctx->d_out[0].p, (const DevFile *)ctx->d_files.p, m,
+        RSG_HIP(ctx, rsg::launch_resolve((const uint8_t *)sl.cout.p, (const DevFile *)sl.cfiles.p, m,
                                          S.d_groups, S.d_hi16, S.d_sum2, S.head.count, S.head.block_len, S.head.rem,
                                          S.head.s2len, (int32_t *)sl.res.p, S.cst));
         timed_end(ctx, t0, S.cst, 1);
@@ -1218,6 +1229,11 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
                    pend.tab.wait_for(std::chrono::seconds(0)) == std::future_status::ready;
         };
         rsg_status s = finish(*S);
+        // the next job's issue stays on this thread: a tail on a worker must
+        // not find it (its walk's round trips call run_hook)
+        std::function<rsg_status()> hook = std::move(S->hook);
+        S->hook = nullptr;
+        S->hook_ready = nullptr;
         if (s == RSG_OK && S->tail) {
             if (overlap) {  // the walk runs beside the next jobs' confirmations and rolls
                 tails[slot] = std::async(std::launch::async, S->tail);
@@ -1227,7 +1243,7 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
             }
         }
         if (!tail_live[slot] && (fatal = complete(i, s)) != RSG_OK) break;
-        if (S->hook && (fatal = S->hook()) != RSG_OK) {  // finish() stopped early on a job-local error
+        if (hook && (fatal = hook()) != RSG_OK) {  // not run by finish() (tables not ready, or a job-local error)
             i++;
             break;
         }

@@ -217,8 +217,8 @@ uint64_t batch_records(const rsg_shard_batch &sb) { return sb.plan ? sb.plan->ho
 // reference generator streams its sums with bounded memory,
 // generator.go:20-52); the host memory of one call is then at most
 // (n - 1) * (cap + one chunk) beyond the generators' own staging.
-uint64_t g_queue_cap = 256ull << 20;        // rsg_testing_set_multi_queue_cap
-std::atomic<uint64_t> g_queue_peak{0};      // largest queue of the last call
+std::atomic<uint64_t> g_queue_cap{256ull << 20};  // rsg_testing_set_multi_queue_cap
+std::atomic<uint64_t> g_queue_peak{0};      // largest queue of the last call (process-wide: valid for single-threaded tests only)
 struct RankQueue {
     std::mutex mu;
     std::condition_variable cv;     // consumer: a chunk arrived or the rank is done
@@ -469,7 +469,7 @@ rsg_status rsg_generate_files_fd_multi(rsg_ctx *const *ctxs, int32_t n, const rs
     for (int q = 0; q < n; q++) {
         RankQueue &rq = qs[(size_t)q];
         rq.abort = &abort;
-        rq.cap = g_queue_cap;
+        rq.cap = g_queue_cap.load();
         if (shards[(size_t)q].empty()) {
             rq.done = true;
             continue;
@@ -592,7 +592,7 @@ rsg_status rsg_generate_files_fd_multi(rsg_ctx *const *ctxs, int32_t n, const rs
 
 rsg_status rsg_testing_multi_queue(uint64_t cap, uint64_t *peak) {
     if (peak) *peak = g_queue_peak.load();
-    if (cap) g_queue_cap = cap;
+    if (cap) g_queue_cap.store(cap);
     return RSG_OK;
 }
 

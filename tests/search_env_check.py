@@ -45,6 +45,22 @@ def main():
         want, _, _ = orc.hash_search(src, head, s1, s2, tg, seed)
         assert eng.hash_search(src, head, s1, s2, tg, seed) == want, k
         n += 1
+    # a multi-job batch: walks (tails) on worker threads beside the next
+    # jobs' confirmations, with their extra round trips in this mode
+    jobs, want = [], []
+    for k in range(5):
+        rng = np.random.default_rng(400 + k)
+        size = int(rng.integers(200_000, 6_000_000)) if k != 4 else 40_000
+        basis = cases.splitmix64_bytes(1900 + k, size)
+        src = cases.mutate(basis, 1950 + k, 0.5, 1, 70000, n_ins=3, n_del=3)
+        seed = 0x1BADB002
+        head = orc.sum_head(basis.size, 0)
+        s1, s2 = orc.parse_records(orc.block_sums(basis, head[1], seed))
+        tg = orc.stable_targets(s1)
+        jobs.append((src, None, head, s1, s2, tg))
+        want.append(orc.hash_search(src, head, s1, s2, tg, seed)[0])
+    assert eng.hash_search_batch(jobs, 0x1BADB002, device=False) == want
+    n += len(jobs)
     eng.close()
     print("ok", n)
 

@@ -297,6 +297,32 @@ def test_batch_device_matches_single(eng):
     assert got == [eng.hash_search_device(*j, seed) for j in jobs]
 
 
+@pytest.mark.parametrize("order", ["big_then_tiny", "tiny_big_tiny"])
+def test_batch_last_confirmation_beside_previous(eng, order):
+    """The last job's confirmation runs on the roll stream beside job n-2's on
+    the confirmation stream (rsg_match.cpp search_batch, last_own): a large
+    sparse confirmation (a 96 MiB cfg3-shaped source, thousands of windows)
+    followed by a tiny last job whose confirmation is queued while the large
+    one still runs.  Each job has its own confirmation scratch, so both match
+    lists equal the oracle's (match.go:21-230)."""
+    seed = cases.SEED
+    sizes = [96 << 20, 30_000] if order == "big_then_tiny" else [20_000, 96 << 20, 25_000]
+    bufs, jobs, want = [], [], []
+    for k, n in enumerate(sizes):
+        basis = cases.splitmix64_bytes(60 + k, n)
+        head, s1, s2 = basis_sums(basis, 0, seed)
+        src = cases.mutate(basis, 70 + k, 0.5, 1, 2 * head[1], n_ins=3, n_del=3)
+        tg = orc.stable_targets(s1)
+        buf = eng.alloc(src.size + 16)
+        buf.upload(src)
+        bufs.append(buf)
+        jobs.append((buf, src.size, head, s1, s2, tg))
+        want.append(orc.hash_search(src, head, s1, s2, tg, seed)[0])
+    assert max(len(w) for w in want) > 1000
+    for _ in range(3):
+        assert eng.hash_search_batch(jobs, seed) == want
+
+
 @pytest.mark.parametrize("blen", [131073, 200000])
 def test_long_blocks_prefix_pass(eng, blen):
     """B > 128 KiB: the roll kernel takes its window sums from the tile_agg /
