@@ -66,7 +66,8 @@ def parse():
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--no-delivery", action="store_true", help="skip the pipelined gather / D2H delivery modes")
     ap.add_argument("--ab", action="store_true", help="A/B the block-sum kernel variants (interleaved rounds)")
-    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5", "filesums", "receive"],
+    ap.add_argument("--workload", default="cfg2",
+                    choices=["cfg2", "cfg3", "cfg4", "cfg4-sender", "cfg5", "filesums", "receive"],
                     help="cfg2 = receiver block sums (the metric); cfg3 = sender match, reported separately")
     ap.add_argument("--cfg3-files", type=int, default=10)
     ap.add_argument("--batches", type=int, default=None,
@@ -115,6 +116,8 @@ def main():
         return bench_sender(args, rank, world, local)
     if args.workload == "cfg4":
         return bench_mixed(args, rank, world, local)
+    if args.workload == "cfg4-sender":
+        return bench_sender_small(args, rank, world, local)
     if args.workload == "cfg5":
         return bench_long(args, rank, world, local)
     if args.workload == "filesums":
@@ -303,10 +306,22 @@ def main():
         recv_off = [[(q * plan.total_records + g[0] * recs_per_file) * rsync_amd.RECORD_BYTES for q in range(world)]
                     for g in groups]
         sb = ShardedBlockSums(eng, descs, arena_bytes, rec_off, send, recv_off)
+        def oracle_check(got):
+            """orc_block_sums of files 0, n/2 and n-1 of every rank (rank q's
+            file f is splitmix64(q n + f + 1)) against their gathered records."""
+            from oracle import oracle as orc
+            ok, k = True, 0
+            for q in range(world):
+                for f in (0, n // 2, n - 1):
+                    want = orc.block_sums(orc.splitmix64_bytes(q * n + f + 1, FILE_BYTES), BLOCK_LEN, SEED)
+                    o = (q * plan.total_records + plan.first_record[f]) * rsync_amd.RECORD_BYTES
+                    ok &= bytes(got[o:o + len(want)]) == want
+                    k += 1
+            return {"oracle_files_checked": k, "oracle_equal": bool(ok)}
         extra["delivery"] = guarded_delivery(args, eng, sb, arenas, recs, world, rank, world * in_bytes,
                                              world * plan.total_records,
                                              lambda d: print(json.dumps(bench_line(dict(extra, delivery=d))),
-                                                             flush=True))
+                                                             flush=True), oracle_check)
         sb.close()
 
     # ---- PCIe-inclusive host path (rank 0, N = 1): host buffers in, records out
@@ -441,12 +456,15 @@ def max_over_ranks(world, *vals):
     return tuple(float(x) for x in t)
 
 
-def measure_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, records_all):
+def measure_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, records_all, oracle_check=None):
     """The generator step with its records delivered, pipelined per batch
     (rsg_block_sums_gather / rsg_block_sums_d2h): kernel of batch b+1 while
     batch b's records move.  Each timed step hashes the rank's whole share
     and delivers it; rates are all ranks' input bytes / the max-over-ranks
-    wall time.  -> dict for the bench line.
+    wall time.  -> dict for the bench line, with "gather_parity": the root's
+    gathered buffer against every rank's SHA-256 of its own records, every
+    rank's D2H copy against the same, and oracle_check(gathered bytes) (the
+    C oracle on sampled files of every rank).
     The communicator is set up before any leg is timed, ~0.1 s of steps run
     after its init, and every leg runs 8 untimed steps first (see below).
     BENCH_DELIVERY_DIAG=2 (one rank): per-chunk kernel times before and
@@ -522,7 +540,24 @@ def measure_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, record
     host = eng.alloc_pinned(max(sb.my_records, 1) * rsync_amd.RECORD_BYTES)
     out["d2h_parallel_pipelined"] = timed(lambda i: sb.run_d2h(arenas[i & 1], SEED, recs, host))
     out["d2h_parallel_pipelined"]["bytes_to_host_per_rank"] = sb.my_records * rsync_amd.RECORD_BYTES
+    # ---- self-check, after the timed legs: every rank's own records (its
+    # d_records, written by the d2h leg's kernels) against what the gather put
+    # on the root and what its D2H put in host memory (generator.go:20-52:
+    # every file's sums, in file-list order)
+    from rsync_amd.dist import all_ranks, gather_parity, records_digest
+    nbytes = sb.my_records * rsync_amd.RECORD_BYTES
+    mine = recs.download(nbytes) if nbytes else np.zeros(0, np.uint8)
+    dg = records_digest(mine)
+    info = all_ranks((dg, sb.my_records, records_digest(host[:nbytes]) == dg), world)
     eng.free_pinned(host)
+    if rank == 0:
+        got = recv.download(sum(n for _, n, _ in info) * rsync_amd.RECORD_BYTES)
+        par = gather_parity(got, [d for d, _, _ in info], [n for _, n, _ in info])
+        par["d2h_ranks_equal"] = [ok for _, _, ok in info]
+        if oracle_check is not None:
+            par.update(oracle_check(got))
+        par["all_equal"] = bool(par["all_equal"] and all(par["d2h_ranks_equal"]) and par.get("oracle_equal", True))
+        out["gather_parity"] = par
     if diag:
         out["diag_gather_after_d2h"] = timed(lambda i: sb.run_gather(arenas[i & 1], SEED, recs, recv, 0))
         out["diag_synced_after_d2h"] = timed(synced)
@@ -530,7 +565,8 @@ def measure_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, record
     return out
 
 
-def guarded_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, records_all, print_line):
+def guarded_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, records_all, print_line,
+                     oracle_check=None):
     """measure_delivery under a watchdog: a collective that stalls for 120 s
     makes rank 0 print the bench line with the error and every rank exit 3
     (a failed collective must not look like success); an exception is
@@ -546,7 +582,7 @@ def guarded_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, record
     if world > 1:
         threading.Thread(target=watchdog, daemon=True).start()
     try:
-        d = measure_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, records_all)
+        d = measure_delivery(args, eng, sb, arenas, recs, world, rank, bytes_all, records_all, oracle_check)
         d.pop("recv", None)
     except Exception as e:  # reported, never fatal to the bench line
         d = {"error": str(e)[:300]}
@@ -743,6 +779,184 @@ def sender_host_path(eng, srcs, metas, dev_res):
     return out
 
 
+class _DevView:
+    """A device address (and size) inside a torch-allocated arena, in the
+    shape the engine's calls take (.ptr, .nbytes)."""
+
+    def __init__(self, ptr, nbytes=0):
+        self.ptr, self.nbytes = int(ptr), int(nbytes)
+
+
+def bench_sender_small(args, rank, world, local):
+    """cfg4-sender: the sender over a file tree of small sources -- SendFiles'
+    per-file hashSearch (sender.go:19-115, match.go:21-230) for 100 000
+    sources of 4-64 KiB (cfg4's lengths, PRNG seed 4), each its basis with one
+    deletion of 1-63 bytes (so matches also fall off block boundaries) and
+    random runs of 1-1400 bytes overwritten over ~50 % of it; B =
+    SumSizesSqroot (700 at these sizes).  Sources device-resident, sums and
+    targets in host memory as receiveSums leaves them, match lists written to
+    host arrays: one rsg_hash_search_batch_device call per pass (the
+    small-file kernel, one wave per file, a few launches per call).  Ranks
+    take every world-th file (strong scaling)."""
+    import torch
+    import torch.distributed as dist
+    import rsync_amd
+    from rsync_amd.engine import SearchBatch
+    from rsync_amd._lib import check as _check
+    NF = 100_000
+    lengths = np.random.default_rng(4).integers(4096, 65537, NF)
+    mine = np.arange(rank, NF, world)
+    L = lengths[mine]
+    eng = rsync_amd.Engine(local)
+    dev = torch.device("cuda", local)
+    a16 = lambda x: (x + 15) // 16 * 16  # noqa: E731
+    bofs = np.concatenate([[0], np.cumsum(a16(L))[:-1]])
+    tb = int(a16(L).sum())
+    bt = torch.empty(tb, dtype=torch.uint8, device=dev)
+    for k, f in enumerate(mine.tolist()):
+        eng.fill_splitmix64(_DevView(bt.data_ptr()), int(L[k]), f + 1, offset=int(bofs[k]))
+    eng.synchronize()
+    # basis sums (reference sizing: B = 700 for every file here) and targets
+    recs, total = eng.block_sums_device(_DevView(bt.data_ptr(), tb), [(int(o), int(n), 0) for o, n in zip(bofs, L)],
+                                       SEED)
+    rec = recs.download(total * 20).reshape(-1, 20)
+    recs.free()
+    heads = [rsync_amd.sum_sizes_sqroot(int(n)) for n in L]
+    counts = np.array([h.count for h in heads], np.int64)
+    first = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    s1 = rec[:, :4].copy().view("<u4").reshape(-1)
+    s2 = rec[:, 4:].copy()
+    tags = ((s1 & 0xFFFF) + (s1 >> 16)) & 0xFFFF
+    fob = np.repeat(np.arange(len(L)), counts)
+    order = np.lexsort((tags, fob))  # per file, stable by tag (sender.go:60-83)
+    targets = (order - first[fob[order]]).astype(np.int32)
+    # sources: one deletion, then ~50 % of the bytes overwritten in runs
+    rng = np.random.default_rng(40 + rank)
+    d = rng.integers(1, 64, len(L))
+    p = (rng.random(len(L)) * (L - d)).astype(np.int64)
+    Ls = L - d
+    sofs = np.concatenate([[0], np.cumsum(a16(Ls))[:-1]])
+    ts = int(a16(Ls).sum())
+    st = torch.empty(ts, dtype=torch.uint8, device=dev)
+    for k in range(len(L)):
+        so, bo, pk, dk, lk = int(sofs[k]), int(bofs[k]), int(p[k]), int(d[k]), int(L[k])
+        st[so:so + pk] = bt[bo:bo + pk]
+        st[so + pk:so + lk - dk] = bt[bo + pk + dk:bo + lk]
+    nr = np.maximum(1, np.round(0.5 * Ls / 700).astype(np.int64))
+    rf = np.repeat(np.arange(len(L)), nr)
+    rl = rng.integers(1, 1401, rf.size)
+    rl = np.minimum(rl, Ls[rf])
+    rs = sofs[rf] + (rng.random(rf.size) * (Ls[rf] - rl + 1)).astype(np.int64)
+    diff = torch.zeros(ts + 1, dtype=torch.int32, device=dev)
+    diff.index_add_(0, torch.from_numpy(rs).to(dev), torch.ones(rf.size, dtype=torch.int32, device=dev))
+    diff.index_add_(0, torch.from_numpy(rs + rl).to(dev), torch.full((rf.size,), -1, dtype=torch.int32, device=dev))
+    cov = diff.cumsum(0, dtype=torch.int32)[:-1] > 0
+    del diff
+    rnd = torch.empty_like(st)
+    torch.cuda.synchronize()
+    eng.fill_splitmix64(_DevView(rnd.data_ptr()), ts, 0xC0FFEE + rank)
+    eng.synchronize()
+    st = torch.where(cov, rnd, st)
+    touched = float(cov.sum()) / float(Ls.sum())
+    del rnd, cov, bt
+    torch.cuda.synchronize()
+    jobs = []
+    for k in range(len(L)):
+        c0, c = int(first[k]), int(counts[k])
+        jobs.append((_DevView(st.data_ptr() + int(sofs[k])), int(Ls[k]), heads[k], s1[c0:c0 + c], s2[c0:c0 + c],
+                     targets[c0:c0 + c]))
+    batch = SearchBatch(eng, jobs, device=True)
+    eng.set_kernel_timing(True)
+    for _ in range(2):
+        _check(batch.run(SEED), eng.ctx)
+    steps = max(1, min(args.steps, 20))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.kernel_times(reset=True)
+    call_ms = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        c0 = time.perf_counter()
+        _check(batch.run(SEED), eng.ctx)
+        call_ms.append(round((time.perf_counter() - c0) * 1e3, 3))
+    dt = time.perf_counter() - t0
+    kt = eng.kernel_times(reset=True)
+    eng.set_kernel_timing(False)
+    nmatch = sum(batch.n_matches(k) for k in range(batch.n))
+    scanned = float(Ls.sum())
+    if world > 1:
+        tt = torch.tensor([dt, scanned], dtype=torch.float64)
+        dist.all_reduce(tt[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(tt[1:])
+        dt, scanned = float(tt[0]), float(tt[1])
+    kernel_ms = kt["roll_ms"] / steps  # every small-file launch of one call
+    src_bytes = float(Ls.sum())
+    cpu, parity, pipeline = None, None, None
+    if rank == 0:
+        # the same files' first 2000 through the large-file pipeline, for
+        # comparison (rsg_testing_set_search_path 1: one roll, confirmation
+        # and walk per file)
+        sub = SearchBatch(eng, jobs[:2000], device=True)
+        eng.set_search_path(1)
+        t1 = time.perf_counter()
+        _check(sub.run(SEED), eng.ctx)
+        t_pipe = time.perf_counter() - t1
+        eng.set_search_path(0)
+        pipeline = {"files": 2000, "gib_s": round(float(Ls[:2000].sum()) / t_pipe / GIB, 3),
+                    "matches_equal": all(sub.matches(k) == batch.matches(k) for k in range(2000))}
+    if rank == 0 and not args.no_cpu:
+        # cpu_baseline leg: the C restatement of hashSearch on a bounded sample
+        # of the files, which also checks the benchmarked match lists
+        from oracle import oracle as orc
+        t_cpu, done, k, eq, checked = 0.0, 0, 0, True, 0
+        while k < len(L) and (t_cpu < args.cpu_seconds or k < 512):
+            src = st[int(sofs[k]):int(sofs[k]) + int(Ls[k])].cpu().numpy()
+            h, (c0, c) = heads[k], (int(first[k]), int(counts[k]))
+            c_0 = time.perf_counter()
+            om, _, _ = orc.hash_search(src, h.astuple(), s1[c0:c0 + c], s2[c0:c0 + c], targets[c0:c0 + c], SEED)
+            t_cpu += time.perf_counter() - c_0
+            done += src.size
+            eq &= om == batch.matches(k)
+            checked += 1
+            k += 1
+        parity = {"files_compared": checked, "equal": bool(eq)}
+        cpu = {"value": round(done / t_cpu / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+               "cpu_model": cpu_model(),
+               "sample": f"first {checked} files of the set vs their basis sums, oracle/rsg_oracle.c orc_hash_search "
+                         f"(scalar C restatement of match.go:21-282), 1 thread, {t_cpu:.1f} s"}
+    if rank == 0:
+        print(json.dumps({"metric": "GiB/s source scanned (sender rolling match), device-resident",
+                          "value": round(scanned * steps / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
+                          "steps": steps, "higher_is_better": True, "scaling": "strong", "dtype": "u32",
+                          "ms_per_step": round(dt * 1e3 / steps, 3), "call_ms": call_ms,
+                          "data": f"synthetic (splitmix64 bases; sources: one 1-63 byte deletion, "
+                                  f"{touched:.0%} of bytes overwritten in 1-1400 byte runs)",
+                          "config": {"workload": "cfg4-sender: 100k sources of 4-64 KiB vs 50%-modified bases, "
+                                                 "B = SumSizesSqroot (700)", "files": NF,
+                                     "rank0_files": int(len(L)), "rank0_bytes": int(src_bytes),
+                                     "matches_per_pass": nmatch,
+                                     "call": "rsg_hash_search_batch_device, one call per pass (sums and targets "
+                                             "in host memory, match lists to host arrays)"},
+                          "roofline": {"bound": "hbm", "kernel": "search_small_kernel (roll + confirmation + walk, "
+                                                                 "one wave per file)",
+                                       "note": "per call: every launch of the small-file kernel; the kernel is "
+                                               "VALU-bound, frac is its HBM fraction as the metric's unit",
+                                       "achieved": round(src_bytes / (kernel_ms * 1e-3) / 1e9, 1),
+                                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                       "frac": round(src_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                       "traffic": committed_traffic("search_small_kernel_cfg4s_bytes_per_call"),
+                                       "kernel_ms_per_call": round(kernel_ms, 4),
+                                       "launches_per_call": kt["roll_launches"] // steps,
+                                       "algorithmic_bytes_per_call": int(src_bytes)},
+                          "pipeline_first_2000_files": pipeline,
+                          "oracle_parity": parity,
+                          "cpu_baseline": cpu}), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 ROLL_ISSUE_NS = 1.91  # measured, see roll_valu_issue
 
 
@@ -913,9 +1127,21 @@ def bench_mixed(args, rank, world, local):
 
     more = {}
     if not args.no_delivery:
+        gfirst = np.concatenate([[0], np.cumsum([-(-ln // BLOCK_LEN) for ln in lengths])])
+
+        def oracle_check(got):
+            """orc_block_sums of 16 files spread over the list (every rank's
+            share) against their gathered records at their global offsets."""
+            from oracle import oracle as orc
+            ok, picks = True, np.linspace(0, NF - 1, 16).astype(int).tolist()
+            for f in picks:
+                want = orc.block_sums(orc.splitmix64_bytes(f + 1, lengths[f]), BLOCK_LEN, SEED)
+                o = int(gfirst[f]) * rsync_amd.RECORD_BYTES
+                ok &= bytes(got[o:o + len(want)]) == want
+            return {"oracle_files_checked": len(picks), "oracle_equal": bool(ok)}
         more["delivery"] = guarded_delivery(args, eng, sb, arenas, recs, world, rank, float(total),
                                             lay.total_records, lambda d: print(json.dumps(line({"delivery": d})),
-                                                                               flush=True))
+                                                                               flush=True), oracle_check)
     if rank == 0:
         print(json.dumps(line(more)), flush=True)
     sb.close()

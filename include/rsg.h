@@ -332,7 +332,9 @@ rsg_status rsg_hash_search_batch_host(rsg_ctx *ctx, rsg_search_job *jobs, uint64
  * launch and confirmation batch (block sums of the windows + resolve) of the
  * sender and every whole-file-sum launch of ctx is bracketed by HIP events on
  * the stream it runs on.  rsg_kernel_times waits for them and returns
- * out[0] = total roll ms, out[1] = roll launches, out[2] = total confirmation
+ * out[0] = total roll ms, out[1] = roll launches (a launch of the small-file
+ * kernel, which rolls, confirms and walks many files at once, counts as a
+ * roll launch), out[2] = total confirmation
  * ms, out[3] = confirmation batches, out[4] = candidate offsets the rolls
  * returned, out[5] = windows confirmed, out[6] = total whole-file-sum kernel
  * ms, out[7] = its launches; reset != 0 drops the recorded events and zeroes

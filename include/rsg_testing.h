@@ -44,6 +44,14 @@ rsg_status rsg_testing_block_sums_diagnostic(rsg_ctx *ctx, int32_t diag);
 rsg_status rsg_testing_md4(const uint8_t *data, uint64_t n, int32_t seeded, int32_t seed, uint64_t piece,
                            uint8_t out[16]);
 
+/* Which path a context's sender searches take (rsg_hash_search_host /
+ * _device / _batch_*): 0 (default) = sources of at most 1 MiB with at most
+ * 1024 basis blocks of at most 8 KiB through the one-wave-per-file kernel
+ * (rsync_amd/csrc/rsg_search_small.hip), everything else through the
+ * large-file pipeline; 1 = every source through the pipeline.  Results are
+ * identical; the tests run the golden searches both ways. */
+rsg_status rsg_testing_set_search_path(rsg_ctx *ctx, int32_t mode);
+
 /* rsg_generate_files_fd_multi's per-rank record queue: *peak (if not NULL)
  * = the largest number of record bytes any rank had queued during the last
  * call; cap != 0 sets the bound per rank for later calls (default 256 MiB,

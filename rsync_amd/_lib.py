@@ -196,6 +196,7 @@ _PROTOS = {
     "rsg_testing_md4": (_st, [_vp, _u64, _i32, _i32, _u64, _vp]),
     "rsg_testing_block_sums_diagnostic": (_st, [_vp, _i32]),
     "rsg_testing_multi_queue": (_st, [_u64, ctypes.POINTER(_u64)]),
+    "rsg_testing_set_search_path": (_st, [_vp, _i32]),
 }
 
 for _name, (_res, _args) in _PROTOS.items():

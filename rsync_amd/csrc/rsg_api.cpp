@@ -303,6 +303,15 @@ void rsg_ctx_destroy(rsg_ctx *c) {
         if (sl.rolled) hipEventDestroy(sl.rolled);
         if (sl.confirmed) hipEventDestroy(sl.confirmed);
     }
+    for (SmallSlot &sl : c->small) {
+        if (sl.dev.p) hipFree(sl.dev.p);
+        if (sl.count.p) hipFree(sl.count.p);
+        PinBuf *ps[] = {&sl.stage, &sl.outs, &sl.matches};
+        for (PinBuf *b : ps)
+            if (b->p) hipHostFree(b->p);
+        if (sl.up) hipEventDestroy(sl.up);
+        if (sl.done) hipEventDestroy(sl.done);
+    }
     PinBuf *pbs[] = {&c->h_in[0], &c->h_in[1], &c->h_out[0], &c->h_out[1], &c->h_desc[0], &c->h_desc[1]};
     for (PinBuf *b : pbs)
         if (b->p) hipHostFree(b->p);

@@ -65,6 +65,16 @@ struct SearchSlot {
 };
 constexpr int kSearchSlots = 4;  // jobs i-1 (walk on a worker), i (confirming), i+1 (rolling), i+2 (being issued)
 
+// One launch slot of the small-file sender (rsg_sender_small.cpp): pinned
+// staging of the launch's descriptors, sums and host sources, its device
+// copy, the per-file results and match lists (pinned: the kernel writes them
+// straight to host memory) and the launch's match counter.
+struct SmallSlot {
+    PinBuf stage, outs, matches;
+    DevBuf dev, count;
+    hipEvent_t up = nullptr, done = nullptr;
+};
+
 struct rsg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -79,6 +89,8 @@ struct rsg_ctx {
     PinBuf h_in[2], h_out[2], h_desc[2];
     // sender scratch
     SearchSlot search[kSearchSlots];
+    SmallSlot small[2];
+    int search_path = 0;  // 0: small files through the one-launch kernel, 1: every file through the pipeline
     DevBuf d_res;
     // multi-GPU
     ncclComm_t comm = nullptr;
@@ -180,6 +192,15 @@ struct Md4 {
     void update(const uint8_t *p, uint64_t n);
     void final(uint8_t out[16]);
 };
+
+// The small-file sender (rsg_sender_small.cpp): settles every job of a
+// search batch that is invalid, empty or eligible for the one-wave-per-file
+// kernel; `rest` = the jobs for the large-file pipeline (not eligible, or
+// candidates past the kernel's LDS list), in job order; msg[i] = job i's
+// error message.  Returns a fatal (HIP / allocation) status or RSG_OK.
+bool search_small_eligible(const rsg_ctx *ctx, const rsg_search_job &j);
+rsg_status search_small_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed, bool host_src,
+                              std::vector<uint64_t> &rest, std::vector<std::string> &msg);
 
 // Kernel timing helpers (no-ops unless ctx->timing): begin records an event
 // on `stream` and returns it; end records the closing event.

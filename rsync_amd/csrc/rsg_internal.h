@@ -139,6 +139,40 @@ int roll_packed();  // RSG_ROLL_PACKED (read once): 0 roll_kernel only, else the
 // / tile_scan passes): each workgroup reads B extra bytes once.
 constexpr uint32_t kFusedMaxB = 4 * kScanTile;
 
+// ---- small-file sender (rsg_search_small.hip): one wave searches one source
+// file end to end (basis sums into LDS, weak sum at every offset, MD4
+// confirmation, the greedy walk), so many small files cost one launch.
+constexpr uint32_t kSmallMaxSrc = 1u << 20;    // source bytes
+constexpr int32_t kSmallMaxCount = 1024;       // basis blocks
+constexpr uint32_t kSmallMaxBlock = 8192;      // block length (each lane sums a window of B bytes)
+struct SmallJob {        // 40 bytes, one per file of a launch
+    uint64_t src;        // device address of the source
+    uint64_t sums;       // byte offset in the launch's blob of sum1[count] | targets[count] | sum2[16 count]
+    uint32_t size;       // source length, 1..kSmallMaxSrc
+    int32_t count;       // 1..kSmallMaxCount
+    uint32_t blen;       // SumHead block length (1..kSmallMaxBlock)
+    uint32_t rem;        // SumHead remainder (0 = the last block is full)
+    uint32_t s2len;      // bytes of sum2 compared (0..16)
+    uint32_t pad;
+};
+static_assert(sizeof(SmallJob) == 40, "SmallJob layout");
+struct SmallOut {        // per file: matches at [base, base + n) of the launch's match array
+    uint32_t base, n;
+    uint32_t status;     // 0 ok, 1 more candidates than the LDS list holds, 2 match array full
+    uint32_t ncand;      // weak-sum candidates (filter hits) the roll found
+};
+// LDS words of one wave for a launch whose counts are <= kc (a power of two):
+// filter (reused for the confirmation results) | keys (u64, kc) | candidates (u64, ccap)
+inline uint32_t small_ccap(uint32_t kc) { return kc * 2 < 512 ? 512 : kc * 2; }
+inline uint32_t small_fwords(uint32_t kc) { return kc * 4 < 512 ? 512 : kc * 4; }
+inline uint32_t small_lds_bytes(uint32_t kc) {
+    const uint32_t f = small_fwords(kc) > small_ccap(kc) ? small_fwords(kc) : small_ccap(kc);
+    return 4 * f + 8 * kc + 8 * small_ccap(kc) + 16;
+}
+hipError_t launch_search_small(const SmallJob *jobs, const uint32_t *order, uint32_t njobs, const uint8_t *blob,
+                               uint32_t seed, uint32_t kc, void *matches, uint32_t match_cap,
+                               uint32_t *match_count, SmallOut *outs, hipStream_t stream);
+
 // ---- whole-file sums (rsg_filesums.hip)
 struct FileSpan {
     uint64_t offset;  // byte offset of the file in the arena

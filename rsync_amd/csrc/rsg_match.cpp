@@ -1274,6 +1274,47 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
     return first;
 }
 
+// A search batch: small sources through the one-wave-per-file kernel
+// (rsg_sender_small.cpp), the rest -- and any small source whose candidates
+// overflowed that kernel's lists -- through the pipeline above.  Each job's
+// result is the same either way.  Returns RSG_OK or the first failing job's
+// status (job order) with its message.
+rsg_status search_jobs(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed, bool host_src) {
+    if (njobs && !jobs) return fail(ctx, RSG_ERR_INVALID, "NULL jobs");
+    std::vector<uint64_t> rest;
+    std::vector<std::string> msg;
+    rsg_status fatal = search_small_batch(ctx, jobs, njobs, seed, host_src, rest, msg);
+    struct Drain {  // the small path's kernels write pinned host memory: nothing outlives the call
+        rsg_ctx *c;
+        ~Drain() {
+            for (int k = 0; k < 2; k++) (void)hipStreamSynchronize(c->side[k]);
+        }
+    } drain{ctx};
+    if (fatal != RSG_OK) {
+        const std::string m = ctx->err;
+        for (uint64_t i = 0; i < njobs; i++)
+            if (jobs[i].status == RSG_OK) jobs[i].status = fatal;
+        ctx->err = m;
+        return fatal;
+    }
+    std::string rest_err;
+    if (!rest.empty()) {
+        std::vector<rsg_search_job> sub(rest.size());
+        for (size_t k = 0; k < rest.size(); k++) sub[k] = jobs[rest[k]];
+        if (search_batch(ctx, sub.data(), sub.size(), seed, host_src) != RSG_OK) rest_err = ctx->err;
+        for (size_t k = 0; k < rest.size(); k++) {
+            jobs[rest[k]].n_matches = sub[k].n_matches;
+            jobs[rest[k]].status = sub[k].status;
+        }
+    }
+    for (uint64_t i = 0; i < njobs; i++)
+        if (jobs[i].status != RSG_OK) {
+            ctx->err = msg[i].empty() ? rest_err : msg[i];
+            return jobs[i].status;
+        }
+    return RSG_OK;
+}
+
 // ---------------------------------------------------------------- streaming sender (§8 a13)
 // io.ReadFull-style pread of [off, off + n) on a few threads; -1 = EOF
 // before n bytes, else 0 or an errno.
@@ -1612,14 +1653,22 @@ rsg_status rsg_hash_search_batch_device(rsg_ctx *ctx, rsg_search_job *jobs, uint
     if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
     std::lock_guard<std::recursive_mutex> lock(ctx->mu);
     RSG_HIP(ctx, hipSetDevice(ctx->device));
-    return search_batch(ctx, jobs, njobs, seed, false);
+    return search_jobs(ctx, jobs, njobs, seed, false);
 }
 
 rsg_status rsg_hash_search_batch_host(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed) {
     if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
     std::lock_guard<std::recursive_mutex> lock(ctx->mu);
     RSG_HIP(ctx, hipSetDevice(ctx->device));
-    return search_batch(ctx, jobs, njobs, seed, true);
+    return search_jobs(ctx, jobs, njobs, seed, true);
+}
+
+rsg_status rsg_testing_set_search_path(rsg_ctx *ctx, int32_t mode) {
+    if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    if (mode < 0 || mode > 1) return fail(ctx, RSG_ERR_INVALID, "search path %d (0 or 1)", mode);
+    ctx->search_path = mode;
+    return RSG_OK;
 }
 
 // The single-file calls are batches of one.
@@ -1639,7 +1688,7 @@ static rsg_status search_one(rsg_ctx *ctx, const void *src, uint64_t src_len, co
     j.targets = targets;
     j.matches = matches;
     j.match_cap = match_cap;
-    const rsg_status s = search_batch(ctx, &j, 1, seed, host_src);
+    const rsg_status s = search_jobs(ctx, &j, 1, seed, host_src);
     *n_matches = j.n_matches;
     return s;
 }

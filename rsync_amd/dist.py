@@ -220,3 +220,38 @@ def rank_records_host(eng: Engine, files: Sequence, layout: ShardLayout, rank: i
         _, rec, _ = eng.block_sums(views, seed, [p.block_len for p in g])
         out.append(rec)
     return b"".join(out)
+
+
+def records_digest(records) -> str:
+    """SHA-256 of one rank's record bytes (what it sent to the root)."""
+    import hashlib
+    return hashlib.sha256(memoryview(records).cast("B")).hexdigest()
+
+
+def all_ranks(obj, world: int) -> list:
+    """obj of every rank, in rank order, on every rank, over the control plane
+    (gloo all_gather_object); world 1 needs no process group."""
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def gather_parity(recv, digests: Sequence[str], records: Sequence[int]) -> dict:
+    """The root's check of a gather (GenerateFiles emits every file's sums in
+    file-list order, generator.go:20-52; rank q's records are the global
+    slice starting at the exclusive prefix of the ranks' counts): the
+    gathered buffer `recv` (bytes on the root) holds, at each rank's slice,
+    exactly the bytes that rank hashed -- their SHA-256 equals the digest
+    the rank reported -- and nothing beyond the last slice is expected.
+    -> {"ranks_equal": [bool per rank], "all_equal": bool}."""
+    mv = memoryview(recv).cast("B")
+    want = sum(records) * RECORD_BYTES
+    ok, o = [], 0
+    for d, n in zip(digests, records):
+        seg = mv[o:o + n * RECORD_BYTES]
+        ok.append(len(seg) == n * RECORD_BYTES and records_digest(seg) == d)
+        o += n * RECORD_BYTES
+    return {"ranks_equal": ok, "all_equal": all(ok) and len(mv) >= want}

@@ -158,6 +158,51 @@ class Conn:
         self.write(struct.pack("<i", _i32(v)))
 
 
+class SearchBatch:
+    """A prepared rsg_hash_search_batch_* call: the rsg_search_job array (with
+    every job's match array) is built once, so repeated calls time only the
+    C-ABI call itself (bench.py's cfg4-sender workload).  jobs as
+    Engine.hash_search_batch."""
+
+    def __init__(self, engine: "Engine", jobs, device: bool = True):
+        self.engine, self.device, self.n = engine, device, len(jobs)
+        self.arr = (_lib.SearchJob * max(self.n, 1))()
+        self._keep, self.outs = [], []
+        for k, (src, src_len, head, sum1, sum2, targets) in enumerate(jobs):
+            j = self.arr[k]
+            if device:
+                j.src, j.src_len = src.ptr, src_len
+            else:
+                a = _u8(src)
+                self._keep.append(a)
+                j.src, j.src_len = _ptr(a).value, a.size if src_len is None else src_len
+            j.head = head if isinstance(head, SumHead) else SumHead(*head)
+            s1 = np.ascontiguousarray(sum1, dtype=np.uint32)
+            s2 = np.ascontiguousarray(sum2, dtype=np.uint8).reshape(-1)
+            tg = np.ascontiguousarray(targets, dtype=np.int32)
+            self._keep += [s1, s2, tg]
+            j.sum1, j.sum2, j.targets = _ptr(s1).value, _ptr(s2).value, _ptr(tg).value
+            cap = j.src_len // max(j.head.block_len, 1) + 2
+            out = np.empty(cap, dtype=_MATCH_DT)
+            self.outs.append(out)
+            j.matches, j.match_cap = ctypes.cast(out.ctypes.data, ctypes.POINTER(Match)), cap
+        self._fn = lib.rsg_hash_search_batch_device if device else lib.rsg_hash_search_batch_host
+
+    def run(self, seed: int) -> int:
+        """One rsg_hash_search_batch_* call; returns its status."""
+        return self._fn(self.engine.ctx, self.arr, self.n, _i32(seed))
+
+    def status(self, k: int) -> int:
+        return self.arr[k].status
+
+    def n_matches(self, k: int) -> int:
+        return self.arr[k].n_matches
+
+    def matches(self, k: int, as_arrays: bool = False):
+        m = self.outs[k][: self.arr[k].n_matches]
+        return m if as_arrays else _matches_list(m, len(m))
+
+
 class Engine:
     """One device context (rsg_ctx): its own stream, scratch and RCCL comm."""
 
@@ -502,42 +547,24 @@ class Engine:
                           as_arrays: bool = False):
         """SendFiles' per-file hashSearch loop (sender.go:19-115) in one
         pipelined call.  jobs = [(src, src_len, head, sum1, sum2, targets)]:
-        src is a DeviceBuffer when device, else host bytes / a uint8 array
-        (src_len None = its length).  Returns one match list per job, or with
-        raise_on_error=False a list of (status, matches) pairs.  as_arrays:
-        matches stay the C-ABI's rsg_match records (numpy structured arrays
-        with fields offset / index), as a Go caller would read them."""
-        n = len(jobs)
-        arr = (_lib.SearchJob * max(n, 1))()
-        keep, outs = [], []
-        for k, (src, src_len, head, sum1, sum2, targets) in enumerate(jobs):
-            j = arr[k]
-            if device:
-                j.src, j.src_len = src.ptr, src_len
-            else:
-                a = _u8(src)
-                keep.append(a)
-                j.src, j.src_len = _ptr(a).value, a.size if src_len is None else src_len
-            j.head = head if isinstance(head, SumHead) else SumHead(*head)
-            s1 = np.ascontiguousarray(sum1, dtype=np.uint32)
-            s2 = np.ascontiguousarray(sum2, dtype=np.uint8).reshape(-1)
-            tg = np.ascontiguousarray(targets, dtype=np.int32)
-            keep += [s1, s2, tg]
-            j.sum1, j.sum2, j.targets = _ptr(s1).value, _ptr(s2).value, _ptr(tg).value
-            cap = j.src_len // max(j.head.block_len, 1) + 2
-            out = np.empty(cap, dtype=_MATCH_DT)
-            outs.append(out)
-            j.matches, j.match_cap = ctypes.cast(out.ctypes.data, ctypes.POINTER(Match)), cap
-        fn = lib.rsg_hash_search_batch_device if device else lib.rsg_hash_search_batch_host
-        st = fn(self.ctx, arr, n, _i32(seed))
-
-        def res(k):
-            m = outs[k][: arr[k].n_matches]
-            return m if as_arrays else _matches_list(m, len(m))
+        src is a DeviceBuffer (or any object with a device address in .ptr)
+        when device, else host bytes / a uint8 array (src_len None = its
+        length).  Returns one match list per job, or with raise_on_error=False
+        a list of (status, matches) pairs.  as_arrays: matches stay the
+        C-ABI's rsg_match records (numpy structured arrays with fields offset /
+        index), as a Go caller would read them."""
+        b = SearchBatch(self, jobs, device)
+        st = b.run(seed)
         if raise_on_error:
             check(st, self.ctx)
-            return [res(k) for k in range(n)]
-        return [(arr[k].status, res(k) if arr[k].status == _lib.OK else []) for k in range(n)]
+            return [b.matches(k, as_arrays) for k in range(b.n)]
+        return [(b.status(k), b.matches(k, as_arrays) if b.status(k) == _lib.OK else []) for k in range(b.n)]
+
+    def set_search_path(self, mode: int):
+        """rsg_testing_set_search_path: 0 = small sources through the
+        one-wave-per-file kernel (default), 1 = every source through the
+        large-file pipeline (identical results)."""
+        check(lib.rsg_testing_set_search_path(self.ctx, mode), self.ctx)
 
     def set_kernel_timing(self, on: bool = True):
         """rsg_set_kernel_timing: bracket the sender's kernels with HIP events."""

@@ -215,3 +215,45 @@ def test_pipelined_gather_and_d2h_one_rank(nbatch):
         sb.close()
     finally:
         eng.close()
+
+
+def _parity_worker(rank, world, port, corrupt, out):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rsync_amd.dist import all_ranks, gather_host, gather_parity, records_digest, shard_layout
+    files = _files()
+    lay = shard_layout([len(f) for f in files], world, 2, 700)
+    local = b"".join(_piece_records(files, p, cases.SEED) for g in lay.batches[rank] for p in g)
+    info = all_ranks((records_digest(local), len(local) // 20), world)
+    got = gather_host(local, lay, rank)  # the root's delivered buffer
+    if rank == 0:
+        buf = bytearray(got)
+        if corrupt is not None:  # one byte of rank `corrupt`'s slice flipped on its way to the root
+            buf[lay.rank_offset[corrupt] * 20 + 7] ^= 0x10
+        out.put(gather_parity(bytes(buf), [d for d, _ in info], [n for _, n in info]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,corrupt", [(2, None), (2, 1), (3, 0), (3, 2)])
+def test_gather_parity_detects_a_bad_slice(world, corrupt):
+    """The multi-GPU bench's self-check (bench.py measure_delivery ->
+    delivery.gather_parity): every rank's SHA-256 of its own records goes to
+    every rank over gloo, and the root compares each rank's slice of the
+    delivered buffer (rank order = file-list order, generator.go:20-52) with
+    it.  An intact gather passes on every rank; one flipped byte fails
+    exactly the rank it belongs to."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_parity_worker, args=(r, world, port, corrupt, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert res["ranks_equal"] == [corrupt is None or q != corrupt for q in range(world)]
+    assert res["all_equal"] == (corrupt is None)
