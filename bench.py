@@ -179,26 +179,8 @@ def main():
     extra = {}
     if args.ab:
         from rsync_amd import _lib
-        # (product variant, diagnostic) pairs; diagnostics write meaningless records
-        names = {(2, 0): "park", (7, 0): "park_reg", (1, 3): "diag_park_memory_only",
-                 (1, 9): "diag_park_reg_memory_only", (1, 4): "diag_park_hash_only",
-                 (1, 6): "diag_linear_read_ldsdma", (1, 5): "diag_linear_read_plain",
-                 (1, 7): "diag_linear_read_ldsdma_misaligned4", (1, 8): "diag_park_memory_only_aligned",
-                 (1, 10): "diag_stream_3w_45k_d1", (1, 11): "diag_stream_3w_21k_d3", (1, 12): "diag_stream_3w_31k_d2",
-                 (1, 13): "diag_stream_8w_8k_d1", (1, 14): "diag_stream_8w_16k_d2", (1, 15): "diag_stream_8w_31k_d2",
-                 (1, 16): "diag_stream_4w_45k_d1", (1, 17): "diag_park_swap_memory_only", (1, 18): "diag_park_swap",
-                 (1, 19): "diag_stream_3w_park_pattern", (1, 20): "diag_park_memory_no_copyout",
-                 (1, 21): "diag_park_memory_no_records", (1, 22): "diag_stream_3w_45k_8wave_wg",
-                 (1, 23): "diag_park_rec1_memory_only", (1, 24): "park_rec1_coalesced_records",
-                 (1, 25): "park_rec2_coalesced_nt_records", (1, 26): "diag_park_rec2_memory_only",
-                 (1, 27): "park_rec3_lane_nt_records", (1, 28): "park_reg_rec2", (1, 29): "diag_park_reg_rec2_memory_only",
-                 (1, 30): "park_rec4_nt_sc1", (1, 31): "park_rec5_nt_sc0_sc1", (1, 32): "park_round4_lane_records",
-                 (1, 33): "diag_stream_rw_interleaved_1tile", (1, 34): "diag_stream_rw_contiguous_1tile",
-                 (1, 35): "diag_stream_rw_contiguous_8tiles", (1, 36): "diag_stream_r_park_pattern_8wave",
-                 (1, 37): "diag_stream_rw_contiguous_4tiles", (1, 38): "diag_stream_rw_contiguous_16tiles",
-                 (1, 39): "diag_stream_rw_contiguous_32tiles", (1, 40): "diag_stream_rw_interleaved_8tiles",
-                 (1, 41): "park_rec6_ring8", (1, 42): "diag_park_rec6_memory_only",
-                 (12, 0): "lpark", (1, 54): "diag_lpark_memory_only"}
+        # the shipped block-sum variants on the same plan (identical records)
+        names = {2: "park", 1: "staged_seg256", 4: "staged_seg128", 14: "pipe_seg512", 0: "direct"}
         only = os.environ.get("AB_ONLY")  # comma-separated substrings: A/B only the matching entries
         if only:
             names = {v: n for v, n in names.items() if any(o in n for o in only.split(","))}
@@ -206,8 +188,7 @@ def main():
         for _ in range(int(os.environ.get("AB_ROUNDS", "5"))):
             for v in names:
                 print(f"ab: {names[v]}", file=sys.stderr, flush=True)
-                eng.set_block_sums_kernel(v[0])
-                eng.set_block_sums_diagnostic(v[1])
+                eng.set_block_sums_kernel(v)
                 for i in range(3):
                     step(i)
                 a0 = torch.cuda.Event(enable_timing=True)
@@ -219,8 +200,7 @@ def main():
                 eng.synchronize(sptr)
                 res[v].append(a0.elapsed_time(a1) / args.steps)
         eng.set_block_sums_kernel(-1)
-        eng.set_block_sums_diagnostic(0)
-        step(0)  # the records hold the product kernel's output again (diagnostics write garbage)
+        step(0)
         eng.synchronize(sptr)
         extra["ab_kernel_ms"] = {names[v]: [round(x, 4) for x in sorted(res[v])] for v in names}
         # consecutive batches on two streams (the generator's two-slot

@@ -34,8 +34,10 @@
 extern "C" {
 #endif
 
-#define RSG_ABI_VERSION 3  /* 2: per-context block-sum kernel knob, multi-GPU calls, rsg_hash_search_fd;
-                              3: rsg_hash_search_fd_batch */
+#define RSG_ABI_VERSION 4  /* 2: per-context block-sum kernel knob, multi-GPU calls, rsg_hash_search_fd;
+                              3: rsg_hash_search_fd_batch;
+                              4: block-sum variants pruned to the shipped set (-1, 0, 1, 2, 3, 4, 6, 14),
+                                 small sources searched by the one-wave-per-file kernel */
 /* One wire record: int32 LE sum1 then sum2[16] (generator.go:341-346). */
 #define RSG_RECORD_BYTES 20
 #define RSG_SUM2_BYTES 16
@@ -148,31 +150,20 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
  * block per segment), 2 = park (three loader waves stream 64-block tiles
  * through LDS, five hasher waves park the blocks in registers; blocks <= 703
  * bytes, otherwise 1 is used), 3 = deep per-lane prefetch for long blocks,
- * 4 / 5 = staged with 128- / 512-byte segments, 6 = staged for blocks at
- * any byte offset (pieces fetched from the 4-byte aligned address below the
- * block, funnel-shifted in registers; needs a 4-byte aligned arena, else 3),
- * 7 = park with register-staged loaders, 8 / 9 = staged with 128- / 256-byte
- * segments and two slabs per wave (a segment's DMA issues two segments
- * ahead), 10 / 11 = staged with 128- / 256-byte segments in persistent
- * workgroups (each wave loops over 64-block groups), 12 = long park (park's
- * ring streaming 704-byte segments of 64-block groups, MD4 states kept in
- * LDS across segments), 13 / 14 / 15 = persistent staged with 128- / 512- /
- * 256-byte segments where each wave requests its next group's first segment
- * before hashing the current group's last one.  Automatic: aligned batches
- * take 2 when 512 <= the largest block <= 703 bytes; 4 when it is
- * 704..32768 bytes and every block starts on a 128-byte line (block length
- * and file offsets multiples of 128; the library's own packing keeps file
- * offsets so); otherwise for 704..8192 bytes 14 unless 512-byte
- * segments through the block's tail chunk read over 1.2x its length (then
- * 1); for 8193..24576 bytes (blocks not on 128-byte lines), 14 when the
- * persistent grid's rounds over the batch's 64-block groups are at least
- * 60 % full, else 1; 1 for all other lengths; unaligned batches (a
- * block not 4-byte aligned) take 6 (3 for blocks >= 8 KiB, else 0, when the
- * arena itself is not 4-byte aligned; 1, 2, 4, 5 and 7-15 fall back to 0
- * there).  The environment variable RSG_BLOCKSUMS_KERNEL sets a new
- * context's initial value.  Returns RSG_ERR_INVALID outside -1..15.  (Timing
- * diagnostics that write meaningless records live in include/rsg_testing.h,
- * not here.) */
+ * 4 = staged with 128-byte segments, 6 = staged for blocks at any byte
+ * offset (pieces fetched from the 4-byte aligned address below the block,
+ * funnel-shifted in registers; needs a 4-byte aligned arena, else 3 / 0),
+ * 14 = persistent staged with 512-byte segments, each wave requesting its
+ * next group's first segment before hashing the current group's last one.
+ * Automatic, in two lines: unaligned blocks -> 6; aligned: 512..703 bytes ->
+ * park (2); on 128-byte lines up to 32 KiB -> 4 (the library's own packing
+ * keeps file offsets on 128-byte lines, so B a multiple of 128 qualifies);
+ * up to 24 KiB when 512-byte segments read at most 1.2 B per block -> 14;
+ * otherwise 1.  The LDS-DMA variants fall back to 0 for blocks that are not
+ * 4-byte aligned.  The environment variable RSG_BLOCKSUMS_KERNEL sets a new
+ * context's initial value.  Returns RSG_ERR_INVALID for any other value
+ * (the variants numbered 5, 7..13 and 15 in ABI 3 were measured slower and
+ * removed; tools/build_ab.sh rebuilds them from the history). */
 rsg_status rsg_set_block_sums_kernel(rsg_ctx *ctx, int32_t variant);
 
 /* Fallback census of ctx's device since the last reset: counts[0] = full

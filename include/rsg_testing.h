@@ -24,16 +24,13 @@ rsg_status rsg_testing_walk(const uint64_t *cand, uint64_t n, const int32_t *tru
                             const rsg_sum_head *head, rsg_match *out, uint64_t cap, uint64_t *n_out,
                             uint64_t stats[2]);
 
-/* Timing diagnostics for DESIGN.md's roofline analysis, on one context:
- * while diag != 0 every aligned block-sum launch of ctx runs the diagnostic
- * instead of the product kernel and the "records" it writes are
- * meaningless.  1 = staged memory only, 2 = staged hashing only, 3 = park
- * memory only, 4 = park hashing only, 5 = linear read of the arena (plain
- * loads), 6 = linear read (LDS DMA), 7 = linear read (LDS DMA) 4 bytes off
- * 16-byte alignment, 8 = park memory only with 16-byte aligned requests,
- * 9.. = further memory-pattern diagnostics (rsg_blocksums.hip lists them).
- * 0 = off (default). */
-rsg_status rsg_testing_block_sums_diagnostic(rsg_ctx *ctx, int32_t diag);
+/* The block-sum kernel variant a launch takes (host arithmetic, the rule
+ * rsg_set_block_sums_kernel documents): variant (-1 = automatic) for a batch
+ * whose blocks are all 4-byte aligned (aligned), all on 128-byte lines
+ * (lines128), in a 4-byte aligned arena (arena_aligned4), longest block
+ * max_blen.  -2 for a variant rsg_set_block_sums_kernel rejects. */
+int32_t rsg_testing_block_sums_choice(int32_t variant, int32_t aligned, int32_t lines128, int32_t arena_aligned4,
+                                      uint32_t max_blen);
 
 /* The product's host MD4 (RFC 1320; rsync_amd/csrc/rsg_md4_host.cpp), used
  * for whole-file sums whose bytes stream through host memory: the sender's

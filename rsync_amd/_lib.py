@@ -24,7 +24,7 @@ RECORD_BYTES = 20
 FILESUM_PLAIN = 0   # MD4(file), rsyncchecksum.go:60-66
 FILESUM_SEEDED = 1  # MD4(int32_LE(seed) || file), match.go:52-53
 CHUNK_SIZE = 256 * 1024
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 OK = 0
 ERR_INVALID = -1
@@ -194,7 +194,7 @@ _PROTOS = {
     "rsg_testing_walk": (_st, [_vp, _u64, _vp, _u64, ctypes.POINTER(SumHead), ctypes.POINTER(Match), _u64,
                                ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "rsg_testing_md4": (_st, [_vp, _u64, _i32, _i32, _u64, _vp]),
-    "rsg_testing_block_sums_diagnostic": (_st, [_vp, _i32]),
+    "rsg_testing_block_sums_choice": (_i32, [_i32, _i32, _i32, _i32, ctypes.c_uint32]),
     "rsg_testing_multi_queue": (_st, [_u64, ctypes.POINTER(_u64)]),
     "rsg_testing_set_search_path": (_st, [_vp, _i32]),
 }

@@ -164,11 +164,11 @@ rsg_status launch_plan(rsg_ctx *ctx, const HostPlan &plan, const void *d_files, 
     if (!d_arena || !d_records) return fail(ctx, RSG_ERR_INVALID, "NULL device pointer");
     const bool aligned = plan.aligned && (((uintptr_t)d_arena & 3u) == 0);
     const bool lines128 = plan.lines128 && (((uintptr_t)d_arena & 127u) == 0);
+    (void)d_scratch;
     RSG_HIP(ctx, rsg::launch_block_sums((const uint8_t *)d_arena, plan.arena_bytes, (const DevFile *)d_files,
                                         (const uint32_t *)d_wg, plan.total_blocks, plan.nwg, aligned,
-                                        plan.max_blen, (uint32_t)seed, (uint8_t *)d_records,
-                                        (uint32_t *)d_scratch, plan.lds_reserve, ctx->bs_variant, ctx->bs_diag,
-                                        stream, lines128));
+                                        plan.max_blen, (uint32_t)seed, (uint8_t *)d_records, plan.lds_reserve,
+                                        ctx->bs_variant, stream, lines128));
     return RSG_OK;
 }
 
@@ -463,18 +463,16 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
 
 rsg_status rsg_set_block_sums_kernel(rsg_ctx *ctx, int32_t variant) {
     RSG_ENTER(ctx);
-    if (variant < -1 || variant > rsg::kBlockSumsVariantMax)
-        return fail(ctx, RSG_ERR_INVALID, "variant must be -1..%d", rsg::kBlockSumsVariantMax);
+    if (!rsg::block_sums_variant_valid(variant))
+        return fail(ctx, RSG_ERR_INVALID, "variant %d: one of -1, 0, 1, 2, 3, 4, 6, 14", variant);
     ctx->bs_variant = variant;
     return RSG_OK;
 }
 
-rsg_status rsg_testing_block_sums_diagnostic(rsg_ctx *ctx, int32_t diag) {
-    RSG_ENTER(ctx);
-    if (diag < 0 || diag > rsg::kBlockSumsDiagMax)
-        return fail(ctx, RSG_ERR_INVALID, "diagnostic must be 0..%d", rsg::kBlockSumsDiagMax);
-    ctx->bs_diag = diag;
-    return RSG_OK;
+int32_t rsg_testing_block_sums_choice(int32_t variant, int32_t aligned, int32_t lines128, int32_t arena_aligned4,
+                                      uint32_t max_blen) {
+    if (!rsg::block_sums_variant_valid(variant)) return -2;
+    return rsg::block_sums_choice(variant, aligned != 0, lines128 != 0, arena_aligned4 != 0, max_blen);
 }
 
 rsg_status rsg_block_sums_fallbacks(rsg_ctx *ctx, uint64_t counts[2], int32_t reset) {

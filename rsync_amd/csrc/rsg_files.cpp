@@ -73,12 +73,14 @@ rsg_status launch_file_sums_staged(rsg_ctx *ctx, const void *d_arena, uint64_t a
     const uint64_t ooff = (n * sizeof(rsg::FileSpan) + 63) & ~63ull;
     uint8_t *hd = (uint8_t *)ctx->h_desc[slot].p;
     lane_order((const rsg::FileSpan *)hd, (uint32_t)n, (uint32_t *)(hd + ooff));
+    bool aligned4 = ((uintptr_t)d_arena & 3u) == 0;
+    for (uint64_t i = 0; i < n && aligned4; i++) aligned4 = (((const rsg::FileSpan *)hd)[i].offset & 3u) == 0;
     uint8_t *dd = (uint8_t *)ctx->d_desc[slot].p;
     RSG_HIP(ctx, hipMemcpyAsync(dd, hd, ooff + n * 4, hipMemcpyHostToDevice, stream));
     hipEvent_t t0 = timed_begin(ctx, stream);
     RSG_HIP(ctx, rsg::launch_file_sums((const uint8_t *)d_arena, arena_bytes, (const rsg::FileSpan *)dd,
                                        (const uint32_t *)(dd + ooff), (uint32_t)n, (uint32_t)mode, (uint32_t)seed,
-                                       (uint8_t *)d_out, stream));
+                                       (uint8_t *)d_out, aligned4, stream));
     timed_end(ctx, t0, stream, 2);
     return RSG_OK;
 }

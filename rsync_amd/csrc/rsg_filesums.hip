@@ -165,19 +165,6 @@ __device__ __forceinline__ void fs_hash_lane(const uint8_t *__restrict__ arena, 
     fs_tail(X, L, h);
 }
 
-__global__ __launch_bounds__(64) void file_sums_kernel(const uint8_t *__restrict__ arena, uint64_t arena_bytes,
-                                                       const FileSpan *__restrict__ files,
-                                                       const uint32_t *__restrict__ order, uint32_t nfiles,
-                                                       uint32_t mode, uint32_t seed, uint8_t *__restrict__ out) {
-    const uint32_t lane_file = blockIdx.x * blockDim.x + threadIdx.x;
-    if (lane_file >= nfiles) return;
-    const uint32_t fi = order[lane_file];
-    uint32_t h[4];
-    fs_hash_lane(arena, arena_bytes, files[fi], mode == 1 ? 4u : 0u, seed, h);
-    uint32_t *o = reinterpret_cast<uint32_t *>(out + 16ull * fi);
-    o[0] = h[0]; o[1] = h[1]; o[2] = h[2]; o[3] = h[3];
-}
-
 // ---------------------------------------------------------------- staged variant
 // The ring kernel above gathers every 16-byte load from 64 different files
 // (64 cache lines per wave instruction): the CU's address path, not HBM,
@@ -197,17 +184,26 @@ __global__ __launch_bounds__(64) void file_sums_kernel(const uint8_t *__restrict
 // so message chunk c = (carry, data words 16 c .. 16 c + 14) with carry =
 // the data word before them -- the data stream is read from the file's own
 // start, never before it.
-constexpr uint32_t kFsUnits = 17;
-constexpr uint32_t kFsPiece = 16 * kFsUnits;  // 272 bytes of LDS per file
-constexpr uint32_t kFsSlab = 64 * kFsPiece;   // 17408 bytes per wave
-constexpr uint32_t kFsDma = kFsSlab / 1024;   // 17 DMA instructions per segment (vmcnt(17) below)
-static_assert(kFsDma == 17, "the segment wait counts 17 DMA instructions");
+// UNITS = 16: every file of the launch starts 4-byte aligned (the library's
+// own arenas pack files at 16 or 128 bytes), so a segment is exactly the
+// file's next 256 bytes -- no funnel shift and no 17th unit, which re-read
+// the first 16 bytes of the next segment (1.08x the file bytes from HBM
+// with 17 units, profiles/r05ba_filesums_summary.json).
+template <int UNITS>
+struct FsShape {
+    static constexpr uint32_t kPiece = 16 * UNITS;  // LDS bytes per file
+    static constexpr uint32_t kSlab = 64 * kPiece;  // per wave
+    static constexpr uint32_t kDma = kSlab / 1024;  // DMA instructions per segment (= UNITS)
+    static_assert(kDma == UNITS, "one DMA instruction per unit of every file");
+};
 
-template <bool SEEDED, int AUX>
+template <bool SEEDED, int AUX, int UNITS>
 __global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict__ arena, uint64_t arena_bytes,
                                                        const FileSpan *__restrict__ files,
                                                        const uint32_t *__restrict__ order, uint32_t nfiles,
                                                        uint32_t seed, uint8_t *__restrict__ out) {
+    constexpr uint32_t kFsUnits = UNITS, kFsPiece = FsShape<UNITS>::kPiece, kFsSlab = FsShape<UNITS>::kSlab,
+                       kFsDma = FsShape<UNITS>::kDma;
     __shared__ __attribute__((aligned(16))) uint8_t slab[2 * kFsSlab];  // two segments in flight
     const uint32_t lane = threadIdx.x;
     const uint32_t lane_file = blockIdx.x * 64 + lane;
@@ -218,11 +214,11 @@ __global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict
     const uint64_t L = F.len + pre;
     const uint64_t nfull = L >> 6;                 // the tail chunk's index
     const uint64_t nseg64 = nfull / 4 + 1;         // segments through the tail chunk
-    const uint32_t sh = (uint32_t)(F.offset & 3u);
+    const uint32_t sh = UNITS == 16 ? 0u : (uint32_t)(F.offset & 3u);
     const uint64_t fstart = F.offset - sh;         // data read from here (4-byte aligned)
-    // staged when every lane's needed bytes [fstart, fstart + 256 nseg + 16)
+    // staged when every lane's needed bytes [fstart, fstart + 256 nseg (+ 16))
     // lie inside the arena (segment counts kept to 32 bits)
-    const bool ok = nseg64 < (1ull << 31) && fstart + 256 * nseg64 + 16 <= arena_bytes;
+    const bool ok = nseg64 < (1ull << 31) && fstart + 256 * nseg64 + (UNITS == 16 ? 0 : 16) <= arena_bytes;
     if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
         if (!active) return;
         uint32_t h[4];
@@ -279,9 +275,13 @@ __global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict
     const uint32_t tail_seg = (uint32_t)(nfull / 4), tail_i = (uint32_t)(nfull % 4);
 #pragma unroll 1
     for (uint32_t s = 0; s < S; s++) {
-        // segment s has landed once at most the younger segment's 17 DMAs are pending
-        if (s + 1 < S) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // segment s has landed once at most the younger segment's UNITS DMAs are pending
+        if (s + 1 < S) {
+            if constexpr (UNITS == 17) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         RSG_FS_READ(s & 1u);
         if (s + 2 < S) RSG_FS_DMA(s + 2, s & 1u);  // in flight while segments s and s + 1 hash
         if (s <= tail_seg && s < nseg) {
@@ -290,7 +290,10 @@ __global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict
                 if (s == tail_seg && i > tail_i) break;
                 uint32_t D[16];
 #pragma unroll
-                for (int k = 0; k < 16; k++) D[k] = __builtin_amdgcn_alignbyte(R[16 * i + k + 1], R[16 * i + k], sh);
+                for (int k = 0; k < 16; k++) {
+                    if constexpr (UNITS == 17) D[k] = __builtin_amdgcn_alignbyte(R[16 * i + k + 1], R[16 * i + k], sh);
+                    else D[k] = R[16 * i + k];
+                }
                 if (SEEDED) {
                     X[0] = carry;
 #pragma unroll
@@ -314,32 +317,17 @@ __global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict
 }
 
 hipError_t launch_file_sums(const uint8_t *arena, uint64_t arena_bytes, const FileSpan *files, const uint32_t *order,
-                            uint32_t nfiles, uint32_t mode, uint32_t seed, uint8_t *out, hipStream_t stream) {
+                            uint32_t nfiles, uint32_t mode, uint32_t seed, uint8_t *out, bool aligned4,
+                            hipStream_t stream) {
     if (nfiles == 0) return hipSuccess;
     // one-wave workgroups: the longest-first lane order then gives an LPT
-    // schedule over the SIMDs (the second round of waves takes the shorter files)
-    // RSG_FILESUMS_KERNEL: 0 = ring, 1 = staged with nt DMA, 2 = staged with
-    // the default cache policy (A/B)
-    static const int variant = [] {
-        const char *e = getenv("RSG_FILESUMS_KERNEL");
-        return e ? atoi(e) : 2;
-    }();
+    // schedule over the SIMDs (the second round of waves takes the shorter
+    // files); the default cache policy (nt DMA re-read neighbouring units,
+    // 1.47x the file bytes, profiles/r03d_filesums_summary.json)
     const dim3 grid((nfiles + 63) / 64), block(64);
-    if (variant == 0)
-        hipLaunchKernelGGL(file_sums_kernel, grid, block, 0, stream, arena, arena_bytes, files, order, nfiles, mode,
-                           seed, out);
-    else if (variant == 1 && mode == 1)
-        hipLaunchKernelGGL((file_sums_staged<true, 2>), grid, block, 0, stream, arena, arena_bytes, files, order,
-                           nfiles, seed, out);
-    else if (variant == 1)
-        hipLaunchKernelGGL((file_sums_staged<false, 2>), grid, block, 0, stream, arena, arena_bytes, files, order,
-                           nfiles, seed, out);
-    else if (mode == 1)
-        hipLaunchKernelGGL((file_sums_staged<true, 0>), grid, block, 0, stream, arena, arena_bytes, files, order,
-                           nfiles, seed, out);
-    else
-        hipLaunchKernelGGL((file_sums_staged<false, 0>), grid, block, 0, stream, arena, arena_bytes, files, order,
-                           nfiles, seed, out);
+    auto kern = mode == 1 ? (aligned4 ? file_sums_staged<true, 0, 16> : file_sums_staged<true, 0, 17>)
+                          : (aligned4 ? file_sums_staged<false, 0, 16> : file_sums_staged<false, 0, 17>);
+    hipLaunchKernelGGL(kern, grid, block, 0, stream, arena, arena_bytes, files, order, nfiles, seed, out);
     return hipGetLastError();
 }
 

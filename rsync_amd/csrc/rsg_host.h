@@ -105,10 +105,8 @@ struct rsg_ctx {
     bool timing = false;
     std::mutex spans_mu;  // spans and stat_* (a search's tail records them from a worker thread)
     std::vector<TimedSpan> spans;
-    // block-sum kernel knobs of this context (rsg_set_block_sums_kernel;
-    // rsg_testing_block_sums_diagnostic): -1 = automatic; 0 = no diagnostic
+    // block-sum kernel variant of this context (rsg_set_block_sums_kernel): -1 = automatic
     int bs_variant = -1;
-    int bs_diag = 0;
     uint64_t stat_candidates = 0, stat_windows = 0;  // roll candidates read back, windows confirmed
 };
 

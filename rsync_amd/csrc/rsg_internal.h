@@ -23,12 +23,15 @@ struct DevFile {
 };
 static_assert(sizeof(DevFile) == 32, "DevFile layout");
 
-// variant / diag: the calling context's knobs (-1 automatic; 0 no diagnostic).
+// variant: the calling context's knob (-1 automatic, rsg_set_block_sums_kernel).
 hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const DevFile *files,
                              const uint32_t *wg_file, uint64_t total_blocks, uint32_t nwg, bool aligned,
-                             uint32_t max_blen, uint32_t seed, uint8_t *out, uint32_t *scratch,
-                             uint32_t lds_reserve, int variant, int diag, hipStream_t stream,
-                             bool lines128 = false);
+                             uint32_t max_blen, uint32_t seed, uint8_t *out, uint32_t lds_reserve, int variant,
+                             hipStream_t stream, bool lines128 = false);
+// The variant a launch takes (rsg_blocksums.hip: the automatic rule and the
+// fallbacks of variants a batch cannot take); host arithmetic.
+int block_sums_choice(int variant, bool aligned, bool lines128, bool arena_aligned4, uint32_t max_blen);
+bool block_sums_variant_valid(int variant);  // -1, 0, 1, 2, 3, 4, 6, 14
 // Files packed into an arena by the library start at multiples of this, so
 // blocks whose length is a multiple of 128 start on 128-byte lines
 constexpr uint64_t kPackAlign = 128;
@@ -37,13 +40,6 @@ inline uint64_t pack_round(uint64_t n) { return (n + kPackAlign - 1) & ~(kPackAl
 // Device scratch a block-sum launch needs: 4 + 4 * ceil(total_blocks / 64) bytes.
 inline uint64_t block_sums_scratch_bytes(uint64_t total_blocks) { return 8 + 4 * ((total_blocks + 63) / 64); }
 
-// Product variants (-1 auto, 0 direct, 1 staged, 2 park, 3 long, 4/5 staged
-// with 128/512-byte segments, 6 staged at any byte offset, 7 park with
-// register-staged loaders) and timing
-// diagnostics (0 off, 1..kBlockSumsDiagMax; outputs meaningless),
-// rsg_blocksums.hip; both per context (rsg_ctx::bs_variant / bs_diag).
-constexpr int kBlockSumsVariantMax = 15;
-constexpr int kBlockSumsDiagMax = 63;
 // RSG_BLOCKSUMS_KERNEL (read once): a context's initial variant.
 int block_sums_variant_env();
 // Fallback census of the current device: [0] staged waves, [1] park tiles
@@ -180,8 +176,11 @@ struct FileSpan {
 };
 // out[16 * i] = MD4 of file i: mode 0 MD4(file), mode 1 MD4(int32_LE(seed) || file).
 // order = a permutation of the files (lane k hashes file order[k]).
+// aligned4: every file offset (and the arena) 4-byte aligned -- segments of
+// exactly 256 file bytes, no funnel shift.
 hipError_t launch_file_sums(const uint8_t *arena, uint64_t arena_bytes, const FileSpan *files, const uint32_t *order,
-                            uint32_t nfiles, uint32_t mode, uint32_t seed, uint8_t *out, hipStream_t stream);
+                            uint32_t nfiles, uint32_t mode, uint32_t seed, uint8_t *out, bool aligned4,
+                            hipStream_t stream);
 
 hipError_t launch_fill_splitmix64(uint8_t *dst, uint64_t n, uint64_t seed, hipStream_t stream);
 

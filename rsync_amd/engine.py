@@ -260,12 +260,6 @@ class Engine:
         (-1 automatic; every variant gives identical records)."""
         check(lib.rsg_set_block_sums_kernel(self.ctx, variant), self.ctx)
 
-    def set_block_sums_diagnostic(self, diag: int):
-        """rsg_testing_block_sums_diagnostic (test hook): while diag != 0 this
-        context's aligned block-sum launches run a timing diagnostic and write
-        meaningless records."""
-        check(lib.rsg_testing_block_sums_diagnostic(self.ctx, diag), self.ctx)
-
     def block_sums_fallbacks(self, reset: bool = True) -> Tuple[int, int]:
         """Fallback census (rsg_block_sums_fallbacks): (staged waves, park
         tiles) of full 64-block groups hashed with per-lane loads instead of

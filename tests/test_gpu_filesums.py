@@ -83,3 +83,27 @@ def test_file_sums_bad_mode(eng):
     from rsync_amd import _lib
     with pytest.raises(_lib.RsgError):
         eng.file_sums([b"abc"], 7)
+
+
+def test_file_sums_device_aligned_segments(eng):
+    """Every file 4-byte aligned (16-byte packed, as the library's arenas):
+    the staged kernel's exact 256-byte segments (no funnel shift, no 17th
+    unit), with lengths around the segment and MD4 padding boundaries, waves
+    whose lanes run past each other's last segment, and a last file ending
+    exactly at the arena end (the per-lane fallback for its wave)."""
+    import rsync_amd
+    rng = np.random.default_rng(23)
+    lens = [int(x) for x in rng.integers(0, 70_000, 900)] + [0, 1, 55, 56, 63, 64, 251, 252, 255, 256, 257, 4096]
+    offs, o = [], 0
+    for n in lens:
+        offs.append(o)
+        o += (n + 15) & ~15
+    arena_bytes = offs[-1] + lens[-1]
+    host = cases.splitmix64_bytes(24, arena_bytes)
+    arena = eng.alloc(arena_bytes)
+    arena.upload(host)
+    for mode, seed in ((rsync_amd.FILESUM_PLAIN, 0), (rsync_amd.FILESUM_SEEDED, -7)):
+        out = eng.file_sums_device(arena, list(zip(offs, lens)), mode, seed)
+        got = out.download(16 * len(lens)).reshape(-1, 16)
+        for i, (off, n) in enumerate(zip(offs, lens)):
+            assert got[i].tobytes() == orc.file_sum(mode, seed, host[off:off + n]), (i, off, n, mode)

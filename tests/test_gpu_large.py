@@ -133,10 +133,8 @@ def _run(eng, unaligned, variant, B, seed=cases.SEED):
     return files, kinds, rec, first, fb
 
 
-@pytest.mark.parametrize("variant,B", [(-1, 700), (2, 700), (7, 700), (1, 700), (4, 700), (4, 1024), (1, 131072),
-                                       (-1, 131072), (5, 4096), (8, 4096), (9, 131072), (10, 4096), (11, 131072), (12, 700), (12, 1024),
-                                       (12, 4096), (12, 131072),
-                                       (13, 1024), (13, 4096), (14, 4096), (15, 4096), (14, 131072)])
+@pytest.mark.parametrize("variant,B", [(-1, 700), (2, 700), (1, 700), (4, 700), (4, 1024), (1, 131072),
+                                       (-1, 131072), (-1, 4096), (14, 1024), (14, 4096), (14, 131072)])
 def test_aligned_arena_past_4gib(eng, variant, B):
     """Aligned batch on a 5 GiB arena: park (regular and irregular tiles) and
     the staged kernels, every checked record equal to the oracle's and not one
@@ -338,30 +336,3 @@ def test_cfg3_real_size_vs_oracle(eng):
     src.free()
 
 
-def test_lpark_arena_end_exact(eng):
-    """The long park kernel (variant 12) on an arena that ends exactly at the
-    last block's last byte, with a full last group whose last block is short
-    (cfg2's layout: 64 files of 1 MiB at B = 700, 1498 blocks each, 64 x 1498
-    a multiple of 64): the last block's final 16-byte request would run past
-    the arena, so that group takes the per-lane path; every record equals
-    the oracle's."""
-    import rsync_amd
-    nf, size, B = 64, 1 << 20, 700
-    files = [cases.splitmix64_bytes(7100 + i, size) for i in range(nf)]
-    want = b"".join(orc.block_sums(f, B, cases.SEED) for f in files)
-    arena = eng.alloc(nf * size)
-    for i, f in enumerate(files):
-        arena.upload(f, offset=i * size)
-    plan = eng.plan([(i * size, size, B) for i in range(nf)], nf * size)
-    recs = eng.alloc(plan.total_records * 20)
-    try:
-        eng.set_block_sums_kernel(12)
-        plan.run(arena, cases.SEED, recs)
-        eng.synchronize()
-    finally:
-        eng.set_block_sums_kernel(-1)
-    got = recs.download(plan.total_records * 20).tobytes()
-    plan.close()
-    recs.free()
-    arena.free()
-    assert got == want

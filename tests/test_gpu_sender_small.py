@@ -77,8 +77,9 @@ def _job(k, seed, rng):
     s2len = int(rng.choice([16, 16, 16, 3, 0]))
     head = (head[0], head[1], s2len, head[3])
     tg = orc.stable_targets(s1)
-    if kind == 5 and tg.size > 1:  # another valid tie order (Go's sort.Slice is unstable)
-        tg = rng.permutation(tg).astype(np.int32)
+    if kind == 5 and tg.size > 1:  # another valid tie order among equal tags (Go's sort.Slice is unstable)
+        tags = ((s1 & 0xFFFF) + (s1 >> 16)) & 0xFFFF
+        tg = np.lexsort((rng.random(tg.size), tags)).astype(np.int32)
     return src, head, s1, s2, tg
 
 
@@ -128,7 +129,8 @@ def test_cfg4_shaped_sampled_vs_oracle(eng):
     """BASELINE cfg4's file shape for the sender: 1024 sources of 4-64 KiB
     against 50 %-modified bases (reference sizing: B = 700) in one batch call;
     every job equals the oracle's hashSearch, and the small-file kernel, not
-    the pipeline, settled them (kernel timing records no roll launch)."""
+    the pipeline, settled them (kernel timing: small-file launches count as
+    rolls; the pipeline's confirmation batches would show, none does)."""
     seed = cases.SEED
     rng = np.random.default_rng(4)
     batch, want, bufs = [], [], []
@@ -151,4 +153,4 @@ def test_cfg4_shaped_sampled_vs_oracle(eng):
         eng.set_kernel_timing(False)
     assert sum(len(w) for w in want) > 20_000
     assert got == want
-    assert t["roll_launches"] == 0
+    assert 1 <= t["roll_launches"] <= 4 and t["confirm_batches"] == 0, t

@@ -33,18 +33,11 @@ SHAPES = [  # (files, file bytes, block length, arenas)
     (256, 4 << 20, 4112, 2),
     (1, 1 << 30, 32768, 2),       # 8: one 1 GiB file at the reference's sizing (B = sqrt(len) = 32768)
 ]
-VARIANTS = {-1: "automatic", 1: "staged", 4: "staged_seg128", 5: "staged_seg512", 8: "staged_seg128_db", 9: "staged_db", 10: "staged_seg128_persist",
-            11: "staged_persist", 12: "lpark", 13: "pipe_seg128", 14: "pipe_seg512", 15: "pipe", 2: "park",
+VARIANTS = {-1: "automatic", 1: "staged", 4: "staged_seg128", 14: "pipe_seg512", 2: "park",
             3: "long_deep_prefetch"}
-DIAGS = {1: "diag_staged_memory_only", 45: "diag_staged_seg128_memory_only", 43: "diag_staged_seg128_db_memory_only",
-         44: "diag_staged_db_memory_only", 2: "diag_staged_hash_only", 6: "diag_linear_read_ldsdma",
-         46: "diag_stream3_contig32k", 47: "diag_stream3_strided512", 48: "diag_stream3_strided128",
-         51: "diag_stream8_contig32k", 49: "diag_stream8_strided512", 50: "diag_stream8_strided128",
-         52: "diag_staged_seg128_persist_memory_only", 53: "diag_staged_persist_memory_only",
-         54: "diag_lpark_memory_only", 55: "diag_stream8_strided512_seq", 56: "diag_stream8_strided128_seq",
-         57: "diag_stream3_strided512_seq", 58: "diag_staged_seg512_memory_only",
-         59: "diag_staged_seg512_persist_memory_only", 60: "staged_seg512_persist",
-         61: "diag_pipe_seg128_memory_only", 62: "diag_pipe_seg512_memory_only", 63: "diag_pipe_memory_only"}
+# SWEEP_SQRT=1: the reference's own block length B = int(sqrt(len)) (rsynccommon.go:22) for files of
+# len = 1, 2, 3, 5, 9, 17, 33, 64 MiB, ~1 GiB of them per shape, at the library's 128-byte packing
+SQRT_LENS_MIB = [1, 2, 3, 5, 9, 17, 33, 64]
 
 
 def main():
@@ -62,8 +55,11 @@ def main():
     # SWEEP_BLENS="1000,4000": 256 x 4 MiB files at each of those block lengths instead
     if os.environ.get("SWEEP_BLENS"):
         shapes = [(256, 4 << 20, int(b), 2) for b in os.environ["SWEEP_BLENS"].split(",")]
+    if os.environ.get("SWEEP_SQRT"):
+        import math
+        shapes = [(max(1, (1 << 30) // (m << 20)), m << 20, int(math.isqrt(m << 20)), 2) for m in SQRT_LENS_MIB]
     rounds = int(os.environ.get("SWEEP_ROUNDS", "1"))
-    only = os.environ.get("SWEEP_ONLY")  # comma-separated variant / diagnostic names
+    only = os.environ.get("SWEEP_ONLY")  # comma-separated variant names
     for nf, fb, blen, narena in shapes:
         total = nf * fb
         arenas = [eng.alloc(total) for _ in range(narena)]
@@ -74,11 +70,9 @@ def main():
         recs = eng.alloc(plan.total_records * rsync_amd.RECORD_BYTES)
         eng.synchronize(sp)
         res = {}
-        runs = [(v, 0, name) for v, name in VARIANTS.items()] + [(1, d, name) for d, name in DIAGS.items()]
+        runs = [(v, name) for v, name in VARIANTS.items()]
         if only:
-            runs = [r for r in runs if r[2] in only.split(",")]
-        if total >= (4 << 30):  # the linear-read ceilings run on <= 4 GiB arenas only
-            runs = [r for r in runs if r[1] not in (5, 6)]
+            runs = [r for r in runs if r[1] in only.split(",")]
         # the memory clock ramps up over the first ~15 ms of launches: warm up
         # before the first variant so it is not timed on a cold card
         eng.set_block_sums_kernel(-1)
@@ -87,9 +81,8 @@ def main():
         while time.perf_counter() - w0 < 0.3:
             plan.run(arenas[0], SEED, recs, stream=sp)
             eng.synchronize(sp)
-        for v, d, name in [r for _ in range(rounds) for r in runs]:
+        for v, name in [r for _ in range(rounds) for r in runs]:
             eng.set_block_sums_kernel(v)
-            eng.set_block_sums_diagnostic(d)
             steps = 5 if total > (4 << 30) else 30
             print(f"shape {nf}x{fb} B={blen}: {name}", file=sys.stderr, flush=True)
             for i in range(10):
@@ -109,7 +102,6 @@ def main():
                 r["rounds_ms"] = prev.get("rounds_ms", [prev["kernel_ms"]]) + [r["kernel_ms"]]
             res[name] = r
         eng.set_block_sums_kernel(-1)
-        eng.set_block_sums_diagnostic(0)
         print(json.dumps({"files": nf, "file_bytes": fb, "block_len": blen, "records": plan.total_records,
                           "variants": res}), flush=True)
         plan.close()
