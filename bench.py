@@ -1312,7 +1312,7 @@ def bench_receive(args, rank, world, local):
     (receiver.go:117-120).  MD4 is one serial chain per file: a single file
     (rsg_receive_data) is hashed on the host as its tokens are applied (on the
     GPU it would get one lane, ~10x slower than a core: measured here too with
-    RSG_RECV_MD4=gpu on the 1 MiB file); the batched call
+    recv_md4 = GPU (rsg_testing_search_option 5) on the 1 MiB file); the batched call
     (rsg_receive_data_batch) hashes many files at once on the GPU, one lane
     per file, and sends a batch's few large files to host threads when that
     is faster (its cost split).  Streams: every block of an identical basis
@@ -1352,11 +1352,11 @@ def bench_receive(args, rank, world, local):
              "md4_on": "host (fused with token application)",
              "cpu_md4_1core_s": round(t_cpu, 4), "cpu_md4_1core_gib_s": round(size / t_cpu / GIB, 4)}
         if size <= (1 << 20):
-            os.environ["RSG_RECV_MD4"] = "gpu"
+            eng.set_option("recv_md4", 1)
             try:
                 (out, used), dg = timed(lambda: eng.receive_data(stream, head, data, seed), 5)
             finally:
-                del os.environ["RSG_RECV_MD4"]
+                eng.set_option("recv_md4", 0)
             r["gpu_one_lane_s"] = round(dg, 4)
         res[f"single_{name}"] = r
         del data, stream, out
@@ -1378,11 +1378,11 @@ def bench_receive(args, rank, world, local):
                     "cpu_md4_1core_gib_s": round(n * size / t_cpu / GIB, 4)}
         if n >= 64:
             for mode in ("host", "gpu"):
-                os.environ["RSG_RECV_MD4"] = mode
+                eng.set_option("recv_md4", 2 if mode == "host" else 1)
                 try:
                     _, dh = timed(lambda: eng.receive_data_batch(jobs, seed), 3)
                 finally:
-                    del os.environ["RSG_RECV_MD4"]
+                    eng.set_option("recv_md4", 0)
                 res[tag]["all_host_threads_gib_s" if mode == "host" else "all_gpu_lanes_gib_s"] = \
                     round(n * size / dh / GIB, 3)
 

@@ -41,13 +41,22 @@ int32_t rsg_testing_block_sums_choice(int32_t variant, int32_t aligned, int32_t 
 rsg_status rsg_testing_md4(const uint8_t *data, uint64_t n, int32_t seeded, int32_t seed, uint64_t piece,
                            uint8_t out[16]);
 
-/* Which path a context's sender searches take (rsg_hash_search_host /
- * _device / _batch_*): 0 (default) = sources of at most 1 MiB with at most
- * 1024 basis blocks of at most 8 KiB through the one-wave-per-file kernel
- * (rsync_amd/csrc/rsg_search_small.hip), everything else through the
- * large-file pipeline; 1 = every source through the pipeline.  Results are
- * identical; the tests run the golden searches both ways. */
-rsg_status rsg_testing_set_search_path(rsg_ctx *ctx, int32_t mode);
+/* Per-context options of the sender and receiver, for tests and same-box
+ * A/B runs (the defaults are the measured product settings; results are the
+ * same under every value):
+ *   0 search path: 0 (default) = sources of at most 1 MiB with at most 1024
+ *     basis blocks of at most 8 KiB through the one-wave-per-file kernel
+ *     (rsync_amd/csrc/rsg_search_small.hip), the rest through the
+ *     large-file pipeline; 1 = every source through the pipeline;
+ *   1 host-built roll tables (0 default: built on the GPU);
+ *   2 report every GPU-built bucket table as overflowed, so the rolls pass
+ *     every filter hit on and the confirmation alone decides (0 default);
+ *   3 speculative selection of the confirmed windows (0 default);
+ *   4 CUs a batch's rolls leave to the previous job's confirmation (default
+ *     32; 0 = confirmations serialised behind the rolls);
+ *   5 receiveData's whole-file sums: 0 (default) by file size, 1 GPU, 2 host.
+ * RSG_ERR_INVALID for an unknown option or value. */
+rsg_status rsg_testing_search_option(rsg_ctx *ctx, int32_t option, int32_t value);
 
 /* rsg_generate_files_fd_multi's per-rank record queue: *peak (if not NULL)
  * = the largest number of record bytes any rank had queued during the last

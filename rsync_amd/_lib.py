@@ -196,10 +196,12 @@ _PROTOS = {
     "rsg_testing_md4": (_st, [_vp, _u64, _i32, _i32, _u64, _vp]),
     "rsg_testing_block_sums_choice": (_i32, [_i32, _i32, _i32, _i32, ctypes.c_uint32]),
     "rsg_testing_multi_queue": (_st, [_u64, ctypes.POINTER(_u64)]),
-    "rsg_testing_set_search_path": (_st, [_vp, _i32]),
+    "rsg_testing_search_option": (_st, [_vp, _i32, _i32]),
 }
 
 for _name, (_res, _args) in _PROTOS.items():
+    if os.environ.get("RSG_LIB_PATH") and not hasattr(lib, _name):
+        continue  # an A/B build of another revision may predate a newer entry point
     _f = getattr(lib, _name)  # AttributeError here = symbol missing from librsg.so
     _f.restype = _res
     _f.argtypes = _args

@@ -90,7 +90,16 @@ struct rsg_ctx {
     // sender scratch
     SearchSlot search[kSearchSlots];
     SmallSlot small[2];
-    int search_path = 0;  // 0: small files through the one-launch kernel, 1: every file through the pipeline
+    // per-context options of the sender and receiver (rsg_testing_search_option;
+    // the defaults are the measured product settings)
+    struct Options {
+        int path = 0;              // 0: small sources through the one-wave-per-file kernel; 1: all through the pipeline
+        bool host_tables = false;  // the roll's filters and bucket table built on the host instead of the GPU
+        bool force_table_ovf = false;  // report the GPU-built bucket table as overflowed (its fallback's tests)
+        bool spec = false;         // speculative selection of the confirmed windows (Walker::spec_batch)
+        int confirm_cus = 32;      // CUs a batch's rolls leave to the previous job's confirmation (0: serial)
+        int recv_md4 = 0;          // receiveData's whole-file sums: 0 by size, 1 GPU, 2 host
+    } opts;
     DevBuf d_res;
     // multi-GPU
     ncclComm_t comm = nullptr;

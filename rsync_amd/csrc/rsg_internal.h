@@ -77,7 +77,6 @@ __host__ __device__ inline uint32_t sel_word(uint32_t s) { return (s >> 2) & 0x7
 __host__ __device__ inline uint32_t sel_mask(uint32_t s) {
     return (1u << ((s >> 24) & 31u)) | (1u << (((s >> 29) | (s << 3)) & 31u));
 }
-bool roll_filter_sel();  // the bit-selection layout (default; RSG_FILTER_SEL=0, read once, selects the hash)
 
 // Exact table of basis weak sums: buckets of kBucketWays u64 entries
 // {sum1 << 32 | flags}; a sum lives in bucket hash1 or hash2.
@@ -111,10 +110,10 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
 // memory; *ovf = 1 if some key found no slot (rsg_match_kernels.hip).
 hipError_t launch_build_tables(const uint32_t *sum1, int32_t count, uint32_t B, uint32_t rem, bool packed,
                                uint32_t *bitmap, uint16_t *filter16, uint64_t *table, uint32_t *keys, uint32_t nb,
-                               uint32_t *ovf, hipStream_t stream);
+                               uint32_t *ovf, bool force_ovf, hipStream_t stream);
 // The packed roll's filter (roll_packed_kernel, fused mode, interior tiles):
 // 2^16 16-bit words, word ((s1 + 128 B) xor s2) mod 2^16, bits s2[0..3],
-// s2[4..7] and (by default) s2[8..11].  s1 of a long window of random bytes is
+// s2[4..7] and s2[8..11] (a third bit: 0.6 % false hits instead of 1.0 %).  s1 of a long window of random bytes is
 // a sum of B terms (near-Gaussian mod 2^16): a word indexed by s1 alone passed
 // 1.9 % of real window sums with two bits, the xor with s2 ~1.0 %.
 constexpr uint32_t kFilter16Words = 1u << 16;
@@ -125,12 +124,9 @@ __host__ __device__ inline uint32_t f16_word(uint32_t sum, uint32_t B) {
 // s (v_pk_lshlrev_b16 masks the count to 4 bits itself), so every tested bit
 // lands in bit 15 of its half and the AND of the shifted words is the test,
 // read by sign compares with no mask.
-__host__ __device__ inline uint32_t f16_mask(uint32_t sum, int nbits = 2) {
-    const uint32_t m = (0x8000u >> ((sum >> 16) & 15u)) | (0x8000u >> ((sum >> 20) & 15u));
-    return nbits == 3 ? m | (0x8000u >> ((sum >> 24) & 15u)) : m;
+__host__ __device__ inline uint32_t f16_mask(uint32_t sum) {
+    return (0x8000u >> ((sum >> 16) & 15u)) | (0x8000u >> ((sum >> 20) & 15u)) | (0x8000u >> ((sum >> 24) & 15u));
 }
-int roll_filter_bits();  // RSG_ROLL_BITS (read once): bits per sum in the packed roll's filter, 2 or 3
-int roll_packed();  // RSG_ROLL_PACKED (read once): 0 roll_kernel only, else the packed roll (default)
 // Block lengths up to which roll derives its window sums itself (no tile_agg
 // / tile_scan passes): each workgroup reads B extra bytes once.
 constexpr uint32_t kFusedMaxB = 4 * kScanTile;

@@ -87,7 +87,6 @@ struct PhaseTimer {
     }
 };
 
-constexpr int kConfirmCus = 32;  // default RSG_CONFIRM_CUS (0 / 16 / 24 / 32 / 40 / 48 / 64 measured)
 
 struct Search {
     PhaseTimer pt;
@@ -158,16 +157,9 @@ void sort_offsets(std::vector<uint64_t> &C, int lowbit = 0) {
     }
 }
 
-// Flags of the events the host waits on.  RSG_BLOCKING_SYNC=1 (A/B): the
-// waiting thread sleeps instead of spinning, leaving its core to the table
-// builders and walks on the worker threads.
-unsigned sync_event_flags() {
-    static const unsigned f = [] {
-        const char *e = getenv("RSG_BLOCKING_SYNC");
-        return (unsigned)hipEventDisableTiming | ((e && e[0] == '1') ? (unsigned)hipEventBlockingSync : 0u);
-    }();
-    return f;
-}
+// Flags of the events the host waits on (spin-waits: a blocking-sync
+// event measured no better beside the table builders and walks).
+unsigned sync_event_flags() { return hipEventDisableTiming; }
 
 // Issue the next job's stage 1 (its roll queues behind this job's on the
 // compute stream) once its tables, built on a worker thread, are ready;
@@ -298,11 +290,6 @@ rsg_status verify(Search &S, const std::vector<uint64_t> &C, std::vector<int32_t
 //  * the sparse test scans up to kSparseBatch pending candidates; a dense
 //    verdict is remembered up to the last candidate it scanned, so a dense
 //    stretch does not rescan them every round trip.
-static bool walk_debug() {
-    static const bool on = getenv("RSG_WALK_DEBUG") != nullptr;
-    return on;
-}
-
 struct Walker {
     int64_t end = 0;   // visited offsets are < end (match.go:70)
     uint64_t size = 0;
@@ -313,24 +300,17 @@ struct Walker {
     uint64_t dense_until = 0;           // candidates below this offset were judged dense
     uint32_t width = 2;                 // successors per chain step in a dense stretch
 
-    bool spec = spec_on();              // speculative selection of sparse batches
+    bool spec = false;                  // speculative selection of sparse batches (rsg_ctx::Options::spec)
 
     uint32_t window(uint64_t q) const { return (uint32_t)std::min<uint64_t>((uint64_t)head.block_len, size - q); }
     int64_t len_of(int32_t i) const { return (i == head.count - 1 && head.rem != 0) ? head.rem : head.block_len; }
 
-    // RSG_CONFIRM_SPEC=1: speculative selection of sparse batches.  Off by
-    // default: it confirms 15 % fewer windows on cfg3 (19 957 against 23 515
-    // per GiB) but must sort the roll's list before queueing them and costs
-    // a round trip where a guess fails, while without it the confirmation is
-    // queued straight from the list; cfg3 1014-1038 against 1002-1058 GiB/s,
-    // two interleaved rounds (profiles/r05q_cfg3_confirm_ab.txt).
-    static bool spec_on() {
-        static const bool on = [] {
-            const char *e = getenv("RSG_CONFIRM_SPEC");
-            return e && e[0] == '1';
-        }();
-        return on;
-    }
+    // Speculative selection of sparse batches (rsg_ctx::Options::spec): off
+    // by default -- it confirms 15 % fewer windows on cfg3 (19 957 against
+    // 23 515 per GiB) but must sort the roll's list before queueing them and
+    // costs a round trip where a guess fails, while without it the
+    // confirmation is queued straight from the list; cfg3 1014-1038 against
+    // 1002-1058 GiB/s, two interleaved rounds (profiles/r05q_cfg3_confirm_ab.txt).
     // Candidate j sits in a chain: another candidate exactly B before or after
     // it, as consecutive matched blocks give (match.go:158 moves the walk
     // from a match at q to q + B).  A random false weak hit almost never does.
@@ -439,10 +419,6 @@ struct Walker {
                 }
                 last_dense = dense;
                 consumed = 0;
-                if (known && walk_debug())  // RSG_WALK_DEBUG: why a job with known results needs another round trip
-                    fprintf(stderr, "[rsg walk] extra round trip at candidate %zu/%zu offset %llu (pos %llu, %s, batch %zu)\n",
-                            i, C.size(), (unsigned long long)c, (unsigned long long)pos, dense ? "dense" : "sparse",
-                            batch.size());
                 batches++;
                 windows += batch.size();
                 rsg_status s = verify(batch, res);
@@ -468,6 +444,7 @@ rsg_status walk(Search &S, const std::vector<uint64_t> &C, uint64_t &pos, std::v
     w.end = S.end;
     w.size = S.size;
     w.head = S.head;
+    w.spec = S.ctx->opts.spec;
     w.out = &S.out;
     w.verify = [&S, &C](const std::vector<uint32_t> &idx, std::vector<int32_t> &res) { return verify(S, C, res, idx); };
     return w.run(C, pos, known);
@@ -490,6 +467,7 @@ rsg_status confirm_all(Search &S, uint32_t n, uint64_t pos, std::vector<uint64_t
     w.end = S.end;
     w.size = S.size;
     w.head = S.head;
+    w.spec = S.ctx->opts.spec;
     // Without the speculative selection every candidate is confirmed, so the
     // confirmation is queued straight from the roll's list in its append
     // order, and the host sorts while the GPU hashes (sorting first kept the
@@ -609,16 +587,8 @@ rsg_status confirm_all_tail(Search &S, const std::vector<uint64_t> &C, const std
 // roll can start before part B exists.  Part B is what the confirmation's
 // resolve reads: basis sums grouped by Sum1 in targets order, their sum2s.
 // Blob layout: filter | filter16 | table | keys | groups | hi16 | sum2.
-// RSG_GPU_TABLES=0 (A/B): part A built on the host (the first job of a
-// batch waited ~0.5 ms for it with the GPU idle, r05t)
-static bool gpu_tables_on() {
-    static const bool on = [] {
-        const char *e = getenv("RSG_GPU_TABLES");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
+// Options::host_tables (tests, A/B): part A built on the host (the first job
+// of a batch waited ~0.5 ms for it with the GPU idle, r05t)
 rsg_status tables_roll(Search &S, const uint32_t *sum1, const int32_t *targets) {
     (void)targets;
     rsg_ctx *ctx = S.ctx;
@@ -632,8 +602,8 @@ rsg_status tables_roll(Search &S, const uint32_t *sum1, const int32_t *targets) 
     if (ntiles64 >= 0xFFFFFFF0ull) return fail(ctx, RSG_ERR_INVALID, "source too large");
     S.ntiles = (uint32_t)ntiles64;
     auto up = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
-    const bool packed = (uint32_t)B <= rsg::kFusedMaxB && rsg::roll_packed();
-    if (gpu_tables_on() && count > 0) {
+    const bool packed = (uint32_t)B <= rsg::kFusedMaxB;
+    if (!ctx->opts.host_tables && count > 0) {
         // the same blob layout, filled by build_tables_kernel (enqueue_scan)
         // from a copy of the Sum1 array; at least two buckets per key
         uint32_t nb = 16;
@@ -667,17 +637,10 @@ rsg_status tables_roll(Search &S, const uint32_t *sum1, const int32_t *targets) 
         bitmap.assign(rsg::kFilterBits / 32, 0);
         filter16.clear();
         if (packed) filter16.assign(rsg::kFilter16Words, 0);
-        const bool sel = rsg::roll_filter_sel();
-        const int nbits = rsg::roll_filter_bits();
         for (int32_t k = 0; k < count; k++) {
             const uint32_t key = sum1[k];
-            if (sel) {
-                bitmap[rsg::sel_word(key)] |= rsg::sel_mask(key);
-            } else {
-                const uint32_t h = rsg::filter_hash(key);
-                bitmap[rsg::filter_word(h)] |= rsg::filter_mask(h);
-            }
-            if (packed) filter16[rsg::f16_word(key, (uint32_t)B)] |= (uint16_t)rsg::f16_mask(key, nbits);
+            bitmap[rsg::sel_word(key)] |= rsg::sel_mask(key);
+            if (packed) filter16[rsg::f16_word(key, (uint32_t)B)] |= (uint16_t)rsg::f16_mask(key);
         }
     });
     // Sum1 -> flags into the 2-choice bucket table, straight from the sums.
@@ -847,7 +810,7 @@ rsg_status enqueue_scan(Search &S, const uint8_t *src, bool host_src) {
                          (const uint32_t *)(b + S.off_sum1), S.head.count, (uint32_t)S.head.block_len,
                          (uint32_t)S.head.rem, S.off_table > S.off_filter16, (uint32_t *)(b + S.off_filter),
                          (uint16_t *)(b + S.off_filter16), (uint64_t *)(b + S.off_table), (uint32_t *)(b + S.off_keys),
-                         S.bmask + 1, (uint32_t *)sl.counts.p + 1, S.side));
+                         S.bmask + 1, (uint32_t *)sl.counts.p + 1, ctx->opts.force_table_ovf, S.side));
     } else {
         RSG_HIP(ctx, hipMemcpyAsync(sl.blob.p, sl.stage.p, S.blob_a_bytes, hipMemcpyHostToDevice, S.side));
     }
@@ -924,11 +887,7 @@ rsg_status finish(Search &S) {
         // sparse range (the hashing of every candidate stays below twice the
         // range, walk()'s own batching rule): confirm them all at once
         const uint64_t range = std::min<uint64_t>((uint64_t)hi * kScanTile, S.size) - (uint64_t)lo * kScanTile;
-        static const bool all_env = [] {
-            const char *e = getenv("RSG_CONFIRM_ALL");  // A/B switch: 0 = host-built confirmation batches
-            return !(e && e[0] == '0');
-        }();
-        if (all_env && n > 0 && n <= kSparseBatch && S.size < (1ull << 42) &&
+        if (n > 0 && n <= kSparseBatch && S.size < (1ull << 42) &&
             (uint64_t)n * (uint64_t)S.head.block_len <= 2 * range + (1u << 20)) {
             auto Cs = std::make_shared<std::vector<uint64_t>>();
             auto sel = std::make_shared<std::vector<uint32_t>>();
@@ -998,35 +957,6 @@ bool job_local(rsg_status s) { return s == RSG_ERR_INVALID || s == RSG_ERR_TRUNC
 // builds job i+2's tables during confirm(i).  Two files' kernels never share
 // the CUs except the memory-bound prefix pass: a confirmation kernel (few
 // lanes, serial MD4 chains) beside a roll kernel ran 3x slower.
-// RSG_LAST_OWN=0 (A/B): the last job's confirmation on the confirmation
-// stream too, behind the previous job's
-static bool last_own() {
-    static const bool on = [] {
-        const char *e = getenv("RSG_LAST_OWN");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-// RSG_START_SERIAL=0 (A/B): the first two jobs' tables build side by side
-// before job 0's roll is queued
-static bool start_serial() {
-    static const bool on = [] {
-        const char *e = getenv("RSG_START_SERIAL");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-// RSG_START_INLINE=0 (A/B): job 0's roll tables on a worker thread too
-static bool start_inline() {
-    static const bool on = [] {
-        const char *e = getenv("RSG_START_INLINE");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int32_t seed, bool host_src) {
     if (njobs && !jobs) return fail(ctx, RSG_ERR_INVALID, "NULL jobs");
     PhaseTimer bt;  // RSG_TIMING: the call's start-up and drain
@@ -1052,8 +982,7 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
     // stream, as before)
     int dev_cus = 256;
     RSG_HIP(ctx, hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    const char *cc = getenv("RSG_CONFIRM_CUS");
-    const int spare = std::max(0, std::min(cc ? atoi(cc) : kConfirmCus, dev_cus - 1));
+    const int spare = std::max(0, std::min(ctx->opts.confirm_cus, dev_cus - 1));
     const bool split = spare > 0 && njobs > 1;  // one job: nothing to overlap its confirmation with
     std::unique_ptr<Search> live[kSearchSlots];
     // Job i's stage 1 in two steps.  prepare(i): validate the job and start
@@ -1125,7 +1054,7 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
             S->cst = ctx->confirm;
             S->roll_grid = (uint32_t)std::max(1, dev_cus - spare);
             S->confirm_lds = 8192;
-            if (i + 1 == njobs && last_own()) {
+            if (i + 1 == njobs) {
                 // the last job's confirmation has no roll to share the chip
                 // with: it queues behind its own roll on the roll stream and
                 // runs beside job i-1's, instead of after it (the drain was
@@ -1179,43 +1108,24 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
         live[i % kSearchSlots] = std::move(S);
         return RSG_OK;
     };
-    auto start = [&](uint64_t i) -> rsg_status {
-        rsg_status s = prepare(i);
-        return s != RSG_OK ? s : issue(i);
-    };
-    // RSG_SEARCH_OVERLAP=0: issue job i+1 only after job i is finished (A/B measurement)
-    const char *ov = getenv("RSG_SEARCH_OVERLAP");
-
-    const bool overlap = !(ov && ov[0] == '0');
     rsg_status fatal = RSG_OK;
     uint64_t i = 0;
-    if (!overlap) {
-        if (njobs) fatal = start(0);
-    } else if (start_serial()) {
-        // job 0 alone first: its roll queues as soon as its own tables are
-        // built (built beside job 1's they took twice as long, and the GPU
-        // idles until then); job 1's tables build while roll 0 runs
-        fatal = prepare(0, start_inline());
-        if (fatal == RSG_OK) fatal = issue(0);
-        if (fatal == RSG_OK && njobs > 1) fatal = prepare(1);
-        if (fatal == RSG_OK && njobs > 1) fatal = issue(1);
-    } else {  // the first two jobs' tables build side by side
-        for (uint64_t k = 0; k < std::min<uint64_t>(njobs, 2) && fatal == RSG_OK; k++) fatal = prepare(k);
-        for (uint64_t k = 0; k < std::min<uint64_t>(njobs, 2) && fatal == RSG_OK; k++) fatal = issue(k);
-    }
+    // job 0 alone first: its roll queues as soon as its own tables are built
+    // on this thread (built beside job 1's they took twice as long, and the
+    // GPU idles until then: +1.5 %, r05); job 1's tables build while roll 0 runs
+    if (njobs) fatal = prepare(0, true);
+    if (fatal == RSG_OK && njobs) fatal = issue(0);
+    if (fatal == RSG_OK && njobs > 1) fatal = prepare(1);
+    if (fatal == RSG_OK && njobs > 1) fatal = issue(1);
     bt.mark("b.issued");
     for (; fatal == RSG_OK && i < njobs; i++) {
-        const uint64_t ahead = overlap ? i + 2 : i + 1;
+        const uint64_t ahead = i + 2;
         // job i+2 takes job i-2's slot: that job's walk (a worker) is done by
         // now; then job i+2's tables build on a worker while job i finishes
-        // here.  With RSG_SEARCH_OVERLAP=0 job i+1 is prepared and issued
-        // after job i instead.
-        if (overlap && i >= 2 && (fatal = join(i - 2)) != RSG_OK) break;
-        if (overlap && ahead < njobs && (fatal = prepare(ahead)) != RSG_OK) break;
-        auto next = [&, ahead]() -> rsg_status {
-            if (!overlap) return ahead < njobs ? start(ahead) : RSG_OK;
-            return ahead < njobs ? issue(ahead) : RSG_OK;
-        };
+        // here
+        if (i >= 2 && (fatal = join(i - 2)) != RSG_OK) break;
+        if (ahead < njobs && (fatal = prepare(ahead)) != RSG_OK) break;
+        auto next = [&, ahead]() -> rsg_status { return ahead < njobs ? issue(ahead) : RSG_OK; };
         const int slot = (int)(i % kSearchSlots);
         Search *S = live[slot].get();
         if (!S) {
@@ -1225,7 +1135,7 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
         S->hook = next;
         S->hook_ready = [&, ahead]() {
             const Pending &pend = pends[ahead & 1];
-            return !overlap || ahead >= njobs || !pend.valid || pend.i != ahead ||
+            return ahead >= njobs || !pend.valid || pend.i != ahead ||
                    pend.tab.wait_for(std::chrono::seconds(0)) == std::future_status::ready;
         };
         rsg_status s = finish(*S);
@@ -1234,20 +1144,15 @@ rsg_status search_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs, int3
         std::function<rsg_status()> hook = std::move(S->hook);
         S->hook = nullptr;
         S->hook_ready = nullptr;
-        if (s == RSG_OK && S->tail) {
-            if (overlap) {  // the walk runs beside the next jobs' confirmations and rolls
-                tails[slot] = std::async(std::launch::async, S->tail);
-                tail_live[slot] = true;
-            } else {
-                s = S->tail();
-            }
+        if (s == RSG_OK && S->tail) {  // the walk runs beside the next jobs' confirmations and rolls
+            tails[slot] = std::async(std::launch::async, S->tail);
+            tail_live[slot] = true;
         }
         if (!tail_live[slot] && (fatal = complete(i, s)) != RSG_OK) break;
         if (hook && (fatal = hook()) != RSG_OK) {  // not run by finish() (tables not ready, or a job-local error)
             i++;
             break;
         }
-        if (!overlap) live[slot].reset();
     }
     bt.mark("b.loop");
     // the last jobs' walks (and, after a fatal error, any still running)
@@ -1663,12 +1568,21 @@ rsg_status rsg_hash_search_batch_host(rsg_ctx *ctx, rsg_search_job *jobs, uint64
     return search_jobs(ctx, jobs, njobs, seed, true);
 }
 
-rsg_status rsg_testing_set_search_path(rsg_ctx *ctx, int32_t mode) {
+rsg_status rsg_testing_search_option(rsg_ctx *ctx, int32_t option, int32_t value) {
     if (!ctx) return fail(nullptr, RSG_ERR_INVALID, "NULL context");
     std::lock_guard<std::recursive_mutex> lock(ctx->mu);
-    if (mode < 0 || mode > 1) return fail(ctx, RSG_ERR_INVALID, "search path %d (0 or 1)", mode);
-    ctx->search_path = mode;
-    return RSG_OK;
+    rsg_ctx::Options &o = ctx->opts;
+    const bool b01 = value == 0 || value == 1;
+    switch (option) {
+        case 0: if (!b01) break; o.path = value; return RSG_OK;
+        case 1: if (!b01) break; o.host_tables = value; return RSG_OK;
+        case 2: if (!b01) break; o.force_table_ovf = value; return RSG_OK;
+        case 3: if (!b01) break; o.spec = value; return RSG_OK;
+        case 4: if (value < 0 || value > 1024) break; o.confirm_cus = value; return RSG_OK;
+        case 5: if (value < 0 || value > 2) break; o.recv_md4 = value; return RSG_OK;
+        default: return fail(ctx, RSG_ERR_INVALID, "unknown option %d", option);
+    }
+    return fail(ctx, RSG_ERR_INVALID, "option %d: bad value %d", option, value);
 }
 
 // The single-file calls are batches of one.
@@ -1730,7 +1644,7 @@ rsg_status rsg_testing_walk(const uint64_t *cand, uint64_t n, const int32_t *tru
     w.size = size;
     w.head = *head;
     w.out = &found;
-    if (stats[0] == 1 || stats[0] == 2) w.spec = stats[0] == 1;  // on input: the selection mode (0 = RSG_CONFIRM_SPEC)
+    w.spec = stats[0] == 1;  // on input: the selection mode (1 = speculative; 0 / 2 = every pending candidate)
     w.verify = [truth](const std::vector<uint32_t> &idx, std::vector<int32_t> &res) {
         for (uint32_t k : idx) res[k] = truth[k];
         return RSG_OK;

@@ -1175,51 +1175,6 @@ hipError_t launch_tile_scan(const TileAgg *agg, uint32_t ntiles, TilePrefix *pre
     return hipGetLastError();
 }
 
-int roll_packed() {
-    // A/B switch RSG_ROLL_PACKED: 0 = roll_kernel for every tile, 1
-    // (default) = the packed roll for the fused mode
-    static const int v = [] {
-        const char *e = getenv("RSG_ROLL_PACKED");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return v;
-}
-
-static bool roll_edge_inside() {
-    static const bool v = [] {
-        const char *e = getenv("RSG_ROLL_EDGE");  // A/B switch: 0 = edge tiles in a separate roll_kernel launch
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
-
-bool roll_bt() {
-    static const bool v = [] {
-        const char *e = getenv("RSG_ROLL_BT");  // A/B switch: 0 = B == tile length rolls like any other B
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
-
-int roll_filter_bits() {
-    static const int v = [] {
-        // A/B switch: 2 = bits S2[0..3], S2[4..7] only; default 3 adds S2[8..11]
-        // (0.6 % instead of 1.0 % false hits: fewer parks for 2-3 more VALU
-        // per two offsets; roll 0.83-0.85 vs 0.86-0.87 ms per GiB)
-        const char *e = getenv("RSG_ROLL_BITS");
-        return (e && e[0] == '2') ? 2 : 3;
-    }();
-    return v;
-}
-
-bool roll_filter_sel() {
-    static const bool sel = [] {
-        const char *e = getenv("RSG_FILTER_SEL");  // A/B switch: 0 = the rotate-xor hash layout
-        return !(e && e[0] == '0');
-    }();
-    return sel;
-}
-
 // ------------------------------------------------------------- roll tables
 // Part A of the basis tables (rsg_match.cpp: tables_roll) built on the GPU
 // from the uploaded Sum1 array, one lane per block k: the Bloom filter bits,
@@ -1234,7 +1189,7 @@ bool roll_filter_sel() {
 // least 2 buckets per key (4 ways each), so that is reserved for pathological
 // key sets.
 __global__ __launch_bounds__(256) void build_tables_kernel(const uint32_t *__restrict__ sum1, int32_t count,
-                                                           uint32_t B, uint32_t rem, int nbits, int sel, int packed,
+                                                           uint32_t B, uint32_t rem, int packed,
                                                            uint32_t *__restrict__ bitmap,
                                                            uint32_t *__restrict__ filter16w,
                                                            unsigned long long *__restrict__ table, uint32_t bmask,
@@ -1242,15 +1197,10 @@ __global__ __launch_bounds__(256) void build_tables_kernel(const uint32_t *__res
     const int32_t k = (int32_t)(blockIdx.x * 256u + threadIdx.x);
     if (k >= count) return;
     const uint32_t v = sum1[k];
-    if (sel) {
-        atomicOr(&bitmap[sel_word(v)], sel_mask(v));
-    } else {
-        const uint32_t h = filter_hash(v);
-        atomicOr(&bitmap[filter_word(h)], filter_mask(h));
-    }
+    atomicOr(&bitmap[sel_word(v)], sel_mask(v));
     if (packed) {
         const uint32_t w = f16_word(v, B);
-        atomicOr(&filter16w[w >> 1], (f16_mask(v, nbits) & 0xffffu) << (16u * (w & 1u)));
+        atomicOr(&filter16w[w >> 1], (f16_mask(v) & 0xffffu) << (16u * (w & 1u)));
     }
     const uint32_t len = (k == count - 1 && rem != 0) ? rem : B;  // types.go: the last block may be short
     const unsigned long long f = 1u | (len == B ? 2u : 4u);
@@ -1298,10 +1248,10 @@ __global__ __launch_bounds__(256) void table_keys_kernel(const unsigned long lon
 
 hipError_t launch_build_tables(const uint32_t *sum1, int32_t count, uint32_t B, uint32_t rem, bool packed,
                                uint32_t *bitmap, uint16_t *filter16, uint64_t *table, uint32_t *keys, uint32_t nb,
-                               uint32_t *ovf, hipStream_t stream) {
+                               uint32_t *ovf, bool force_ovf, hipStream_t stream) {
     if (count <= 0) return hipSuccess;
     hipLaunchKernelGGL(build_tables_kernel, dim3(((uint32_t)count + 255) / 256), dim3(256), 0, stream, sum1, count, B,
-                       rem, roll_filter_bits(), roll_filter_sel() ? 1 : 0, packed ? 1 : 0, bitmap,
+                       rem, packed ? 1 : 0, bitmap,
                        reinterpret_cast<uint32_t *>(filter16), reinterpret_cast<unsigned long long *>(table), nb - 1,
                        ovf);
     hipError_t e = hipGetLastError();
@@ -1310,10 +1260,9 @@ hipError_t launch_build_tables(const uint32_t *sum1, int32_t count, uint32_t B, 
     hipLaunchKernelGGL(table_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, stream,
                        reinterpret_cast<const unsigned long long *>(table), n, sum1, keys);
     e = hipGetLastError();
-    // RSG_TESTING_TABLE_OVF=1: report an incomplete table anyway (tests of
-    // the rolls' every-filter-hit fallback)
-    static const bool force = getenv("RSG_TESTING_TABLE_OVF") != nullptr;
-    if (e == hipSuccess && force) e = hipMemsetAsync(ovf, 1, 4, stream);
+    // force_ovf (rsg_testing_search_option): report an incomplete table
+    // anyway (tests of the rolls' every-filter-hit fallback)
+    if (e == hipSuccess && force_ovf) e = hipMemsetAsync(ovf, 1, 4, stream);
     return e;
 }
 
@@ -1338,36 +1287,25 @@ hipError_t launch_roll(const uint8_t *src, uint64_t size, uint32_t B, uint32_t r
     if (fused && filter16) {
         // Interior tiles [tile_lo, t_int): every offset of tile t visited
         // ((t+1) T <= end) and its window and shifted-byte loads inside the
-        // source ((t+1) T + B + 48 <= size).  The packed kernel (default) takes
-        // the whole range and rolls the rest -- the source's last B bytes or
-        // so -- with its scalar edge path (RSG_ROLL_EDGE=0: a roll_kernel
-        // launch takes them).  A range with no interior tile is roll_kernel's.
+        // source ((t+1) T + B + 48 <= size).  The packed kernel takes the
+        // whole range and rolls the rest -- the source's last B bytes or so --
+        // with its scalar edge path (one launch; a separate roll_kernel
+        // launch for the edge measured the same).  A range
+        // with no interior tile is roll_kernel's.
         const uint64_t lim = std::min<uint64_t>(end, size >= (uint64_t)B + 48 ? size - B - 48 : 0);
         const uint32_t t_int = (uint32_t)std::max<uint64_t>(tile_lo, std::min<uint64_t>(tile_hi, lim / kScanTile));
         if (t_int > tile_lo) {
-            const uint32_t g = min(grid, t_int - tile_lo);
-            if (roll_edge_inside()) {
-                // the whole range: the packed kernel rolls its edge tiles itself
-                const uint32_t ga = min(grid, tile_hi - tile_lo);
-                const bool bt = B == kScanTile && roll_bt();
-                auto kern = roll_filter_bits() == 3 ? (bt ? roll_packed_kernel<3, true, true> : roll_packed_kernel<3, true, false>)
-                                                    : (bt ? roll_packed_kernel<2, true, true> : roll_packed_kernel<2, true, false>);
-                hipLaunchKernelGGL(kern, dim3(ga), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo,
-                                   t_int, tile_hi, filter16, table_keys, bmask, cand, cap, count, ovf);
-                return hipGetLastError();
-            }
-            auto kern = roll_filter_bits() == 3 ? roll_packed_kernel<3, false, false> : roll_packed_kernel<2, false, false>;
-            hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, t_int,
-                               t_int, filter16, table_keys, bmask, cand, cap, count, ovf);
-            const hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return e;
+            const uint32_t ga = min(grid, tile_hi - tile_lo);
+            // B = the tile length (the reference's B for a 1 GiB file): a
+            // tile's shifted bytes are carried into the next tile
+            auto kern = B == kScanTile ? roll_packed_kernel<3, true, true> : roll_packed_kernel<3, true, false>;
+            hipLaunchKernelGGL(kern, dim3(ga), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, t_int,
+                               tile_hi, filter16, table_keys, bmask, cand, cap, count, ovf);
+            return hipGetLastError();
         }
-        tile_lo = t_int;
-        if (tile_hi <= tile_lo) return hipSuccess;
     }
     const uint32_t g = min(grid, tile_hi - tile_lo);
-    auto kern = roll_filter_sel() ? roll_kernel<true> : roll_kernel<false>;
-    hipLaunchKernelGGL(kern, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, tile_hi, agg,
+    hipLaunchKernelGGL(roll_kernel<true>, dim3(g), dim3(kRollThreads), 0, stream, src, size, B, rem, end, tile_lo, tile_hi, agg,
                        pre, ntiles, bitmap, table, bmask, cand, cap, count, fused ? 1u : 0u, ovf);
     return hipGetLastError();
 }

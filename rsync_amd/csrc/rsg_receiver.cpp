@@ -97,16 +97,13 @@ void md4_seeded(Md4 &h, int32_t seed) {
 // ~5.5 GiB/s.  A file whose lane would take longer than the GPU path needs
 // for a whole 256 MiB batch (> ~4 MiB) is hashed on host threads instead,
 // beside the GPU pipeline: a host core does one chain at ~1 GiB/s.
-// RSG_RECV_MD4 = gpu / host forces one side (tests, A/B).
+// rsg_ctx::Options::recv_md4 = 1 (GPU) / 2 (host) forces one side (tests, A/B;
+// rsg_testing_search_option 5).
 constexpr uint64_t kHostMd4MinBytes = 4ull << 20;
 // rsg_receive_data: files at least this large apply their tokens on a second
 // thread while the caller's thread hashes behind it (one thread below: the
 // thread start costs more than it saves).
 constexpr uint64_t kPipelineMinBytes = 8ull << 20;
-int recv_md4_mode() {  // read per call: tests switch it within one process
-    const char *e = getenv("RSG_RECV_MD4");
-    return (e && !strcmp(e, "gpu")) ? 1 : ((e && !strcmp(e, "host")) ? 2 : 0);
-}
 bool on_host(const rsg_recv_job &j, int mode) {
     if (mode) return mode == 2;
     return j.out_cap >= kHostMd4MinBytes;
@@ -192,9 +189,8 @@ rsg_status rsg_receive_data(rsg_ctx *ctx, const uint8_t *tokens, uint64_t tokens
     // One file: h = MD4(seed_LE || rebuilt file) (receiver.go:117-120,166) is
     // one serial chain, hashed here as the tokens are applied -- on a GPU it
     // would get one lane, ~10x slower than this core.
-    // RSG_RECV_MD4=gpu checks it with the GPU's seeded file-sum kernel instead.
-    const char *e = getenv("RSG_RECV_MD4");
-    const bool gpu = e && !strcmp(e, "gpu");
+    // Options::recv_md4 = 1 checks it with the GPU's seeded file-sum kernel instead.
+    const bool gpu = ctx->opts.recv_md4 == 1;
     Md4 h;
     md4_seeded(h, seed);
     uint64_t sum_at = 0;
@@ -292,7 +288,7 @@ rsg_status rsg_receive_data_batch(rsg_ctx *ctx, rsg_recv_job *jobs, uint64_t njo
     // large files: a host pool beside the GPU pipeline (on_host)
     std::vector<uint8_t> is_host(njobs, 0);
     std::vector<uint64_t> host_jobs;
-    const int md4_mode = recv_md4_mode();
+    const int md4_mode = ctx->opts.recv_md4;
     for (uint64_t q = 0; q < njobs; q++)
         if (on_host(jobs[q], md4_mode)) {
             is_host[q] = 1;

@@ -98,7 +98,7 @@ struct Chunk {
 }  // namespace
 
 bool search_small_eligible(const rsg_ctx *ctx, const rsg_search_job &j) {
-    return ctx->search_path != 1 && j.src_len >= 1 && j.src_len <= rsg::kSmallMaxSrc && j.head.count >= 1 &&
+    return ctx->opts.path != 1 && j.src_len >= 1 && j.src_len <= rsg::kSmallMaxSrc && j.head.count >= 1 &&
            j.head.count <= rsg::kSmallMaxCount && j.head.block_len >= 1 &&
            (uint32_t)j.head.block_len <= rsg::kSmallMaxBlock;
 }

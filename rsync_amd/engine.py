@@ -554,11 +554,17 @@ class Engine:
             return [b.matches(k, as_arrays) for k in range(b.n)]
         return [(b.status(k), b.matches(k, as_arrays) if b.status(k) == _lib.OK else []) for k in range(b.n)]
 
+    SEARCH_OPTIONS = {"path": 0, "host_tables": 1, "force_table_ovf": 2, "spec": 3, "confirm_cus": 4, "recv_md4": 5}
+
+    def set_option(self, name: str, value: int):
+        """rsg_testing_search_option: one of SEARCH_OPTIONS on this context
+        (include/rsg_testing.h; results are identical under every value)."""
+        check(lib.rsg_testing_search_option(self.ctx, self.SEARCH_OPTIONS[name], int(value)), self.ctx)
+
     def set_search_path(self, mode: int):
-        """rsg_testing_set_search_path: 0 = small sources through the
-        one-wave-per-file kernel (default), 1 = every source through the
-        large-file pipeline (identical results)."""
-        check(lib.rsg_testing_set_search_path(self.ctx, mode), self.ctx)
+        """0 = small sources through the one-wave-per-file kernel (default),
+        1 = every source through the large-file pipeline."""
+        self.set_option("path", mode)
 
     def set_kernel_timing(self, on: bool = True):
         """rsg_set_kernel_timing: bracket the sender's kernels with HIP events."""

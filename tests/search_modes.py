@@ -1,8 +1,8 @@
-"""Run by tests/test_gpu_match.py in a child process, so that switches the
-library reads once per process (RSG_GPU_TABLES, RSG_TESTING_TABLE_OVF,
-RSG_CONFIRM_SPEC) take effect: the golden match cases and seeded random
-searches through the C-ABI against the C oracle.  Prints "ok <n>" on success,
-raises on the first mismatch."""
+"""Used by tests/test_gpu_match.py::test_search_modes_vs_oracle on a context
+whose search options (rsg_testing_search_option) were changed: the golden
+match cases, seeded random searches and a multi-job batch through the C-ABI
+against the C oracle.  Returns the number of searches checked; raises on the
+first mismatch."""
 import json
 import os
 import sys
@@ -17,9 +17,7 @@ import cases  # noqa: E402
 from oracle import oracle as orc  # noqa: E402
 
 
-def main():
-    import rsync_amd
-    eng = rsync_amd.Engine(0)
+def check_all(eng):
     gold = json.load(open(os.path.join(HERE, "golden", "match_cases.json")))
     n = 0
     for name, (src, basis, blen, seed) in sorted(cases.match_cases().items()):
@@ -61,9 +59,4 @@ def main():
         want.append(orc.hash_search(src, head, s1, s2, tg, seed)[0])
     assert eng.hash_search_batch(jobs, 0x1BADB002, device=False) == want
     n += len(jobs)
-    eng.close()
-    print("ok", n)
-
-
-if __name__ == "__main__":
-    main()
+    return n

@@ -164,17 +164,16 @@ def test_identical_large_property(eng):
 
 @pytest.mark.parametrize("seed_case", range(4))
 @pytest.mark.parametrize("recv_md4", ["default", "gpu"])
-def test_delta_round_trip_on_gpu(eng, seed_case, recv_md4, monkeypatch):
+def test_delta_round_trip_on_gpu(eng, seed_case, recv_md4):
     """The whole delta path through the C-ABI: receiver block sums of the
     basis (generator.go:325-350) -> sender search (match.go:21-230) -> tokens
     (token.go) + whole-file sum (GPU file-sum kernel) -> receiveData
     (receiver.go:98-188) rebuilds the source and passes the seeded MD4 check
     (default: the host MD4 fused with token application, one file being one
-    serial chain; RSG_RECV_MD4=gpu: the GPU's file-sum kernel); a flipped sum
+    serial chain; recv_md4 = gpu: the GPU's file-sum kernel, rsg_testing_search_option 5); a flipped sum
     byte is reported as corruption (receiver.go:171-173)."""
     import rsync_amd
-    if recv_md4 != "default":
-        monkeypatch.setenv("RSG_RECV_MD4", recv_md4)
+    eng.set_option("recv_md4", 1 if recv_md4 == "gpu" else 0)
     rng = np.random.default_rng(900 + seed_case)
     basis = cases.splitmix64_bytes(910 + seed_case, int(rng.integers(50_000, 2_000_000)))
     src = cases.mutate(basis, 920 + seed_case, 0.4, 1, 5000, n_ins=3, n_del=3)
@@ -196,6 +195,7 @@ def test_delta_round_trip_on_gpu(eng, seed_case, recv_md4, monkeypatch):
     with pytest.raises(rsync_amd.RsgError) as e:
         eng.receive_data(bytes(bad), head, basis, seed)
     assert e.value.status == rsync_amd._lib.ERR_CORRUPT
+    eng.set_option("recv_md4", 0)
 
 
 @pytest.mark.gpu
@@ -340,18 +340,17 @@ def test_long_blocks_prefix_pass(eng, blen):
 
 
 @pytest.mark.parametrize("mode", ["auto", "gpu", "host"])
-def test_receive_data_batch(eng, mode, monkeypatch):
+def test_receive_data_batch(eng, mode):
     """rsg_receive_data_batch over a transfer's worth of files (RecvFiles'
     per-file receiveData, receiver.go:18-188): 48 random delta streams plus
     edge jobs -- a flipped whole-file sum byte (RSG_ERR_CORRUPT, receiver.go:
     171-173), a stream cut before its sum, a match token without a basis
     (RSG_ERR_INVALID), an empty file -- each job's status and bytes equal the
     oracle's receive_data; the good jobs are unaffected by the bad ones.
-    mode: which side checks the whole-file sums (RSG_RECV_MD4; auto = the
-    batch's cost split)."""
+    mode: which side checks the whole-file sums (rsg_testing_search_option
+    5; auto = the batch's cost split)."""
     import rsync_amd
-    if mode != "auto":
-        monkeypatch.setenv("RSG_RECV_MD4", mode)
+    eng.set_option("recv_md4", {"auto": 0, "gpu": 1, "host": 2}[mode])
     from rsync_amd import _lib
     seed = 0x5EED
     jobs, want = [], []
@@ -385,6 +384,7 @@ def test_receive_data_batch(eng, mode, monkeypatch):
     assert e.value.status == _lib.ERR_CORRUPT
     assert [r[:2] for r in eng.receive_data_batch([j for j, w in zip(jobs, want) if w[0] == _lib.OK], seed)] \
         == [(w[1], w[2]) for w in want if w[0] == _lib.OK]
+    eng.set_option("recv_md4", 0)
 
 
 def test_receive_data_batch_mixed_sizes(eng):
@@ -417,18 +417,21 @@ def test_receive_data_batch_mixed_sizes(eng):
             assert data == orc.receive_data(jobs[k][0], jobs[k][1], jobs[k][2], seed)[0], k
 
 
-@pytest.mark.parametrize("env", [{"RSG_GPU_TABLES": "0"}, {"RSG_TESTING_TABLE_OVF": "1"}, {"RSG_CONFIRM_SPEC": "1"}],
-                         ids=["host_tables", "table_overflow_fallback", "speculative_selection"])
-def test_search_modes_vs_oracle(env):
-    """The search's other modes, each in a child process (the library reads
-    these switches once): roll tables built on the host; a GPU-built table
-    reported incomplete, so the rolls pass every filter hit on as a candidate
-    and the confirmation alone decides; the speculative confirmation batches.
-    Golden cases and random searches against the oracle in every mode."""
-    import subprocess
-    import sys
-    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "search_env_check.py")
-    r = subprocess.run([sys.executable, script], env={**os.environ, **env}, capture_output=True, text=True,
-                       timeout=110)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    assert r.stdout.strip().startswith("ok"), r.stdout
+@pytest.mark.parametrize("option,value", [("host_tables", 1), ("force_table_ovf", 1), ("spec", 1), ("confirm_cus", 0),
+                                          ("path", 1)])
+def test_search_modes_vs_oracle(option, value):
+    """The search's other modes, each on a fresh context
+    (rsg_testing_search_option): roll tables built on the host; a GPU-built
+    table reported incomplete, so the rolls pass every filter hit on as a
+    candidate and the confirmation alone decides; the speculative
+    confirmation batches; confirmations serialised behind the rolls; every
+    source through the large-file pipeline.  Golden cases, random searches
+    and a multi-job batch against the oracle in every mode."""
+    import rsync_amd
+    import search_modes
+    eng = rsync_amd.Engine(0)
+    try:
+        eng.set_option(option, value)
+        assert search_modes.check_all(eng) > 20
+    finally:
+        eng.close()
