@@ -333,7 +333,11 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     uint32_t n = 0;
     if (g < total_blocks) locate_block(files, wg_file, g, off, n, wave_first / kBlockSumThreads);
     const uint32_t sh = UNAL ? (uint32_t)(off & 3u) : 0u;
+#ifdef RSG_DIAG_A16  // A/B-build diagnostic only: 16-byte aligned fetches (wrong sums)
+    const uint64_t loff = off & ~15ull;
+#else
     const uint64_t loff = off - sh;  // 4-byte aligned fetch start
+#endif
     const uint32_t nseg = n ? (n >> 6) / kChunks + 1 : 0;  // segments through the tail chunk
     const uint32_t S = rfl32((uint32_t)wave_max_u64(nseg));
     const uint64_t base = rfl64(wave_min_u64(n ? loff : ~0ull));
@@ -374,6 +378,10 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     }
     uint32_t R[Seg<512>::kSegBytes / 4 + 4];  // fixed bound, as voff
     const uint8_t *mine = slab + lane * kPiece;
+    // UNAL: volatile keeps one ds_read_b128 per unit (conflict-free at the
+    // 272-byte stride); left to itself the compiler split the funnel-shifted
+    // reads into ds_read2_b32, whose 32-bank groups conflict 4-way there
+    typedef uint32_t U32x4 __attribute__((ext_vector_type(4)));
 #define RSG_DMA_SEGMENT(S_)                                                                                      \
     do {                                                                                                         \
         const uint32_t so_ = kSegBytes * (S_);                                                                   \
@@ -385,8 +393,13 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     do {                                                                                                         \
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                                         \
         _Pragma("unroll") for (int q_ = 0; q_ < (int)(SEG / 16) + (UNAL ? 1 : 0); q_++) {                        \
-            const uint4 v_ = *reinterpret_cast<const uint4 *>(mine + 16 * q_);                                  \
-            R[4 * q_ + 0] = v_.x; R[4 * q_ + 1] = v_.y; R[4 * q_ + 2] = v_.z; R[4 * q_ + 3] = v_.w;              \
+            if constexpr (UNAL) {                                                                                \
+                const U32x4 v_ = *(const volatile __attribute__((address_space(3))) U32x4 *)(mine + 16 * q_);    \
+                R[4 * q_ + 0] = v_.x; R[4 * q_ + 1] = v_.y; R[4 * q_ + 2] = v_.z; R[4 * q_ + 3] = v_.w;          \
+            } else {                                                                                             \
+                const uint4 v_ = *reinterpret_cast<const uint4 *>(mine + 16 * q_);                              \
+                R[4 * q_ + 0] = v_.x; R[4 * q_ + 1] = v_.y; R[4 * q_ + 2] = v_.z; R[4 * q_ + 3] = v_.w;          \
+            }                                                                                                    \
         }                                                                                                        \
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                       \
     } while (0)

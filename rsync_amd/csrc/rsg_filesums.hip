@@ -169,42 +169,52 @@ __device__ __forceinline__ void fs_hash_lane(const uint8_t *__restrict__ arena, 
 // The ring kernel above gathers every 16-byte load from 64 different files
 // (64 cache lines per wave instruction): the CU's address path, not HBM,
 // bounds it (27 % of 8 TB/s on cfg4's files).  Here a wave's 64 files
-// stream through a private LDS slab, 256 bytes of every file per segment, by
+// stream through a private LDS slab, 128 bytes of every file per segment, by
 // LDS DMA: instruction i, lane l fills slab bytes [1024 i + 16 l, +16) =
-// unit u = (64 i + l) % 17 of file j = (64 i + l) / 17, i.e. four files'
-// 272-byte pieces per instruction (a piece starts at the file's first byte
-// rounded down to 4; the 17th unit feeds the funnel shift).
+// slot (64 i + l) % U of file j = (64 i + l) / U's piece of U units (U = 8
+// or 9 below; a piece starts at the file's first byte rounded down to 4).
 // global_load_lds takes a 64-bit address per lane, so a wave's files may lie
 // anywhere in an arena of any size (a buffer descriptor's 31-bit offsets
 // would confine them to 2 GiB).  Waves with a file whose needed bytes run
-// past the arena's end hash with the ring path above.  A unit a lane does not need
-// (its file is done) re-reads the unit's segment-0 bytes, which lie inside
-// the arena by that check.
+// past the arena's end hash with the ring path above.  A unit a lane does not
+// need (its file is done) re-reads the file's last segment, lines fetched a
+// segment earlier (segment 0, read back at the end, counted ~2 % of extra
+// traffic from the Infinity Cache, round 6).
 // Seeded mode: message word 0 is the seed, word w >= 1 is data word w - 1,
 // so message chunk c = (carry, data words 16 c .. 16 c + 14) with carry =
 // the data word before them -- the data stream is read from the file's own
 // start, never before it.
-// UNITS = 16: every file of the launch starts 4-byte aligned (the library's
-// own arenas pack files at 16 or 128 bytes), so a segment is exactly the
-// file's next 256 bytes -- no funnel shift and no 17th unit, which re-read
-// the first 16 bytes of the next segment (1.08x the file bytes from HBM
-// with 17 units, profiles/r05ba_filesums_summary.json).
-template <int UNITS>
+// ALN: every file of the launch starts 4-byte aligned (the library's own
+// arenas pack files at 16 or 128 bytes), so a segment is exactly the file's
+// next 256 bytes: no funnel shift, and the 17th unit of each piece -- kept
+// so the per-lane ds_read_b128 of a 272-byte stride stays conflict-free --
+// re-reads the segment's own last 16 bytes, a line just fetched, instead of
+// the next segment's first 16 bytes.
+// Measured alternatives (round 6, profiles/r06k_filesums_ab.txt, kernel ms
+// on cfg4's 100 000 files): 128-byte segments (8 waves per CU) 0.88,
+// three slabs in flight 0.82-0.86, 512-byte segments 1.07, 256-byte
+// segments with the 16 units rotated instead of padded (5 waves per CU)
+// 0.84, against 0.80 for this layout: neither occupancy nor prefetch depth
+// bounds it (the 64 files' interleaved 256-byte pieces do, as for the
+// block-sum kernels' staged order, §4.1 of DESIGN.md).
 struct FsShape {
-    static constexpr uint32_t kPiece = 16 * UNITS;  // LDS bytes per file
-    static constexpr uint32_t kSlab = 64 * kPiece;  // per wave
-    static constexpr uint32_t kDma = kSlab / 1024;  // DMA instructions per segment (= UNITS)
-    static_assert(kDma == UNITS, "one DMA instruction per unit of every file");
+    static constexpr uint32_t kChunks = 4;                  // MD4 chunks per segment
+    static constexpr uint32_t kSeg = 64 * kChunks;          // file bytes per segment
+    static constexpr uint32_t kUnits = 4 * kChunks + 1;     // 16-byte units per piece (272 bytes)
+    static constexpr uint32_t kPiece = 16 * kUnits;         // LDS bytes per file
+    static constexpr uint32_t kSlab = 64 * kPiece;          // LDS bytes per wave and segment
+    static constexpr uint32_t kDma = kUnits;                // DMA instructions per segment
 };
 
-template <bool SEEDED, int AUX, int UNITS>
+template <bool SEEDED, int AUX, bool ALN>
 __global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict__ arena, uint64_t arena_bytes,
                                                        const FileSpan *__restrict__ files,
                                                        const uint32_t *__restrict__ order, uint32_t nfiles,
                                                        uint32_t seed, uint8_t *__restrict__ out) {
-    constexpr uint32_t kFsUnits = UNITS, kFsPiece = FsShape<UNITS>::kPiece, kFsSlab = FsShape<UNITS>::kSlab,
-                       kFsDma = FsShape<UNITS>::kDma;
-    __shared__ __attribute__((aligned(16))) uint8_t slab[2 * kFsSlab];  // two segments in flight
+    using Sh = FsShape;
+    constexpr uint32_t CH = Sh::kChunks, SEG = Sh::kSeg, NU = Sh::kUnits, PIECE = Sh::kPiece, SLAB = Sh::kSlab,
+                       NDMA = Sh::kDma;
+    __shared__ __attribute__((aligned(16))) uint8_t slab[2 * SLAB];  // two segments in flight
     const uint32_t lane = threadIdx.x;
     const uint32_t lane_file = blockIdx.x * 64 + lane;
     const bool active = lane_file < nfiles;
@@ -213,12 +223,12 @@ __global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict
     const uint64_t pre = SEEDED ? 4u : 0u;
     const uint64_t L = F.len + pre;
     const uint64_t nfull = L >> 6;                 // the tail chunk's index
-    const uint64_t nseg64 = nfull / 4 + 1;         // segments through the tail chunk
-    const uint32_t sh = UNITS == 16 ? 0u : (uint32_t)(F.offset & 3u);
+    const uint64_t nseg64 = nfull / CH + 1;        // segments through the tail chunk
+    const uint32_t sh = ALN ? 0u : (uint32_t)(F.offset & 3u);
     const uint64_t fstart = F.offset - sh;         // data read from here (4-byte aligned)
-    // staged when every lane's needed bytes [fstart, fstart + 256 nseg (+ 16))
+    // staged when every lane's needed bytes [fstart, fstart + SEG nseg (+ 16))
     // lie inside the arena (segment counts kept to 32 bits)
-    const bool ok = nseg64 < (1ull << 31) && fstart + 256 * nseg64 + (UNITS == 16 ? 0 : 16) <= arena_bytes;
+    const bool ok = nseg64 < (1ull << 31) && fstart + SEG * nseg64 + (ALN ? 0 : 16) <= arena_bytes;
     if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
         if (!active) return;
         uint32_t h[4];
@@ -232,67 +242,66 @@ __global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, m, 64));
     const uint32_t S = rfl32(smax);
-    // per DMA instruction i: this lane's unit (file j, unit u), its address
-    // at segment 0 and the segments it is needed for
-    const uint8_t *ua[kFsDma];
-    uint32_t un[kFsDma];
+    // per DMA instruction i: this lane's unit (file j, unit u; ALN: the pad
+    // re-reads unit 15), its address at segment 0 and the file's segments
+    const uint8_t *ua[NDMA];
+    uint32_t un[NDMA];
 #pragma unroll
-    for (uint32_t i = 0; i < kFsDma; i++) {
-        const uint32_t idx = 64u * i + lane, j = idx / kFsUnits, u = idx - kFsUnits * j;
+    for (uint32_t i = 0; i < NDMA; i++) {
+        const uint32_t idx = 64u * i + lane, j = idx / NU, t = idx - NU * j;
+        const uint32_t u = ALN && t == NU - 1 ? t - 1 : t;
         const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)fstart, (int)j, 64);
         const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(fstart >> 32), (int)j, 64);
         ua[i] = arena + (((uint64_t)hi << 32) | lo) + 16u * u;
-        un[i] = (uint32_t)__shfl((int)nseg, (int)j, 64);
+        un[i] = max((uint32_t)__shfl((int)nseg, (int)j, 64), 1u) - 1u;  // the file's last segment
     }
 #define RSG_FS_DMA(S_, SL_)                                                                                    \
     do {                                                                                                       \
-        uint8_t *d_ = slab + (SL_) * kFsSlab;                                                                  \
-        _Pragma("unroll") for (uint32_t i_ = 0; i_ < kFsDma; i_++) {                                           \
-            const uint8_t *a_ = ua[i_] + ((S_) < un[i_] ? 256ull * (S_) : 0ull);                              \
+        uint8_t *d_ = slab + (SL_) * SLAB;                                                                     \
+        _Pragma("unroll") for (uint32_t i_ = 0; i_ < NDMA; i_++) {                                             \
+            const uint8_t *a_ = ua[i_] + (uint64_t)SEG * min((uint32_t)(S_), un[i_]);                         \
             __builtin_amdgcn_global_load_lds((const void *)a_, (__attribute__((address_space(3))) void *)(d_ + 1024u * i_), \
                                              16, 0, AUX);                                                      \
         }                                                                                                      \
     } while (0)
-    uint32_t R[4 * kFsUnits];
+    uint32_t R[4 * NU];
+    // volatile: one ds_read_b128 per unit; left to itself the compiler split
+    // the reads into ds_read2_b32, whose 32-bank groups conflict
+    typedef uint32_t FsVec __attribute__((ext_vector_type(4)));
 #define RSG_FS_READ(SL_)                                                                                       \
     do {                                                                                                       \
-        const uint8_t *mine = slab + (SL_) * kFsSlab + lane * kFsPiece;                                         \
-        _Pragma("unroll") for (int q_ = 0; q_ < (int)kFsUnits; q_++) {                                         \
-            const uint4 v_ = *reinterpret_cast<const uint4 *>(mine + 16 * q_);                                 \
+        const uint8_t *b_ = slab + (SL_) * SLAB + lane * PIECE;                                                \
+        _Pragma("unroll") for (uint32_t q_ = 0; q_ < (ALN ? 4 * CH : NU); q_++) {                              \
+            const FsVec v_ = *(const volatile __attribute__((address_space(3))) FsVec *)(b_ + 16 * q_);        \
             R[4 * q_ + 0] = v_.x; R[4 * q_ + 1] = v_.y; R[4 * q_ + 2] = v_.z; R[4 * q_ + 3] = v_.w;             \
         }                                                                                                      \
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                     \
     } while (0)
     // Two segments in flight per wave: segment s + 2 is issued into the slab
-    // segment s was just copied out of (one in flight left only ~1.2 us of
-    // hashing to cover each segment's HBM latency)
+    // segment s was just copied out of
     RSG_FS_DMA(0u, 0u);
     if (S > 1) RSG_FS_DMA(1u, 1u);
     uint32_t h[4];
     md4_init(h);
     uint32_t carry = seed;  // seeded: the message word before the chunk's data words
     uint32_t X[16];
-    const uint32_t tail_seg = (uint32_t)(nfull / 4), tail_i = (uint32_t)(nfull % 4);
+    const uint32_t tail_seg = (uint32_t)(nfull / CH), tail_i = (uint32_t)(nfull % CH);
 #pragma unroll 1
     for (uint32_t s = 0; s < S; s++) {
-        // segment s has landed once at most the younger segment's UNITS DMAs are pending
-        if (s + 1 < S) {
-            if constexpr (UNITS == 17) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        // segment s has landed once at most the younger segment's NDMA DMAs are pending
+        if (s + 1 < S) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         RSG_FS_READ(s & 1u);
         if (s + 2 < S) RSG_FS_DMA(s + 2, s & 1u);  // in flight while segments s and s + 1 hash
         if (s <= tail_seg && s < nseg) {
 #pragma unroll
-            for (uint32_t i = 0; i < 4; i++) {
+            for (uint32_t i = 0; i < CH; i++) {
                 if (s == tail_seg && i > tail_i) break;
                 uint32_t D[16];
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
-                    if constexpr (UNITS == 17) D[k] = __builtin_amdgcn_alignbyte(R[16 * i + k + 1], R[16 * i + k], sh);
-                    else D[k] = R[16 * i + k];
+                    if constexpr (ALN) D[k] = R[16 * i + k];
+                    else D[k] = __builtin_amdgcn_alignbyte(R[16 * i + k + 1], R[16 * i + k], sh);
                 }
                 if (SEEDED) {
                     X[0] = carry;
@@ -325,8 +334,8 @@ hipError_t launch_file_sums(const uint8_t *arena, uint64_t arena_bytes, const Fi
     // files); the default cache policy (nt DMA re-read neighbouring units,
     // 1.47x the file bytes, profiles/r03d_filesums_summary.json)
     const dim3 grid((nfiles + 63) / 64), block(64);
-    auto kern = mode == 1 ? (aligned4 ? file_sums_staged<true, 0, 16> : file_sums_staged<true, 0, 17>)
-                          : (aligned4 ? file_sums_staged<false, 0, 16> : file_sums_staged<false, 0, 17>);
+    auto kern = mode == 1 ? (aligned4 ? file_sums_staged<true, 0, true> : file_sums_staged<true, 0, false>)
+                          : (aligned4 ? file_sums_staged<false, 0, true> : file_sums_staged<false, 0, false>);
     hipLaunchKernelGGL(kern, grid, block, 0, stream, arena, arena_bytes, files, order, nfiles, seed, out);
     return hipGetLastError();
 }

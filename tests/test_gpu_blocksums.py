@@ -392,3 +392,38 @@ def test_automatic_rule_library_packed(eng, blen):
     files = [cases.splitmix64_bytes(7000 + i, n) for i, n in enumerate(lens)]
     _, rec, _ = eng.block_sums(files, cases.SEED, blen)
     assert rec == b"".join(orc.block_sums(f, blen, cases.SEED) for f in files)
+
+
+SQRT_LENS_MIB = [1, 2, 3, 5, 9, 17, 33, 64]
+
+
+def test_reference_sizing_sqrt_lengths(eng):
+    """The reference's own block length B = isqrt(len) (rsynccommon.go:22) for
+    files of 1, 2, 3, 5, 9, 17, 33 and 64 MiB -- B = 1024, 1448, 1773, 2289,
+    3072, 4222, 5882, 8192, most not a multiple of 128 or even of 4 -- on the
+    device arena the sweep measures (tools/blocklen_sweep.py SWEEP_SQRT=1:
+    files packed at 128-byte offsets, two per length, the second one byte
+    short) through the automatic rule, and through the host path with the
+    default sizing (block_len 0); every record equal to the oracle's."""
+    import math
+    lens = [x for m in SQRT_LENS_MIB for x in ((m << 20), (m << 20) - 1)]
+    blens = [math.isqrt(m << 20) for m in SQRT_LENS_MIB for _ in range(2)]
+    offs, o = [], 0
+    for n in lens:
+        offs.append(o)
+        o += (n + 127) & ~127
+    host = np.zeros(o, np.uint8)
+    datas = []
+    for i, (off, n) in enumerate(zip(offs, lens)):
+        d = cases.splitmix64_bytes(9100 + i, n)
+        host[off:off + n] = d
+        datas.append(d)
+    want = b"".join(orc.block_sums(d, b, cases.SEED) for d, b in zip(datas, blens))
+    arena = eng.alloc(o)
+    arena.upload(host)
+    recs, total = eng.block_sums_device(arena, [(a, n, b) for a, n, b in zip(offs, lens, blens)], cases.SEED)
+    assert recs.download(total * 20).tobytes() == want
+    # host path, reference sizing chosen by the library (block_len 0 -> isqrt for len > 490000)
+    heads, rec, _ = eng.block_sums(datas[::2], cases.SEED, 0)
+    assert [h.block_len for h in heads] == blens[::2]
+    assert rec == b"".join(orc.block_sums(d, b, cases.SEED) for d, b in zip(datas[::2], blens[::2]))

@@ -35,7 +35,7 @@ SHAPES = [  # (files, file bytes, block length, arenas)
 ]
 VARIANTS = {-1: "automatic", 1: "staged", 4: "staged_seg128", 14: "pipe_seg512", 2: "park",
             3: "long_deep_prefetch"}
-# SWEEP_SQRT=1: the reference's own block length B = int(sqrt(len)) (rsynccommon.go:22) for files of
+# SWEEP_SQRT=1 (or a list of MiB, "2,3"): the reference's own block length B = int(sqrt(len)) (rsynccommon.go:22) for files of
 # len = 1, 2, 3, 5, 9, 17, 33, 64 MiB, ~1 GiB of them per shape, at the library's 128-byte packing
 SQRT_LENS_MIB = [1, 2, 3, 5, 9, 17, 33, 64]
 
@@ -57,7 +57,8 @@ def main():
         shapes = [(256, 4 << 20, int(b), 2) for b in os.environ["SWEEP_BLENS"].split(",")]
     if os.environ.get("SWEEP_SQRT"):
         import math
-        shapes = [(max(1, (1 << 30) // (m << 20)), m << 20, int(math.isqrt(m << 20)), 2) for m in SQRT_LENS_MIB]
+        mibs = SQRT_LENS_MIB if os.environ["SWEEP_SQRT"] == "1" else [int(x) for x in os.environ["SWEEP_SQRT"].split(",")]
+        shapes = [(max(1, (1 << 30) // (m << 20)), m << 20, int(math.isqrt(m << 20)), 2) for m in mibs]
     rounds = int(os.environ.get("SWEEP_ROUNDS", "1"))
     only = os.environ.get("SWEEP_ONLY")  # comma-separated variant names
     for nf, fb, blen, narena in shapes:
