@@ -313,10 +313,17 @@ template <uint32_t SEG, bool UNAL>
 __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
-    // nt policy on the DMA: every byte is read once (A/B against the default
-    // policy, profiles/r02f_blocklen_sweep_nt.jsonl: B = 4096 0.239 -> 0.219 ms,
-    // cfg5 6.48 -> 6.25 ms, B = 1024 and the sender's confirmation unchanged)
-    constexpr int DMA_AUX = 2;
+    // Aligned: nt policy on the DMA, every byte is read once (A/B against the
+    // default policy, profiles/r02f_blocklen_sweep_nt.jsonl: B = 4096 0.239 ->
+    // 0.219 ms, cfg5 6.48 -> 6.25 ms).  UNAL: the default policy.  A piece
+    // starting mid-line shares its first and last 128-byte lines with the
+    // block's previous and next segments, requested one segment apart; nt
+    // lines were gone by then (FETCH 1.51x the block bytes at B = 1773,
+    // 1.31x with the default policy) -- round 6,
+    // profiles/r06o_blocklen_policy_ab.txt: B = 1773 / 2289 / 4222 / 5882
+    // 0.262 / 0.260 / 0.257 / 0.253 -> 0.222 / 0.227 / 0.234 / 0.235 ms per
+    // GiB, cfg3's confirmation windows 1112 -> 1161 GiB/s.
+    constexpr int DMA_AUX = UNAL ? 0 : 2;
     constexpr uint32_t kSegBytes = Seg<SEG>::kSegBytes, kUnits = Seg<SEG>::kUnits, kPiece = Seg<SEG>::kPiece;
     constexpr uint32_t kWaveSlab = Seg<SEG>::kWaveSlab, kDmaPerSeg = Seg<SEG>::kDmaPerSeg;
     constexpr uint32_t kChunks = Seg<SEG>::kChunks;
@@ -333,11 +340,7 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     uint32_t n = 0;
     if (g < total_blocks) locate_block(files, wg_file, g, off, n, wave_first / kBlockSumThreads);
     const uint32_t sh = UNAL ? (uint32_t)(off & 3u) : 0u;
-#ifdef RSG_DIAG_A16  // A/B-build diagnostic only: 16-byte aligned fetches (wrong sums)
-    const uint64_t loff = off & ~15ull;
-#else
     const uint64_t loff = off - sh;  // 4-byte aligned fetch start
-#endif
     const uint32_t nseg = n ? (n >> 6) / kChunks + 1 : 0;  // segments through the tail chunk
     const uint32_t S = rfl32((uint32_t)wave_max_u64(nseg));
     const uint64_t base = rfl64(wave_min_u64(n ? loff : ~0ull));
@@ -445,6 +448,7 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
 // the automatic choice for 704..24576-byte blocks not on 128-byte lines (see
 // launch_block_sums).  The 128- and 256-byte forms (variants 13 / 15) and
 // the memory-only diagnostic live in the round-5 history (tools/build_ab.sh).
+template <int DMA_AUX>
 __global__ __launch_bounds__(kBlockSumThreads) void block_sums_pipe(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
@@ -452,7 +456,7 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_pipe(
     constexpr uint32_t kUnits = Seg<SEG>::kUnits, kPiece = Seg<SEG>::kPiece;
     constexpr uint32_t kWaveSlab = Seg<SEG>::kWaveSlab, kDmaPerSeg = Seg<SEG>::kDmaPerSeg;
     constexpr uint32_t kChunks = Seg<SEG>::kChunks;
-    constexpr int DMA_AUX = 2;
+
     __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * kWaveSlab];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1051,8 +1055,19 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                                    arena_bytes, files, wg_file, total_blocks, seed, out);
             break;
         case 14:
-            hipLaunchKernelGGL(block_sums_pipe, pipe_grid(nwg), block, 0, stream, arena, arena_bytes, files, wg_file,
-                               total_blocks, seed, out);
+            // cache policy: the default one up to 4 KiB blocks (a 512-byte piece
+            // off the 128-byte lines shares a line with the block's next
+            // segment, kept in L2 only without nt: B = 1000 / 1448 / 2000 / 3504
+            // 0.238 / 0.239 / 0.230 / 0.216 -> 0.230 / 0.228 / 0.224 / 0.212 ms
+            // per GiB), nt above (6000 / 8000 / 12000 / 20000: 0.211 / 0.245 /
+            // 0.254 / 0.227 against 0.217 / 0.263 / 0.270 / 0.253 without);
+            // profiles/r06o_blocklen_policy_ab.txt
+            if (max_blen <= 4096)
+                hipLaunchKernelGGL(block_sums_pipe<0>, pipe_grid(nwg), block, 0, stream, arena, arena_bytes, files,
+                                   wg_file, total_blocks, seed, out);
+            else
+                hipLaunchKernelGGL(block_sums_pipe<2>, pipe_grid(nwg), block, 0, stream, arena, arena_bytes, files,
+                                   wg_file, total_blocks, seed, out);
             break;
         case 3: {
             const uint64_t waves = (total_blocks + 63) / 64;
