@@ -70,6 +70,8 @@ def parse():
                     choices=["cfg2", "cfg3", "cfg4", "cfg4-sender", "cfg5", "filesums", "receive"],
                     help="cfg2 = receiver block sums (the metric); cfg3 = sender match, reported separately")
     ap.add_argument("--cfg3-files", type=int, default=10)
+    ap.add_argument("--search-option", action="append", default=[], metavar="NAME=VALUE",
+                    help="cfg3 A/B only: a per-context sender option (engine.SEARCH_OPTIONS, e.g. confirm_cus=24)")
     ap.add_argument("--batches", type=int, default=None,
                     help="batches per rank for the pipelined delivery modes (records of batch b move while "
                          "batch b+1 is hashed); default 4, or 1 at N = 1, where the root's records are "
@@ -580,6 +582,9 @@ def bench_sender(args, rank, world, local):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import cases
     eng = rsync_amd.Engine(local)
+    for opt in args.search_option:
+        name, value = opt.split("=")
+        eng.set_option(name, int(value))
     size = 1 << 30
     rng = np.random.default_rng(3 + rank)
     basis = eng.alloc(size)
@@ -673,6 +678,7 @@ def bench_sender(args, rank, world, local):
                           "data": "synthetic (splitmix64 bases; sources 50% overwritten + shifts)",
                           "config": {"workload": "cfg3: 10 x 1 GiB sources vs 50%-modified bases, B=32768",
                                      "files": args.cfg3_files, "matches_per_pass": nm // steps,
+                                     **({"search_options": args.search_option} if args.search_option else {}),
                                      "call": "rsg_hash_search_batch_device, one call per pass"},
                           "ms_per_file": round(dt * 1e3 / (steps * len(metas)), 3), "call_ms": call_ms,
                           "single_file_calls_gib_s": single_gib_s,

@@ -270,6 +270,11 @@ rsg_status rsg_hash_search_fd(rsg_ctx *ctx, int32_t fd, int64_t offset, uint64_t
  * reading its file's bytes itself), so several files' serial MD4 chains
  * proceed side by side instead of one after the other.  file_sum = NULL
  * skips a job's sum; head.count == 0 (sendFile) reads the file only for it.
+ * Unlike the reference (match.go:52-53,268) and rsg_hash_search_fd, the sum
+ * is computed from a second read of the file, not from the searched bytes: a
+ * file rewritten in place at the same length mid-transfer can give a sum
+ * that does not match the sent data (the receiver's check then fails; see
+ * DESIGN.md 4.2.1).
  * Every job's n_matches and status are set: RSG_OK, RSG_ERR_INVALID (its own
  * arguments), RSG_ERR_TRUNCATED (beyond match_cap; n_matches is the full
  * count), RSG_ERR_IO (short file / read error).  A HIP or allocation failure

@@ -1399,7 +1399,10 @@ rsg_status search_fd(rsg_ctx *ctx, int32_t fd, int64_t off0, uint64_t size, cons
 
 // MD4(int32_LE(seed) || bytes [off, off + n) of fd) (match.go:52-53), the
 // bytes read with pread in 1 MiB pieces (hashed while cache-hot).  0, an
-// errno, or -1 for EOF before n bytes.
+// errno, or -1 for EOF before n bytes.  A second read of the file, apart from
+// the search's (the reference hashes the bytes it matches and sends): a file
+// rewritten in place mid-transfer can give a sum of other contents
+// (documented in rsg.h / DESIGN.md 4.2.1).
 int file_sum_fd(int fd, int64_t off, uint64_t n, int32_t seed, uint8_t out[16], std::vector<uint8_t> &buf) {
     constexpr uint64_t kPiece = 1ull << 20;
     buf.resize(kPiece);
