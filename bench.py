@@ -182,7 +182,7 @@ def main():
     if args.ab:
         from rsync_amd import _lib
         # the shipped block-sum variants on the same plan (identical records)
-        names = {2: "park", 1: "staged_seg256", 4: "staged_seg128", 14: "pipe_seg512", 0: "direct"}
+        names = {2: "park", 1: "staged_seg256", 4: "staged_seg128", 7: "lines", 0: "direct"}
         only = os.environ.get("AB_ONLY")  # comma-separated substrings: A/B only the matching entries
         if only:
             names = {v: n for v, n in names.items() if any(o in n for o in only.split(","))}

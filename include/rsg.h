@@ -34,10 +34,11 @@
 extern "C" {
 #endif
 
-#define RSG_ABI_VERSION 4  /* 2: per-context block-sum kernel knob, multi-GPU calls, rsg_hash_search_fd;
+#define RSG_ABI_VERSION 5  /* 2: per-context block-sum kernel knob, multi-GPU calls, rsg_hash_search_fd;
                               3: rsg_hash_search_fd_batch;
                               4: block-sum variants pruned to the shipped set (-1, 0, 1, 2, 3, 4, 6, 14),
-                                 small sources searched by the one-wave-per-file kernel */
+                                 small sources searched by the one-wave-per-file kernel;
+                              5: variant 7 (line windows) replaces 14 */
 /* One wire record: int32 LE sum1 then sum2[16] (generator.go:341-346). */
 #define RSG_RECORD_BYTES 20
 #define RSG_SUM2_BYTES 16
@@ -153,17 +154,18 @@ rsg_status rsg_block_sums_planned(rsg_ctx *ctx, const rsg_plan *plan, const void
  * 4 = staged with 128-byte segments, 6 = staged for blocks at any byte
  * offset (pieces fetched from the 4-byte aligned address below the block,
  * funnel-shifted in registers; needs a 4-byte aligned arena, else 3 / 0),
- * 14 = persistent staged with 512-byte segments, each wave requesting its
- * next group's first segment before hashing the current group's last one.
- * Automatic, in two lines: unaligned blocks -> 6; aligned: 512..703 bytes ->
- * park (2); on 128-byte lines up to 32 KiB -> 4 (the library's own packing
- * keeps file offsets on 128-byte lines, so B a multiple of 128 qualifies);
- * up to 24 KiB when 512-byte segments read at most 1.2 B per block -> 14;
- * otherwise 1.  The LDS-DMA variants fall back to 0 for blocks that are not
- * 4-byte aligned.  The environment variable RSG_BLOCKSUMS_KERNEL sets a new
- * context's initial value.  Returns RSG_ERR_INVALID for any other value
- * (the variants numbered 5, 7..13 and 15 in ABI 3 were measured slower and
- * removed; tools/build_ab.sh rebuilds them from the history). */
+ * 7 = line windows: each block's bytes fetched as the 128-byte lines that
+ * hold them, each line once, for blocks at any offset (needs a 128-byte
+ * aligned arena, else 6 for unaligned blocks and 1 for aligned ones).
+ * Automatic, in two lines: unaligned blocks, or blocks of >= 704 bytes off
+ * the 128-byte lines -> 7; 512..703 bytes -> park (2); on the 128-byte lines
+ * up to 32 KiB -> 4 (the library's own packing keeps file offsets on the
+ * lines, so B a multiple of 128 qualifies); otherwise 1.  The LDS-DMA
+ * variants fall back to 0 for blocks that are not 4-byte aligned.  The
+ * environment variable RSG_BLOCKSUMS_KERNEL sets a new context's initial
+ * value.  Returns RSG_ERR_INVALID for any other value (the variants
+ * numbered 5, 8..15 in ABI 3 and 4 were measured slower and removed;
+ * tools/build_ab.sh rebuilds them from the history). */
 rsg_status rsg_set_block_sums_kernel(rsg_ctx *ctx, int32_t variant);
 
 /* Fallback census of ctx's device since the last reset: counts[0] = full

@@ -27,9 +27,10 @@ rsg_status rsg_testing_walk(const uint64_t *cand, uint64_t n, const int32_t *tru
 /* The block-sum kernel variant a launch takes (host arithmetic, the rule
  * rsg_set_block_sums_kernel documents): variant (-1 = automatic) for a batch
  * whose blocks are all 4-byte aligned (aligned), all on 128-byte lines
- * (lines128), in a 4-byte aligned arena (arena_aligned4), longest block
- * max_blen.  -2 for a variant rsg_set_block_sums_kernel rejects. */
-int32_t rsg_testing_block_sums_choice(int32_t variant, int32_t aligned, int32_t lines128, int32_t arena_aligned4,
+ * (lines128), in an arena whose base is aligned to arena_align (0: less than
+ * 4 bytes, 1: 4 bytes, 2: 128 bytes), longest block max_blen.  -2 for a
+ * variant rsg_set_block_sums_kernel rejects. */
+int32_t rsg_testing_block_sums_choice(int32_t variant, int32_t aligned, int32_t lines128, int32_t arena_align,
                                       uint32_t max_blen);
 
 /* The product's host MD4 (RFC 1320; rsync_amd/csrc/rsg_md4_host.cpp), used

@@ -24,7 +24,7 @@ RECORD_BYTES = 20
 FILESUM_PLAIN = 0   # MD4(file), rsyncchecksum.go:60-66
 FILESUM_SEEDED = 1  # MD4(int32_LE(seed) || file), match.go:52-53
 CHUNK_SIZE = 256 * 1024
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 OK = 0
 ERR_INVALID = -1

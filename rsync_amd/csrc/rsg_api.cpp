@@ -469,10 +469,11 @@ rsg_status rsg_set_block_sums_kernel(rsg_ctx *ctx, int32_t variant) {
     return RSG_OK;
 }
 
-int32_t rsg_testing_block_sums_choice(int32_t variant, int32_t aligned, int32_t lines128, int32_t arena_aligned4,
+int32_t rsg_testing_block_sums_choice(int32_t variant, int32_t aligned, int32_t lines128, int32_t arena_align,
                                       uint32_t max_blen) {
     if (!rsg::block_sums_variant_valid(variant)) return -2;
-    return rsg::block_sums_choice(variant, aligned != 0, lines128 != 0, arena_aligned4 != 0, max_blen);
+    return rsg::block_sums_choice(variant, aligned != 0, lines128 != 0, arena_align < 0 ? 0 : arena_align > 2 ? 2 : arena_align,
+                                  max_blen);
 }
 
 rsg_status rsg_block_sums_fallbacks(rsg_ctx *ctx, uint64_t counts[2], int32_t reset) {

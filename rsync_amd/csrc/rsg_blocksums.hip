@@ -433,158 +433,123 @@ __global__ __launch_bounds__(kBlockSumThreads) void block_sums_staged(
     store_tile_records(out, wave_first / 64, lane, reinterpret_cast<uint32_t *>(slab), n, s1, t, h);
 }
 
-// Variant 14 (round 5): the persistent staged kernel with each wave's group
-// boundary hidden, 512-byte segments.  Diagnostics showed the staged
-// pattern's cost is its temporal order, not the piece length alone, and that
-// a persistent wave pays a full memory round trip plus the block lookup at
-// every group start with nothing of its own in flight.  Here the next group
-// is located (uniform loads) while the current group's last segment is in
-// flight, its segment 0 is requested as soon as the slab is free (before the
-// current group's last segment is hashed), and the current group's records
-// leave after the next group's first segment has landed.  Measured
-// (profiles/r05am, r05ao sweeps, ms per GiB): memory only 0.179 against the
-// staged kernel's 0.200 at B = 1024 (0.180 / 0.186 at 2048, 0.218 / 0.219 at
-// 4096).  With 512-byte segments (one wave per SIMD, LDS-bound anyway) it is
-// the automatic choice for 704..24576-byte blocks not on 128-byte lines (see
-// launch_block_sums).  The 128- and 256-byte forms (variants 13 / 15) and
-// the memory-only diagnostic live in the round-5 history (tools/build_ab.sh).
-template <int DMA_AUX>
-__global__ __launch_bounds__(kBlockSumThreads) void block_sums_pipe(
+// Variant 7 (round 6): line windows.  The staged kernels fetch each block's
+// segments from the block's own start, so a block that does not start on a
+// 128-byte line reads, every segment, a line it read (partly) the segment
+// before: 3 lines per 256-byte segment, 1.3-1.5x the block bytes in FETCH_SIZE
+// (B = 1773, profiles/r06o_blocklen_policy_ab.txt).  Here lane j's windows are
+// the 128-byte lines from the one holding its first byte: window w =
+// [A_j + 128 w, +128), A_j = that line, delta_j = off_j - A_j < 128.  Step s
+// hashes chunks 2s and 2s+1, whose 33 words (32 + the funnel word) start at
+// word delta_j / 4 of window s and end in window s+1, so windows s and s+1
+// sit in the wave's two slabs (144-byte pieces: 8 data units + a pad unit the
+// buffer range check drops) and window s+2 is requested into window s's slab
+// once its words are in registers.  The words are read with one ds_read_b32
+// each from a per-lane base chosen per word (window s or s+1: a compare and a
+// select, ~15 % more VALU than the staged kernel's 17 ds_read_b128 per four
+// chunks).  ALN: every block 4-byte aligned (no funnel shift).  The arena
+// must start on a 128-byte line (launch_block_sums checks).
+// DMA_AUX: nt (2): every line is fetched once per block now; nt measured
+// 3-9 % faster than the default policy (B = 1448 / 1773 / 4222 / 5882: 0.208 /
+// 0.200 / 0.181 / 0.188 against 0.209 / 0.204 / 0.195 / 0.206 ms per GiB,
+// profiles/r06v_lines_policy_ab.txt)
+// PU: 16-byte units per piece (8 data + 1 or 2 dropped pads).  Lane j's word
+// k sits in bank (PU*4*j + delta_j/4 + k) mod 32, and consecutive blocks of
+// one file have delta_j = (j B + c) mod 128: with PU = 9, B = 6000 put all 32
+// lanes on one bank (0.50 ms per GiB against 0.21); the launcher picks the PU
+// whose 4 PU + B/4 has the fewest factors of 2 mod 32.
+template <bool ALN, int DMA_AUX, uint32_t PU>
+__global__ __launch_bounds__(kBlockSumThreads) void block_sums_lines(
     const uint8_t *__restrict__ arena, uint64_t arena_bytes, const DevFile *__restrict__ files,
     const uint32_t *__restrict__ wg_file, uint64_t total_blocks, uint32_t seed, uint8_t *__restrict__ out) {
-    constexpr uint32_t SEG = 512;
-    constexpr uint32_t kUnits = Seg<SEG>::kUnits, kPiece = Seg<SEG>::kPiece;
-    constexpr uint32_t kWaveSlab = Seg<SEG>::kWaveSlab, kDmaPerSeg = Seg<SEG>::kDmaPerSeg;
-    constexpr uint32_t kChunks = Seg<SEG>::kChunks;
-
-    __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * kWaveSlab];
+    constexpr uint32_t kWin = 128, kUnits = PU, kPiece = 16 * kUnits, kSlab = 64 * kPiece, kDma = kSlab / 1024;
+    static_assert(PU == 9 || PU == 10, "nine or ten units per piece");
+    __shared__ __attribute__((aligned(16))) uint8_t slab_all[(kBlockSumThreads / 64) * 2 * kSlab];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint8_t *slab = slab_all + wave * kWaveSlab;
-    const uint8_t *mine = slab + lane * kPiece;
-    const uint64_t groups = (total_blocks + 63) / 64, stride = (uint64_t)gridDim.x * (kBlockSumThreads / 64);
-    uint64_t gw = (uint64_t)blockIdx.x * (kBlockSumThreads / 64) + wave;
-    if (gw >= groups) return;
-    uint32_t voff[Seg<512>::kDmaPerSeg];  // fixed bound (see block_sums_staged)
-    __amdgpu_buffer_rsrc_t rsrc;
-    // the lane offsets and buffer of group d's DMA (valid until the next call)
-    auto point = [&](const GroupDesc &d) {
-        rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(arena + d.base), (short)0, 0x7FFFFFFF, 0x00020000);
-        const uint32_t rel = (uint32_t)(d.off - d.base);
-#pragma unroll
-        for (uint32_t i = 0; i < kDmaPerSeg; i++) {
-            const uint32_t idx = 64u * i + lane;
-            const uint32_t j = idx / kUnits, u = idx - kUnits * j;
-            const uint32_t v = (uint32_t)__shfl((int)rel, (int)j, 64) + 16u * u;
-            voff[i] = u + 1 < kUnits ? v : 0x80000000u;
-        }
-    };
-    auto dma = [&](uint32_t s) {
-#pragma unroll
-        for (uint32_t i = 0; i < kDmaPerSeg; i++)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(slab + 1024u * i),
-                                                     16, voff[i], SEG * s, 0, DMA_AUX);
-    };
-    uint32_t R[Seg<512>::kSegBytes / 4 + 4];
-    auto read_segment = [&]() {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int q = 0; q < (int)(SEG / 16); q++) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(mine + 16 * q);
-            R[4 * q + 0] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    };
-    GroupDesc cur, nxt;
-    locate_group<SEG>(arena, arena_bytes, files, wg_file, total_blocks, gw * 64, lane, cur);
-    if (cur.staged) {
-        point(cur);
-        dma(0);
-    }
-    // the previous group's records, stored once the next group's first
-    // segment has landed (the slab is free then)
-    bool pend = false;
-    uint64_t pend_tile = 0;
-    uint32_t pn = 0, ph[4] = {0, 0, 0, 0}, pt = 0;
-    int32_t ps1 = 0;
-#pragma unroll 1
-    for (;;) {
-        const uint64_t nw = gw + stride;
-        const bool has_next = nw < groups;
+    uint8_t *slab = slab_all + wave * 2 * kSlab;
+    const uint64_t wave_first = (uint64_t)blockIdx.x * kBlockSumThreads + wave * 64u;
+    const uint64_t g = wave_first + lane;
+    uint64_t off = 0;
+    uint32_t n = 0;
+    if (g < total_blocks) locate_block(files, wg_file, g, off, n, wave_first / kBlockSumThreads);
+    const uint32_t sh = ALN ? 0u : (uint32_t)(off & 3u);
+    const uint32_t delta = (uint32_t)(off & (kWin - 1));
+    const uint64_t aoff = off - delta;                      // line-aligned fetch start
+    const uint32_t nfull = n >> 6;
+    const uint32_t steps = n ? nfull / 2 + 1 : 0;           // step s: chunks 2s, 2s+1 (through the tail chunk)
+    const uint32_t S = rfl32((uint32_t)wave_max_u64(steps));
+    const uint64_t base = rfl64(wave_min_u64(n ? aoff : ~0ull));
+    // windows 0..S of every lane (the last one only for the funnel word)
+    const uint64_t top = rfl64(wave_max_u64(n ? aoff + (uint64_t)kWin * (S + 1) : 0));
+    const bool full = wave_first + 63 < total_blocks;
+    const bool staged = full && top <= arena_bytes && (top - base) <= 0x7FFFFFFFull;
+    if (!staged) {
+        if (full && lane == 0) count_fallback(0);
+        if (n == 0) return;
         uint32_t h[4];
         md4_init(h);
         int32_t s1 = 0;
         uint32_t t = 0;
-        const uint32_t n = cur.n, nfull = n >> 6;
-        bool next_located = false;
-        if (!cur.staged) {
-            if (pend) {
-                store_record(out, pend_tile * 64 + lane, pn, ps1, pt, ph);
-                pend = false;
-            }
-            if (n) {
-                hash_block_direct<true>(arena, (uintptr_t)(arena + arena_bytes), cur.off, n, seed, h, s1, t);
-                store_record(out, gw * 64 + lane, n, s1, t, h);
-            }
-            if (!has_next) break;
-            gw = nw;
-            locate_group<SEG>(arena, arena_bytes, files, wg_file, total_blocks, gw * 64, lane, cur);
-            if (cur.staged) {
-                point(cur);
-                dma(0);
-            }
-            continue;
-        }
-        read_segment();
-        if (pend) {
-            store_tile_records(out, pend_tile, lane, reinterpret_cast<uint32_t *>(slab), pn, ps1, pt, ph);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads done before the slab is refilled
-            pend = false;
-        }
-        const uint32_t S = cur.S;
-        if (S == 1 && has_next) {
-            locate_group<SEG>(arena, arena_bytes, files, wg_file, total_blocks, nw * 64, lane, nxt);
-            next_located = true;
-        }
+        hash_block_direct<ALN>(arena, (uintptr_t)(arena + arena_bytes), off, n, seed, h, s1, t);
+        store_record(out, g, n, s1, t, h);
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(arena + base), (short)0, 0x7FFFFFFF, 0x00020000);
+    const uint32_t rel = (uint32_t)(aoff - base);
+    // DMA instruction i, lane t: piece j = (64 i + t) / 9 (lane j's window),
+    // unit u = (64 i + t) % 9; u == 8 is the dropped pad
+    uint32_t voff[10];  // fixed bound (a template-dependent one drops the host launch stub, as in staged)
+#pragma unroll
+    for (uint32_t i = 0; i < kDma; i++) {
+        const uint32_t idx = 64u * i + lane;
+        const uint32_t j = idx / kUnits, u = idx - kUnits * j;
+        const uint32_t v = (uint32_t)__shfl((int)rel, (int)j, 64) + 16u * u;
+        voff[i] = u < 8 ? v : 0x80000000u;
+    }
+#define RSG_DMA_WINDOW(W_)                                                                                       \
+    do {                                                                                                         \
+        uint8_t *d_ = slab + ((W_) & 1u) * kSlab;                                                                \
+        _Pragma("unroll") for (uint32_t i_ = 0; i_ < kDma; i_++)                                                 \
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(d_ + 1024u * i_), \
+                                                     16, voff[i_], kWin * (W_), 0, DMA_AUX);                     \
+    } while (0)
+    // word k of step s: word dw + k of window s, or of window s+1 past its 32 words
+    const uint32_t dw = delta >> 2;
+    const uint32_t mine = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t *)(slab + lane * kPiece) + 4u * dw;
+    constexpr int NW = ALN ? 32 : 33;
+    uint32_t R[33];
+    R[32] = 0;  // ALN: the funnel word is never read
+    const uint32_t nfull_c = nfull;
+    uint32_t h[4];
+    md4_init(h);
+    int32_t s1 = 0;
+    uint32_t t = 0;
+    RSG_DMA_WINDOW(0u);
+    RSG_DMA_WINDOW(1u);
 #pragma unroll 1
-        for (uint32_t cs = 0; cs < S; cs++) {
-            const bool more = cs + 1 < S;
-            if (more) {
-                dma(cs + 1);
-            } else if (next_located && nxt.staged) {
-                point(nxt);  // the slab is free: segment cs is in R
-                dma(0);
-            }
+    for (uint32_t s = 0; s < S; s++) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t a0 = mine + (s & 1u) * kSlab;               // window s
+        const uint32_t a1 = mine + ((s + 1u) & 1u) * kSlab - kWin;  // window s+1, minus its 32 words
+        typedef __attribute__((address_space(3))) const volatile uint32_t lds32;
 #pragma unroll
-            for (uint32_t i = 0; i < kChunks; i++) {
-                const uint32_t c = kChunks * cs + i;
-                if (c < nfull) hash_chunk<true>(R + 16 * i, R[16 * i + 16], 0, c, h, s1, t);
-                else if (c == nfull) hash_tail<true>(R + 16 * i, R[16 * i + 16], 0, n, seed, h, s1, t);
-            }
-            if (more) {
-                if (cs + 2 == S && has_next) {
-                    // the wave would wait for segment cs + 1 here anyway
-                    locate_group<SEG>(arena, arena_bytes, files, wg_file, total_blocks, nw * 64, lane, nxt);
-                    next_located = true;
-                }
-                read_segment();
-            }
+        for (int k = 0; k < NW; k++) {
+            const uint32_t a = dw + (uint32_t)k < 32u ? a0 : a1;
+            R[k] = *(lds32 *)(uintptr_t)(a + 4u * (uint32_t)k);
         }
-        pend = true;
-        pend_tile = gw;
-        pn = n;
-        ps1 = s1;
-        pt = t;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (s + 2 <= S) RSG_DMA_WINDOW(s + 2);  // into window s's slab, in flight while s hashes
 #pragma unroll
-        for (int k = 0; k < 4; k++) ph[k] = h[k];
-        if (!has_next) break;
-        gw = nw;
-        cur = nxt;  // if staged, its segment 0 is in flight (pointed above)
+        for (uint32_t i = 0; i < 2; i++) {
+            const uint32_t c = 2 * s + i;
+            if (c < nfull_c) hash_chunk<ALN>(R + 16 * i, R[16 * i + 16], sh, c, h, s1, t);
+            else if (c == nfull_c) hash_tail<ALN>(R + 16 * i, R[16 * i + 16], sh, n, seed, h, s1, t);
+        }
     }
-    if (pend) {
-        // no DMA in flight: the slab is free
-        store_tile_records(out, pend_tile, lane, reinterpret_cast<uint32_t *>(slab), pn, ps1, pt, ph);
-    }
+#undef RSG_DMA_WINDOW
+    store_tile_records(out, wave_first / 64, lane, reinterpret_cast<uint32_t *>(slab), n, s1, t, h);
 }
 
 // ---------------------------------------------------------------- park variant (loader + register park)
@@ -983,30 +948,30 @@ int block_sums_variant_env() {
 }
 
 bool block_sums_variant_valid(int v) {
-    return v == -1 || v == 0 || v == 1 || v == 2 || v == 3 || v == 4 || v == 6 || v == 14;
+    return v == -1 || v == 0 || v == 1 || v == 2 || v == 3 || v == 4 || v == 6 || v == 7;
 }
 
 // The automatic rule, in two lines (rsg.h; tests/test_abi.py pins its
 // boundaries, DESIGN.md §4.1 has the measurements behind each):
-//   unaligned blocks -> 6; aligned: 512..703 bytes -> park (2); on 128-byte
-//   lines up to 32 KiB -> 128-byte segments (4); up to 24 KiB, when 512-byte
-//   segments read at most 1.2 B per block -> 14; otherwise 256-byte segments (1).
+//   unaligned blocks, or blocks of >= 704 bytes off the 128-byte lines -> line
+//   windows (7); 512..703 -> park (2); on the lines up to 32 KiB -> 4; else 1.
 // A variant the batch cannot take falls back: the LDS-DMA kernels need
-// 4-byte aligned blocks (else 0), the any-offset kernel a 4-byte aligned
-// arena (else 3 for blocks >= 8 KiB, 0 below), park blocks <= 703 bytes
-// (else 1).
-int block_sums_choice(int variant, bool aligned, bool lines128, bool arena_aligned4, uint32_t max_blen) {
+// 4-byte aligned blocks (else 0), line windows a 128-byte aligned arena (else
+// 6 for unaligned blocks, 1 for aligned ones), the any-offset kernel a 4-byte
+// aligned arena (else 3 for blocks >= 8 KiB, 0 below), park blocks <= 703
+// bytes (else 1).  arena_align: 0 = not 4-byte aligned, 1 = 4-byte, 2 = 128-byte.
+int block_sums_choice(int variant, bool aligned, bool lines128, int arena_align, uint32_t max_blen) {
     int v = variant;
     if (v == -1) {
-        const uint64_t seg512 = (uint64_t)((max_blen >> 6) / 8 + 1) * 512;  // bytes the 512-byte segments read per block
-        if (!aligned) v = 6;
+        if (!aligned) v = 7;
         else if (max_blen >= kParkMinBytes && max_blen <= kRegMaxBytes) v = 2;
-        else if (max_blen > kRegMaxBytes && max_blen <= 32768 && lines128) v = 4;
-        else if (max_blen > kRegMaxBytes && max_blen <= 24576 && seg512 * 5 <= (uint64_t)max_blen * 6) v = 14;
+        else if (max_blen > kRegMaxBytes && lines128 && max_blen <= 32768) v = 4;
+        else if (max_blen > kRegMaxBytes && !lines128) v = 7;
         else v = 1;
     }
-    if (!aligned && (v == 1 || v == 2 || v == 4 || v == 14)) v = 0;
-    if (v == 6 && !arena_aligned4) v = max_blen >= kLongBlockBytes ? 3 : 0;
+    if (!aligned && (v == 1 || v == 2 || v == 4)) v = 0;
+    if (v == 7 && arena_align < 2) v = aligned ? 1 : 6;
+    if (v == 6 && arena_align < 1) v = max_blen >= kLongBlockBytes ? 3 : 0;
     if (v == 2 && max_blen > kRegMaxBytes) v = 1;
     return v;
 }
@@ -1018,21 +983,14 @@ static uint32_t park_grid(uint64_t total_blocks) {
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus, ntile));
 }
 
-// The persistent staged kernel (14): one resident 512-byte-segment workgroup
-// per CU (LDS-limited) loops over the waves' 64-block groups.
-static dim3 pipe_grid(uint32_t nwg) {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return dim3(std::max(1u, std::min<uint32_t>(nwg, (uint32_t)cus)));
-}
-
 hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const DevFile *files,
                              const uint32_t *wg_file, uint64_t total_blocks, uint32_t nwg, bool aligned,
                              uint32_t max_blen, uint32_t seed, uint8_t *out, uint32_t lds_reserve, int variant,
                              hipStream_t stream, bool lines128) {
     if (total_blocks == 0) return hipSuccess;
     const dim3 block(kBlockSumThreads), grid(nwg);
-    const int v = block_sums_choice(variant, aligned, lines128, ((uintptr_t)arena & 3u) == 0, max_blen);
+    const uintptr_t ab = (uintptr_t)arena;
+    const int v = block_sums_choice(variant, aligned, lines128, (ab & 127u) == 0 ? 2 : (ab & 3u) == 0 ? 1 : 0, max_blen);
     switch (v) {
         case 1:
             hipLaunchKernelGGL((block_sums_staged<256, false>), grid, block, 0, stream, arena, arena_bytes, files,
@@ -1054,20 +1012,16 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                 hipLaunchKernelGGL((block_sums_staged<256, true>), grid, block, lds_reserve, stream, arena,
                                    arena_bytes, files, wg_file, total_blocks, seed, out);
             break;
-        case 14:
-            // cache policy: the default one up to 4 KiB blocks (a 512-byte piece
-            // off the 128-byte lines shares a line with the block's next
-            // segment, kept in L2 only without nt: B = 1000 / 1448 / 2000 / 3504
-            // 0.238 / 0.239 / 0.230 / 0.216 -> 0.230 / 0.228 / 0.224 / 0.212 ms
-            // per GiB), nt above (6000 / 8000 / 12000 / 20000: 0.211 / 0.245 /
-            // 0.254 / 0.227 against 0.217 / 0.263 / 0.270 / 0.253 without);
-            // profiles/r06o_blocklen_policy_ab.txt
-            if (max_blen <= 4096)
-                hipLaunchKernelGGL(block_sums_pipe<0>, pipe_grid(nwg), block, 0, stream, arena, arena_bytes, files,
-                                   wg_file, total_blocks, seed, out);
-            else
-                hipLaunchKernelGGL(block_sums_pipe<2>, pipe_grid(nwg), block, 0, stream, arena, arena_bytes, files,
-                                   wg_file, total_blocks, seed, out);
+        case 7:  // line windows (the arena on a 128-byte line, checked by block_sums_choice)
+        {
+            auto tz = [](uint32_t x) { return x == 0 ? 5 : std::min(5, __builtin_ctz(x)); };  // factors of 2 mod 32
+            const uint32_t bw = (max_blen / 4) & 31u;
+            const bool ten = tz((36u + bw) & 31u) > tz((40u + bw) & 31u);
+            auto kern = aligned ? (ten ? block_sums_lines<true, 2, 10> : block_sums_lines<true, 2, 9>)
+                                : (ten ? block_sums_lines<false, 2, 10> : block_sums_lines<false, 2, 9>);
+            hipLaunchKernelGGL(kern, grid, block, lds_reserve, stream, arena, arena_bytes, files, wg_file, total_blocks,
+                               seed, out);
+        }
             break;
         case 3: {
             const uint64_t waves = (total_blocks + 63) / 64;

@@ -30,8 +30,9 @@ hipError_t launch_block_sums(const uint8_t *arena, uint64_t arena_bytes, const D
                              hipStream_t stream, bool lines128 = false);
 // The variant a launch takes (rsg_blocksums.hip: the automatic rule and the
 // fallbacks of variants a batch cannot take); host arithmetic.
-int block_sums_choice(int variant, bool aligned, bool lines128, bool arena_aligned4, uint32_t max_blen);
-bool block_sums_variant_valid(int variant);  // -1, 0, 1, 2, 3, 4, 6, 14
+// arena_align: 0 = the arena base not 4-byte aligned, 1 = 4-byte, 2 = 128-byte
+int block_sums_choice(int variant, bool aligned, bool lines128, int arena_align, uint32_t max_blen);
+bool block_sums_variant_valid(int variant);  // -1, 0, 1, 2, 3, 4, 6, 7
 // Files packed into an arena by the library start at multiples of this, so
 // blocks whose length is a multiple of 128 start on 128-byte lines
 constexpr uint64_t kPackAlign = 128;

@@ -31,7 +31,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(_lib.lib, s), s
     assert set(syms) == set(_lib.EXPORTED)
-    assert _lib.lib.rsg_abi_version() == _lib.ABI_VERSION == 4
+    assert _lib.lib.rsg_abi_version() == _lib.ABI_VERSION == 5
 
 
 def test_no_device_fails_loudly():
@@ -136,26 +136,30 @@ def test_apply_tokens_errors():
 
 def test_block_sums_rule_boundaries():
     """The block-sum kernel choice (rsg_set_block_sums_kernel's automatic
-    rule, rsg.h), pinned at every boundary on the host: unaligned -> 6 (3 / 0
-    in an unaligned arena); aligned 512..703 -> park (2); on 128-byte lines up
-    to 32 KiB -> 4; up to 24 KiB when 512-byte segments read <= 1.2 B -> 14;
-    else 1.  Forced variants the batch cannot take fall back."""
+    rule, rsg.h), pinned at every boundary on the host: unaligned blocks, or
+    blocks of >= 704 bytes off the 128-byte lines -> line windows (7); aligned
+    512..703 -> park (2); on the lines up to 32 KiB -> 4; else 1.  Forced
+    variants the batch cannot take fall back (arena_align: 0 / 1 / 2 = the
+    arena base not 4-byte / 4-byte / 128-byte aligned)."""
     from rsync_amd import _lib
     ch = _lib.lib.rsg_testing_block_sums_choice
     for B in (64, 700, 4096, 8191, 8192, 131072):
-        assert ch(-1, 0, 0, 1, B) == 6
+        assert ch(-1, 0, 0, 2, B) == 7
+        assert ch(-1, 0, 0, 1, B) == 6                          # line windows need a 128-byte aligned arena
         assert ch(-1, 0, 0, 0, B) == (3 if B >= 8192 else 0)
-    want = {511: 1, 512: 2, 703: 2, 704: 1, 853: 1, 854: 14, 1024: 1, 1224: 1, 1280: 14, 4096: 14,
-            8000: 14, 16000: 14, 24576: 14, 24577: 1, 32768: 1, 131072: 1}
+    want = {64: 1, 511: 1, 512: 2, 703: 2, 704: 7, 1024: 7, 1448: 7, 4096: 7, 24577: 7, 32768: 7, 131072: 7}
     for B, v in want.items():
-        assert ch(-1, 1, 0, 1, B) == v, B
+        assert ch(-1, 1, 0, 2, B) == v, B                       # aligned, off the lines
+        assert ch(-1, 1, 0, 1, B) == (1 if v == 7 else v), B     # ... in an arena off the lines
     for B, v in {511: 1, 512: 2, 703: 2, 704: 4, 2176: 4, 16384: 4, 32768: 4, 32769: 1}.items():
-        assert ch(-1, 1, 1, 1, B) == v, B
-    assert ch(2, 1, 0, 1, 704) == 1          # park holds blocks <= 703 bytes
-    for v in (1, 2, 4, 14):
-        assert ch(v, 0, 0, 1, 700) == 0      # LDS-DMA kernels need 4-byte aligned blocks
+        assert ch(-1, 1, 1, 2, B) == v, B
+    assert ch(2, 1, 0, 2, 704) == 1          # park holds blocks <= 703 bytes
+    for v in (1, 2, 4):
+        assert ch(v, 0, 0, 2, 700) == 0      # LDS-DMA kernels need 4-byte aligned blocks
     assert ch(6, 0, 0, 0, 32768) == 3 and ch(6, 0, 0, 0, 700) == 0
-    for v in (0, 1, 3, 4, 6, 14):
-        assert ch(v, 1, 1, 1, 4096) == v
-    for bad in (5, 7, 8, 9, 10, 11, 12, 13, 15, 16, -2):
-        assert ch(bad, 1, 0, 1, 700) == -2
+    assert ch(7, 0, 0, 0, 32768) == 3 and ch(7, 0, 0, 0, 700) == 0
+    assert ch(7, 0, 0, 1, 700) == 6 and ch(7, 1, 0, 1, 700) == 1
+    for v in (0, 1, 3, 4, 6, 7):
+        assert ch(v, 1, 1, 2, 4096) == v
+    for bad in (5, 8, 9, 10, 11, 12, 13, 14, 15, 16, -2):
+        assert ch(bad, 1, 0, 2, 700) == -2

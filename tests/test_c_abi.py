@@ -28,8 +28,8 @@ BIN = os.path.join(CDIR, "abi_conformance")
 def _binary():
     """The program built by __graft_entry__.build(); rebuilt here when gcc is
     available and the binary is missing or stale (CPU box only)."""
-    src = os.path.join(CDIR, "abi_conformance.c")
-    if not os.path.exists(BIN) or os.path.getmtime(BIN) < os.path.getmtime(src):
+    srcs = [os.path.join(CDIR, "abi_conformance.c"), os.path.join(CDIR, "..", "..", "include", "rsg.h")]
+    if not os.path.exists(BIN) or os.path.getmtime(BIN) < max(os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", CDIR], check=True)
     return BIN
 

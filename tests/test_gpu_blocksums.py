@@ -118,7 +118,7 @@ def test_device_aligned_multi_file(eng):
     assert got == want
 
 
-@pytest.mark.parametrize("variant", [-1, 14])
+@pytest.mark.parametrize("variant", [-1, 7])
 def test_planned_cfg2_full(eng, variant):
     """cfg2 at full size (1024 x 1 MiB @ B=700, generated on the device):
     every one of the 1 533 952 records bit-exact vs the oracle (~1.5 s of
@@ -184,7 +184,7 @@ def test_generate_and_send_sums_wire(eng):
     assert bytes(conn.buf) == want
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 6, 14])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 6, 7])
 @pytest.mark.parametrize("blen", [700, 64, 1024, 1400, 1773, 4096, 131072])
 def test_kernel_variants_match(eng, variant, blen):
     """Every kernel variant (direct / staged / park / long / staged with 128-
@@ -209,7 +209,31 @@ def test_kernel_variants_match(eng, variant, blen):
     assert rec_dev == want
 
 
-@pytest.mark.parametrize("variant", [-1, 3, 6])
+@pytest.mark.parametrize("blen", [2000, 2289, 3504, 6000, 1773, 4222, 5882, 1448])
+def test_line_windows_piece_strides(eng, blen):
+    """Variant 7 (line windows) at block lengths whose launch takes 10-unit
+    pieces (2000 / 2289 / 3504 / 6000: the bank-conflict choice) and 9-unit
+    ones (1773 / 4222 / 5882 / 1448), on the sweep's layout (files back to
+    back, every block off the 128-byte lines) and on ragged files, through
+    the host path and a device arena; every record equal to the oracle's."""
+    lens = [1 << 20, (1 << 20) - 1, blen * 64 * 2 + 7, blen, 1, 12345, 0, 300_001]
+    files = [cases.splitmix64_bytes(8100 + i, n) for i, n in enumerate(lens)]
+    want = b"".join(orc.block_sums(f, blen, cases.SEED) for f in files)
+    try:
+        eng.set_block_sums_kernel(7)
+        _, rec, _ = eng.block_sums(files, cases.SEED, blen)
+        arena = eng.alloc(sum(lens))
+        offs = np.cumsum([0] + lens[:-1]).tolist()
+        arena.upload(np.concatenate(files))
+        recs, total = eng.block_sums_device(arena, [(o, n, blen) for o, n in zip(offs, lens)], cases.SEED)
+        rec_dev = recs.download(total * 20).tobytes()
+    finally:
+        eng.set_block_sums_kernel(-1)
+    assert rec == want
+    assert rec_dev == want
+
+
+@pytest.mark.parametrize("variant", [-1, 3, 6, 7])
 @pytest.mark.parametrize("blen", [700, 32768, 8192, 131072])
 def test_unaligned_windows(eng, variant, blen):
     """The sender's confirmation shape: windows of one block each at random
@@ -236,7 +260,7 @@ def test_unaligned_windows(eng, variant, blen):
     assert got == want
 
 
-@pytest.mark.parametrize("variant", [1, 3, 4, 6, 14])
+@pytest.mark.parametrize("variant", [1, 3, 4, 6, 7])
 def test_variants_long_blocks_full_waves(eng, variant):
     """cfg5's block length with full 64-block waves (the staged LDS-DMA path
     of variants 1/4/5, not only their direct fallback): a 24 MiB file at
@@ -257,14 +281,12 @@ def test_variants_long_blocks_full_waves(eng, variant):
     assert got == want
 
 
-@pytest.mark.parametrize("variant", [14])
-@pytest.mark.parametrize("blen", [64, 1400])
+@pytest.mark.parametrize("variant,blen", [(2, 64), (7, 64), (7, 1400)])
 def test_persistent_waves_many_groups(eng, variant, blen):
-    """The persistent staged kernels with several 64-block groups per wave
-    (more groups than resident waves), so the pipelined variants (13-15)
-    hand each group over to the next: files of ragged lengths straddling
-    groups, one ending exactly at the arena end (the last group takes the
-    per-lane path after staged ones)."""
+    """Many more 64-block groups than resident waves: the persistent park
+    grid (one workgroup per CU, tiles handed round) and the line-window
+    kernel over files of ragged lengths straddling groups, one ending
+    exactly at the arena end (the last group takes the per-lane path)."""
     rng = np.random.default_rng(blen)
     # B = 64: 6 k groups, more than the resident waves of every variant (4096
     # at 128-byte segments); B = 1400: 3.7 k groups (more than 2048 / 1024
@@ -293,7 +315,7 @@ def test_persistent_waves_many_groups(eng, variant, blen):
     assert got == want
 
 
-@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 6, 14])
+@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 6, 7])
 def test_variants_device_aligned_arena(eng, variant):
     """Aligned device arena (the staged / park fast paths), files straddling
     waves and tiles, a file ending exactly at the arena end (park's direct
@@ -372,7 +394,7 @@ def test_kernel_knobs_are_per_context():
         _, rec_a, _ = a.block_sums(files, cases.SEED, 700)  # a: direct
         assert rec_a == want
         a.set_block_sums_kernel(-1)
-        for bad in (99, 5, 7, 12, 15, -2):
+        for bad in (99, 5, 8, 12, 14, 15, -2):
             with pytest.raises(rsync_amd.RsgError):
                 a.set_block_sums_kernel(bad)
     finally:

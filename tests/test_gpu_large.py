@@ -134,7 +134,7 @@ def _run(eng, unaligned, variant, B, seed=cases.SEED):
 
 
 @pytest.mark.parametrize("variant,B", [(-1, 700), (2, 700), (1, 700), (4, 700), (4, 1024), (1, 131072),
-                                       (-1, 131072), (-1, 4096), (14, 1024), (14, 4096), (14, 131072)])
+                                       (-1, 131072), (-1, 4096), (7, 1000), (7, 4096), (7, 131072)])
 def test_aligned_arena_past_4gib(eng, variant, B):
     """Aligned batch on a 5 GiB arena: park (regular and irregular tiles) and
     the staged kernels, every checked record equal to the oracle's and not one
@@ -144,7 +144,7 @@ def test_aligned_arena_past_4gib(eng, variant, B):
     assert fb == (0, 0), fb
 
 
-@pytest.mark.parametrize("variant,B", [(-1, 700), (6, 700), (6, 32768), (6, 131072)])
+@pytest.mark.parametrize("variant,B", [(-1, 700), (6, 700), (6, 32768), (6, 131072), (7, 32768), (-1, 131072)])
 def test_unaligned_arena_past_4gib(eng, variant, B):
     """The same arena with every file at an odd offset (the unaligned staged
     kernel: pieces from the 4-byte aligned address below each block)."""

@@ -21,7 +21,7 @@ SHAPES_UNALIGNED = [  # files at odd offsets (every block unaligned): direct / l
     (1024, 1 << 20, 1024, 2),
     (256, 4 << 20, 4096, 2),
 ]
-VARIANTS_UNALIGNED = {0: "direct", 3: "long_deep_prefetch", 6: "staged_unaligned"}
+VARIANTS_UNALIGNED = {0: "direct", 3: "long_deep_prefetch", 6: "staged_unaligned", 7: "lines"}
 SHAPES = [  # (files, file bytes, block length, arenas)
     (1, 1 << 30, 131072, 2),      # one 1 GiB file, cfg5's block length
     (1024, 1 << 20, 1024, 2),     # 1 MiB files at the reference's own sizing (B = 1024)
@@ -33,8 +33,8 @@ SHAPES = [  # (files, file bytes, block length, arenas)
     (256, 4 << 20, 4112, 2),
     (1, 1 << 30, 32768, 2),       # 8: one 1 GiB file at the reference's sizing (B = sqrt(len) = 32768)
 ]
-VARIANTS = {-1: "automatic", 1: "staged", 4: "staged_seg128", 14: "pipe_seg512", 2: "park",
-            3: "long_deep_prefetch"}
+VARIANTS = {-1: "automatic", 1: "staged", 4: "staged_seg128", 2: "park",
+            3: "long_deep_prefetch", 7: "lines", 6: "staged_unaligned"}
 # SWEEP_SQRT=1 (or a list of MiB, "2,3"): the reference's own block length B = int(sqrt(len)) (rsynccommon.go:22) for files of
 # len = 1, 2, 3, 5, 9, 17, 33, 64 MiB, ~1 GiB of them per shape, at the library's 128-byte packing
 SQRT_LENS_MIB = [1, 2, 3, 5, 9, 17, 33, 64]
