@@ -11,13 +11,20 @@
 // (copy stream), one kernel (compute stream) whose per-file match lists and
 // statuses land straight in pinned host memory.  Two slots: chunk c+1 is
 // packed and uploaded while chunk c runs, chunk c-1's results are scattered
-// into the callers' match arrays meanwhile.  Files whose candidates overflow
+// into the callers' match arrays meanwhile.  (Scattering chunk c-2 instead,
+// so that packing never waits for the kernel it feeds, measured slower:
+// 12.4-13.1 against 11.1-11.4 ms per cfg4-sender call, round 6.)  Files whose candidates overflow
 // the kernel's LDS list go back to the caller for the large-file pipeline.
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <string>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -30,7 +37,7 @@ namespace rsgh {
 
 namespace {
 
-constexpr uint64_t kChunkJobs = 16384;
+constexpr uint64_t kChunkJobs = 16384;  // 8192 / 4096: 248-264 / 255-272 GiB/s against 280-285 (cfg4-sender, round 6)
 constexpr uint64_t kChunkBlob = 128ull << 20;   // sums bytes per launch
 constexpr uint64_t kChunkSrc = 256ull << 20;    // host-source bytes per launch
 constexpr uint64_t kChunkMatches = 4ull << 20;  // match slots per launch (16 B each)
@@ -52,18 +59,79 @@ uint64_t match_slots(const rsg_search_job &j, uint32_t kc) {
     return std::min<uint64_t>(rsg::small_ccap(kc), j.src_len / std::max(1u, minlen) + 1);
 }
 
+// Seven workers kept for the process (a call runs ~30 parallel loops; a
+// thread per loop and worker cost ~3 ms of the 17 ms cfg4-sender call,
+// round 6) plus the calling thread.  One loop at a time (calls into the
+// small-file path hold their context's lock; a second context's loop waits
+// for the pool).
+class Pool {
+public:
+    static Pool &get() {
+        static Pool p;
+        return p;
+    }
+    void run(const std::function<void()> &work) {
+        std::unique_lock<std::mutex> one(busy_);
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            work_ = &work;
+            pending_ = (int)th_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> g(mu_);
+        done_.wait(g, [&] { return pending_ == 0; });
+        work_ = nullptr;
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+            gen_++;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+
+private:
+    Pool() {
+        for (int i = 0; i < 7; i++) th_.emplace_back([this] { loop(); });
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void()> *w;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+                w = work_;
+            }
+            (*w)();
+            std::lock_guard<std::mutex> g(mu_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex busy_, mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void()> *work_ = nullptr;
+    uint64_t gen_ = 0;
+    int pending_ = 0;
+    bool stop_ = false;
+};
+
 template <class F>
 void parallel_for(uint64_t n, F f) {
-    const int nt = (int)std::min<uint64_t>(8, std::max<uint64_t>(1, n / 256));
     std::atomic<uint64_t> next{0};
-    auto work = [&] {
+    const std::function<void()> work = [&] {
         for (uint64_t i; (i = next.fetch_add(64)) < n;)
             for (uint64_t k = i; k < std::min(n, i + 64); k++) f(k);
     };
-    std::vector<std::thread> pool;
-    for (int t = 1; t < nt; t++) pool.emplace_back(work);
-    work();
-    for (auto &t : pool) t.join();
+    if (n < 512) work();
+    else Pool::get().run(work);
 }
 
 // check_args of rsg_match.cpp without touching the context (worker threads):
@@ -79,15 +147,33 @@ std::string validate(const rsg_search_job &j, std::vector<uint8_t> &seen) {
     if (h.count > 0 && h.block_len == 0) return "zero block length";
     if (h.count > 0 && (!j.sum1 || !j.sum2 || !j.targets)) return "NULL sums or targets";
     if (j.match_cap && !j.matches) return "NULL matches";
+    if (h.count > 0 && j.src_len > 0 && !j.src) return "NULL source";
     seen.assign((size_t)h.count, 0);
     for (int32_t k = 0; k < h.count; k++) {
         const int32_t i = j.targets[k];
         if (i < 0 || i >= h.count || seen[(size_t)i]) return "targets is not a permutation";
         seen[(size_t)i] = 1;
     }
-    if (h.count > 0 && j.src_len > 0 && !j.src) return "NULL source";
     return "";
 }
+
+// RSG_TIMING: the call's host phases, summed over its chunks, to stderr
+struct SmallTimes {
+    bool on = getenv("RSG_TIMING") != nullptr;
+    double ms[6] = {};  // validate, chunk, pack, issue, wait, scatter
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(int k) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        ms[k] += std::chrono::duration<double, std::milli>(n - t).count();
+        t = n;
+    }
+    ~SmallTimes() {
+        if (on)
+            fprintf(stderr, "[rsg] small: validate %.3f chunk %.3f pack %.3f issue %.3f wait %.3f scatter %.3f ms\n",
+                    ms[0], ms[1], ms[2], ms[3], ms[4], ms[5]);
+    }
+};
 
 struct Chunk {
     uint32_t kc = 64;
@@ -107,6 +193,7 @@ rsg_status search_small_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs
                               std::vector<uint64_t> &rest, std::vector<std::string> &msg) {
     rest.clear();
     msg.assign(njobs, std::string());
+    SmallTimes tm;
     // 1. validate every job (job-local errors settle it), settle the empty
     // ones (count 0: sendFile, sender.go:86-88; empty source), classify
     std::vector<uint8_t> kind(njobs, 0);  // 0 settled, 1 small, 2 rest
@@ -124,6 +211,7 @@ rsg_status search_small_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs
         if (j.head.count == 0 || j.src_len == 0) return;
         kind[i] = search_small_eligible(ctx, j) ? 1 : 2;
     });
+    tm.lap(0);
     // 2. chunks: per count class, in job order
     std::vector<Chunk> chunks;
     {
@@ -150,6 +238,7 @@ rsg_status search_small_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs
         for (Chunk &ch : open)
             if (!ch.jobs.empty()) chunks.push_back(std::move(ch));
     }
+    tm.lap(1);
     if (chunks.empty()) return RSG_OK;
     // sources written on the context's stream (fills, copies) come first
     RSG_HIP(ctx, hipEventRecord(ctx->side_done[0], ctx->stream));
@@ -163,7 +252,9 @@ rsg_status search_small_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs
     rsg_status s;
     // 3. results of chunk c (its kernel done): matches into the callers' arrays
     auto scatter = [&](const Chunk &ch, SmallSlot &sl) -> rsg_status {
+        tm.lap(3);
         RSG_HIP(ctx, hipEventSynchronize(sl.done));
+        tm.lap(4);
         const SmallOut *outs = (const SmallOut *)sl.outs.p;
         const rsg_match *ms = (const rsg_match *)sl.matches.p;
         std::atomic<bool> any_rest{false};
@@ -189,6 +280,7 @@ rsg_status search_small_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs
         if (any_rest)
             for (uint64_t k = 0; k < ch.jobs.size(); k++)
                 if (back[k]) rest.push_back(ch.jobs[k]);
+        tm.lap(5);
         return RSG_OK;
     };
     for (size_t c = 0; c <= chunks.size(); c++) {
@@ -230,9 +322,17 @@ rsg_status search_small_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs
                                    (uint32_t)j.head.rem, (uint32_t)j.head.s2len, 0};
             });
             // longest files first: the launch's last waves are its shortest
+            // (a counting sort on the length in 4 KiB steps, kSmallMaxSrc = 1 MiB)
             uint32_t *order = (uint32_t *)(st + off_order);
-            for (uint64_t k = 0; k < J; k++) order[k] = (uint32_t)k;
-            std::stable_sort(order, order + J, [&](uint32_t a, uint32_t b) { return desc[a].size > desc[b].size; });
+            {
+                constexpr uint32_t kBins = (uint32_t)(rsg::kSmallMaxSrc >> 12) + 1;
+                uint32_t cnt[kBins + 1] = {};
+                auto bin = [&](uint64_t k) { return kBins - 1 - (desc[k].size >> 12); };  // longest first
+                for (uint64_t k = 0; k < J; k++) cnt[bin(k) + 1]++;
+                for (uint32_t b = 0; b < kBins; b++) cnt[b + 1] += cnt[b];
+                for (uint64_t k = 0; k < J; k++) order[cnt[bin(k)]++] = (uint32_t)k;
+            }
+            tm.lap(2);
             RSG_HIP(ctx, hipMemcpyAsync(sl.dev.p, st, total, hipMemcpyHostToDevice, copy));
             RSG_HIP(ctx, hipEventRecord(sl.up, copy));
             RSG_HIP(ctx, hipStreamWaitEvent(comp, sl.up, 0));

@@ -154,3 +154,43 @@ def test_cfg4_shaped_sampled_vs_oracle(eng):
     assert sum(len(w) for w in want) > 15_000
     assert got == want
     assert 1 <= t["roll_launches"] <= 4 and t["confirm_batches"] == 0, t
+
+
+@pytest.mark.parametrize("device", [True, False], ids=["device", "host"])
+def test_bad_targets_settled_in_small_path(eng, device):
+    """A small job whose `targets` is not a permutation fails on its own
+    (RSG_ERR_INVALID, checked when its sums are packed; the kernel skips it)
+    while the jobs around it, in the same launch, equal the oracle."""
+    import rsync_amd
+    seed = cases.SEED
+    rng = np.random.default_rng(77)
+    jobs, want, bufs = [], [], []
+    for k in range(5):
+        src, head, s1, s2, tg = _job(7 + 11 * k, seed, rng)
+        if head[0] == 0 or src.size == 0:
+            continue
+        want.append(orc.hash_search(src, head, s1, s2, tg, seed)[0])
+        jobs.append([src, head, s1, s2, tg])
+    bad = jobs[1]
+    jobs.insert(1, [bad[0], bad[1], bad[2], bad[3], np.zeros_like(bad[4])])
+    want.insert(1, None)
+    batch = []
+    for src, head, s1, s2, tg in jobs:
+        if device:
+            buf = eng.alloc(max(src.size, 1))
+            buf.upload(src)
+            bufs.append(buf)
+            batch.append((buf, src.size, head, s1, s2, tg))
+        else:
+            batch.append((src, None, head, s1, s2, tg))
+    eng.set_kernel_timing(True)
+    try:
+        got = eng.hash_search_batch(batch, seed, device=device, raise_on_error=False)
+        t = eng.kernel_times()
+    finally:
+        eng.set_kernel_timing(False)
+    assert [st for st, _ in got] == [0 if w is not None else rsync_amd._lib.ERR_INVALID for w in want]
+    for (st, m), w in zip(got, want):
+        if w is not None:
+            assert m == w
+    assert t["roll_launches"] >= 1 and t["confirm_batches"] == 0, t

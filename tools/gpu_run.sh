@@ -1,9 +1,9 @@
 #!/bin/bash
 # One gpurun call's worth of GPU work, each step under its own time limit,
 # chained so that the first failure (or a hang) ends the call.
-#   tools/gpu_run.sh <tag> <step>...   steps: tests | newtests | smoke | sweep | variants | ab8 | ab |
-#                                             bench | cfg3 | cfg4 | cfg5 | filesums | receive |
-#                                             prof_cfg2 | prof_cfg3 | prof_cfg4 | prof_cfg5 | prof_filesums
+#   tools/gpu_run.sh <tag> <step>...   steps: tests | newtests | smoke | sweep | sqrt | variants | ab8 | ab |
+#                                             bench | cfg3 | cfg4 | cfg4s | cfg5 | filesums | receive |
+#                                             prof_cfg2 | prof_cfg3 | prof_cfg4 | prof_cfg4s | prof_cfg5 | prof_filesums
 set -o pipefail
 TAG=$1; shift
 mkdir -p gpurun_out
@@ -24,6 +24,9 @@ for S in "$@"; do
     cfg5) timeout -k 10 200 python bench.py --workload cfg5 --steps 50 > gpurun_out/${TAG}_cfg5.json 2> gpurun_out/${TAG}_cfg5.err || exit 1 ;;
     filesums) timeout -k 10 300 python bench.py --workload filesums > gpurun_out/${TAG}_filesums.json 2> gpurun_out/${TAG}_filesums.err || exit 1 ;;
     receive) timeout -k 10 300 python bench.py --workload receive > gpurun_out/${TAG}_receive.json 2> gpurun_out/${TAG}_receive.err || exit 1 ;;
+    cfg4s) timeout -k 10 400 python bench.py --workload cfg4-sender --steps 10 --cpu-seconds 5 > gpurun_out/${TAG}_cfg4s.json 2> gpurun_out/${TAG}_cfg4s.err || exit 1 ;;
+    sqrt) SWEEP_SQRT=1 SWEEP_ONLY=automatic timeout -k 10 300 python tools/blocklen_sweep.py > gpurun_out/${TAG}_sqrt.jsonl 2> gpurun_out/${TAG}_sqrt.err || exit 1 ;;
+    prof_cfg4s) PASSES="FETCH_SIZE;WRITE_SIZE" bash tools/profile_kernel.sh ${TAG}_cfg4s search_small --workload cfg4-sender --steps 3 --warmup 1 --no-cpu || exit 1 ;;
     prof_cfg2) bash tools/profile_kernel.sh ${TAG}_cfg2 block_sums --steps 20 --warmup 5 --no-cpu --no-host-path --no-delivery || exit 1 ;;
     prof_cfg3) PASSES="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE;SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE;FETCH_SIZE" bash tools/profile_kernel.sh ${TAG}_cfg3 roll --workload cfg3 --steps 2 --warmup 1 --cfg3-files 4 --no-cpu --no-host-path || exit 1 ;;
     prof_cfg4) PASSES="FETCH_SIZE;WRITE_SIZE" bash tools/profile_kernel.sh ${TAG}_cfg4 block_sums --workload cfg4 --steps 20 --no-cpu --no-host-path --no-delivery || exit 1 ;;

@@ -1,0 +1,7 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+T=r06aa
+mkdir -p gpurun_out
+RSG_TIMING=1 timeout -k 10 400 python bench.py --workload cfg4-sender --steps 5 --no-cpu > gpurun_out/${T}_cfg4s.json 2> gpurun_out/${T}_cfg4s.err || { tail -20 gpurun_out/${T}_cfg4s.err; exit 4; }
+grep "small:" gpurun_out/${T}_cfg4s.err | tail -8
+python -c "import json;d=json.load(open('gpurun_out/${T}_cfg4s.json'));print(d['value'], d['call_ms'], d['roofline']['kernel_ms_per_call'])"
