@@ -18,8 +18,9 @@ extern "C" {
  * or -1.  cand must be strictly increasing.  Returns the match list the walk
  * produces and stats[0] = confirmation round trips, stats[1] = windows
  * confirmed, i.e. what the GPU path would have issued.  On input stats[0]
- * picks the sparse batches' selection: 1 = speculative, 2 = every pending
- * candidate, 0 = as RSG_CONFIRM_SPEC says (default: every candidate). */
+ * picks the sparse batches' selection: 1 = speculative, 0 or 2 = every
+ * pending candidate (the default, as the "spec" option of
+ * rsg_testing_search_option). */
 rsg_status rsg_testing_walk(const uint64_t *cand, uint64_t n, const int32_t *truth, uint64_t size,
                             const rsg_sum_head *head, rsg_match *out, uint64_t cap, uint64_t *n_out,
                             uint64_t stats[2]);

@@ -194,3 +194,44 @@ def test_bad_targets_settled_in_small_path(eng, device):
         if w is not None:
             assert m == w
     assert t["roll_launches"] >= 1 and t["confirm_batches"] == 0, t
+
+
+def test_two_contexts_concurrently():
+    """Two contexts searching small-file batches from two threads at once:
+    their parallel loops share the library's worker pool (one loop at a
+    time), and each batch still equals the oracle job by job."""
+    import threading
+    import rsync_amd
+    seed = cases.SEED
+    rng = np.random.default_rng(91)
+    sets = []
+    for t in range(2):
+        jobs, want = [], []
+        for k in range(700):
+            src, head, s1, s2, tg = _job(5000 * (t + 1) + k, seed, rng)
+            jobs.append((src, None, head, s1, s2, tg))
+            want.append(orc.hash_search(src, head, s1, s2, tg, seed)[0])
+        sets.append((jobs, want))
+    engines = [rsync_amd.Engine(0), rsync_amd.Engine(0)]
+    got = [None, None]
+    err = []
+
+    def run(t):
+        try:
+            for _ in range(3):
+                got[t] = engines[t].hash_search_batch(sets[t][0], seed, device=False)
+        except Exception as e:  # surfaced below
+            err.append(e)
+
+    try:
+        th = [threading.Thread(target=run, args=(t,)) for t in range(2)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(120)
+        assert not err, err
+        for t in range(2):
+            assert got[t] == sets[t][1], t
+    finally:
+        for e in engines:
+            e.close()
