@@ -934,10 +934,11 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
 // slabs (256-byte segments), 2 = park (three loader waves + five hashers with
 // register-parked blocks, blocks <= 703 bytes), 3 = long blocks with deep
 // per-lane prefetch, 4 = staged with 128-byte segments, 6 = staged for
-// blocks at any byte offset (funnel-shifted pieces), 14 = persistent staged
-// with 512-byte segments and hidden group boundaries.  (The numbers of the
-// variants measured and dropped in rounds 1-5 -- 5, 7..13, 15 -- are not
-// reused; tools/build_ab.sh rebuilds them from the round-5 history.)
+// blocks at any byte offset (funnel-shifted pieces), 7 = line windows (each
+// block's bytes as the 128-byte lines that hold them, every line once).  (7
+// was a dropped round-3 variant's number; the other dropped ones -- 5,
+// 8..15, 14 the persistent 512-byte kernel until round 6 -- are not reused;
+// tools/build_ab.sh rebuilds them from the history.)
 int block_sums_variant_env() {
     static const int v = [] {
         const char *e = getenv("RSG_BLOCKSUMS_KERNEL");
