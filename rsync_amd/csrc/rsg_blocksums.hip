@@ -936,7 +936,7 @@ __global__ __launch_bounds__(kPkThreads) void block_sums_park(
 // per-lane prefetch, 4 = staged with 128-byte segments, 6 = staged for
 // blocks at any byte offset (funnel-shifted pieces), 7 = line windows (each
 // block's bytes as the 128-byte lines that hold them, every line once).  (7
-// was a dropped round-3 variant's number; the other dropped ones -- 5,
+// was a dropped ABI-3 variant's number, reused from ABI 5; the other dropped ones -- 5,
 // 8..15, 14 the persistent 512-byte kernel until round 6 -- are not reused;
 // tools/build_ab.sh rebuilds them from the history.)
 int block_sums_variant_env() {
