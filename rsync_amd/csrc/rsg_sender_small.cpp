@@ -17,6 +17,7 @@
 // the kernel's LDS list go back to the caller for the large-file pipeline.
 #include <stdio.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -63,19 +64,24 @@ uint64_t match_slots(const rsg_search_job &j, uint32_t kc) {
 // thread per loop and worker cost ~3 ms of the 17 ms cfg4-sender call,
 // round 6) plus the calling thread.  One loop at a time (calls into the
 // small-file path hold their context's lock; a second context's loop waits
-// for the pool).
+// for the pool).  A forked child has none of the parent's workers: there
+// the calling thread runs the loop alone.
 class Pool {
 public:
     static Pool &get() {
-        static Pool p;
-        return p;
+        static Pool *p = new Pool;  // never destroyed: the workers idle in their wait until the process ends
+        return *p;
     }
     void run(const std::function<void()> &work) {
+        if (getpid() != pid_) {
+            work();
+            return;
+        }
         std::unique_lock<std::mutex> one(busy_);
         {
             std::lock_guard<std::mutex> g(mu_);
             work_ = &work;
-            pending_ = (int)th_.size();
+            pending_ = kWorkers;
             gen_++;
         }
         cv_.notify_all();
@@ -84,19 +90,10 @@ public:
         done_.wait(g, [&] { return pending_ == 0; });
         work_ = nullptr;
     }
-    ~Pool() {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            stop_ = true;
-            gen_++;
-        }
-        cv_.notify_all();
-        for (auto &t : th_) t.join();
-    }
-
 private:
-    Pool() {
-        for (int i = 0; i < 7; i++) th_.emplace_back([this] { loop(); });
+    static constexpr int kWorkers = 7;
+    Pool() : pid_(getpid()) {
+        for (int i = 0; i < kWorkers; i++) std::thread([this] { loop(); }).detach();
     }
     void loop() {
         uint64_t seen = 0;
@@ -106,7 +103,6 @@ private:
                 std::unique_lock<std::mutex> g(mu_);
                 cv_.wait(g, [&] { return gen_ != seen; });
                 seen = gen_;
-                if (stop_) return;
                 w = work_;
             }
             (*w)();
@@ -114,13 +110,12 @@ private:
             if (--pending_ == 0) done_.notify_one();
         }
     }
-    std::vector<std::thread> th_;
+    const pid_t pid_;
     std::mutex busy_, mu_;
     std::condition_variable cv_, done_;
     const std::function<void()> *work_ = nullptr;
     uint64_t gen_ = 0;
     int pending_ = 0;
-    bool stop_ = false;
 };
 
 template <class F>
