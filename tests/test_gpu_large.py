@@ -304,6 +304,38 @@ def test_release_arenas(eng):
     _ARENAS.clear()
 
 
+def test_cfg3_batch_three_files_vs_oracle(eng):
+    """The bench's call shape at real size: three cfg3 files (1 GiB bases,
+    ~50 % overwritten sources with insertions and deletions, B = 32 768) in
+    ONE rsg_hash_search_batch_device call, so the pipeline runs as in the
+    bench -- each file's confirmation beside the next file's roll on the
+    CUs the roll leaves free, the last one beside the previous one, the
+    windows through the line-window kernel -- and every file's match list
+    equals the oracle's hashSearch (~20 s of oracle time)."""
+    size = 1 << 30
+    rng = np.random.default_rng(33)
+    jobs, want, bufs = [], [], []
+    for f in range(3):
+        basis = eng.alloc(size)
+        src = eng.alloc(size + 4096)
+        n = cases.make_cfg3_file(eng, basis, src, size, 40 + f, 32768, rng)
+        eng.synchronize()
+        rec = orc.block_sums(basis.download(size), 0, cases.SEED)
+        basis.free()
+        s1, s2 = orc.parse_records(rec)
+        tg = orc.stable_targets(s1)
+        head = orc.sum_head(size, 0)
+        want.append(orc.hash_search(src.download(n), head, s1, s2, tg, cases.SEED)[0])
+        jobs.append((src, n, head, s1, s2, tg))
+        bufs.append(src)
+    got = eng.hash_search_batch(jobs, cases.SEED)
+    for f in range(3):
+        assert len(want[f]) > 10_000
+        assert got[f] == want[f], f
+    for b in bufs:
+        b.free()
+
+
 def test_cfg3_real_size_vs_oracle(eng):
     """BASELINE cfg3 at its real size, one file: a 1 GiB basis and a source
     with ~50 % of its bytes overwritten plus insertions and deletions (the
