@@ -59,6 +59,10 @@ type Engine struct{ ctx *C.rsg_ctx }
 
 // New opens device `device`.  RSG_ERR_NODEV maps to ErrUnavailable.
 func New(device int) (*Engine, error) {
+	// the shared library must be the one this binding's header describes
+	if v := int(C.rsg_abi_version()); v != int(C.RSG_ABI_VERSION) {
+		return nil, fmt.Errorf("librsg ABI %d, binding built against %d", v, int(C.RSG_ABI_VERSION))
+	}
 	var ctx *C.rsg_ctx
 	if st := C.rsg_ctx_create(C.int32_t(device), &ctx); st != C.RSG_OK {
 		if st == C.RSG_ERR_NODEV {
