@@ -38,6 +38,9 @@ namespace rsgh {
 
 namespace {
 
+// the first launch is small, so the GPU starts after packing a few thousand
+// files instead of 16 384 (the rest of the call's packing hides under it)
+constexpr uint64_t kFirstChunkJobs = 2048;
 constexpr uint64_t kChunkJobs = 16384;  // 8192 / 4096: 248-264 / 255-272 GiB/s against 280-285 (cfg4-sender, round 6)
 constexpr uint64_t kChunkBlob = 128ull << 20;   // sums bytes per launch
 constexpr uint64_t kChunkSrc = 256ull << 20;    // host-source bytes per launch
@@ -219,7 +222,8 @@ rsg_status search_small_batch(rsg_ctx *ctx, rsg_search_job *jobs, uint64_t njobs
             const uint32_t kc = count_class(j.head.count);
             Chunk &ch = open[__builtin_ctz(kc) - 6];
             const uint64_t b = blob_bytes(j.head.count), s = host_src ? a16(j.src_len) : 0, m = match_slots(j, kc);
-            if (!ch.jobs.empty() && (ch.jobs.size() >= kChunkJobs || ch.blob + b > kChunkBlob ||
+            const uint64_t cap_jobs = chunks.empty() ? kFirstChunkJobs : kChunkJobs;
+            if (!ch.jobs.empty() && (ch.jobs.size() >= cap_jobs || ch.blob + b > kChunkBlob ||
                                      ch.src + s > kChunkSrc || ch.slots + m > kChunkMatches)) {
                 chunks.push_back(std::move(ch));
                 ch = Chunk();
