@@ -1236,6 +1236,9 @@ def bench_filesums(args, rank, world, local):
     NF = 100_000
     lengths = np.random.default_rng(4).integers(4096, 65537, NF).tolist()
     eng = rsync_amd.Engine(local)
+    for opt in args.search_option:
+        name, value = opt.split("=")
+        eng.set_option(name, int(value))
     offs, at = [], 0
     for n in lengths:
         offs.append(at)
@@ -1297,7 +1300,8 @@ def bench_filesums(args, rank, world, local):
         "unit": "GiB/s", "n_gpus": 1, "steps": steps, "higher_is_better": True, "dtype": "u32",
         "data": "synthetic (splitmix64 bytes generated on device)",
         "config": {"workload": "whole-file MD4 over cfg4's 100k files (4-64 KiB)", "files": NF, "total_bytes": total,
-                   "call": "rsg_file_sums_device, descriptors uploaded and waited on per call"},
+                   "call": "rsg_file_sums_device, descriptors uploaded and waited on per call",
+                   **({"search_options": args.search_option} if args.search_option else {})},
         "modes": res, "spot_parity": {"files": min(k, 256), "equal": parity},
         "roofline": {"bound": "hbm", "kernel": "file_sums_staged<seeded>",
                      "achieved": round(total / (res["seeded"]["kernel_ms"] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
