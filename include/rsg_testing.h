@@ -59,10 +59,7 @@ rsg_status rsg_testing_md4(const uint8_t *data, uint64_t n, int32_t seeded, int3
  *   5 receiveData's whole-file sums: 0 (default) by file size, 1 GPU, 2 host;
  *   6 the whole-file sums' lane order: files sorted longest first in length
  *     buckets of 2^value bytes, 0..40 (default 10; 40 keeps the callers'
- *     order);
- *   7 ... region-major: 0 (default) off, else 12..40: files grouped by arena
- *     region of 2^value bytes, longest first inside a region, the full waves
- *     of 64 ordered by their longest file.
+ *     order).
  * RSG_ERR_INVALID for an unknown option or value. */
 rsg_status rsg_testing_search_option(rsg_ctx *ctx, int32_t option, int32_t value);
 

@@ -51,45 +51,6 @@ void lane_order(const rsg::FileSpan *spans, uint32_t n, uint32_t *order, int shi
     for (uint32_t i = 0; i < n; i++) order[count[key(spans[i].len)]++] = i;
 }
 
-// Stable counting sort of idx[0, n) by key(idx[i]) < nkeys into out.
-template <class K>
-void counting_sort(const uint32_t *idx, uint32_t n, uint32_t nkeys, K key, uint32_t *out) {
-    std::vector<uint32_t> count(nkeys + 1, 0);
-    for (uint32_t i = 0; i < n; i++) count[key(idx[i])]++;
-    uint32_t at = 0;
-    for (uint32_t k = 0; k < nkeys; k++) {
-        const uint32_t c = count[k];
-        count[k] = at;
-        at += c;
-    }
-    for (uint32_t i = 0; i < n; i++) out[count[key(idx[i])]++] = idx[i];
-}
-
-// Region-major variant (rsg_testing_search_option 7): files sorted by arena
-// region of 2^region_shift bytes, longest first inside a region, cut into
-// waves of 64, and the full waves ordered by their longest file (the partial
-// wave, if any, stays last).  A wave's 64 files then lie in one region.
-void lane_order_regions(const rsg::FileSpan *spans, uint32_t n, uint32_t *order, int shift, int region_shift) {
-    std::vector<uint32_t> a(n), b(n);
-    lane_order(spans, n, a.data(), shift);
-    constexpr uint32_t kRegions = 1u << 16;
-    counting_sort(a.data(), n, kRegions, [&](uint32_t i) {
-        return (uint32_t)std::min<uint64_t>(spans[i].offset >> region_shift, kRegions - 1);
-    }, b.data());
-    const uint32_t full = n / 64;
-    std::vector<uint32_t> waves(full), key(full), sorted(full);
-    constexpr uint32_t kKeys = 1u << 16;
-    for (uint32_t w = 0; w < full; w++) {
-        uint64_t m = 0;
-        for (uint32_t l = 0; l < 64; l++) m = std::max<uint64_t>(m, spans[b[64 * w + l]].len);
-        waves[w] = w;
-        key[w] = kKeys - 1 - (uint32_t)std::min<uint64_t>(m >> shift, kKeys - 1);
-    }
-    counting_sort(waves.data(), full, kKeys, [&](uint32_t w) { return key[w]; }, sorted.data());
-    for (uint32_t w = 0; w < full; w++) memcpy(order + 64 * w, b.data() + 64 * sorted[w], 64 * 4);
-    memcpy(order + 64 * full, b.data() + 64 * full, (n - 64 * full) * 4);
-}
-
 }  // namespace
 
 namespace rsgh {
@@ -112,11 +73,7 @@ rsg_status launch_file_sums_staged(rsg_ctx *ctx, const void *d_arena, uint64_t a
                                    int32_t mode, int32_t seed, void *d_out, int slot, hipStream_t stream) {
     const uint64_t ooff = (n * sizeof(rsg::FileSpan) + 63) & ~63ull;
     uint8_t *hd = (uint8_t *)ctx->h_desc[slot].p;
-    if (ctx->opts.fs_region_shift)
-        lane_order_regions((const rsg::FileSpan *)hd, (uint32_t)n, (uint32_t *)(hd + ooff), ctx->opts.fs_key_shift,
-                           ctx->opts.fs_region_shift);
-    else
-        lane_order((const rsg::FileSpan *)hd, (uint32_t)n, (uint32_t *)(hd + ooff), ctx->opts.fs_key_shift);
+    lane_order((const rsg::FileSpan *)hd, (uint32_t)n, (uint32_t *)(hd + ooff), ctx->opts.fs_key_shift);
     bool aligned4 = ((uintptr_t)d_arena & 3u) == 0;
     for (uint64_t i = 0; i < n && aligned4; i++) aligned4 = (((const rsg::FileSpan *)hd)[i].offset & 3u) == 0;
     uint8_t *dd = (uint8_t *)ctx->d_desc[slot].p;

@@ -206,11 +206,7 @@ struct FsShape {
     static constexpr uint32_t kDma = kUnits;                // DMA instructions per segment
 };
 
-// KREG > 0 (an A/B build, bench --fs-regs): the copies go through registers
-// instead of LDS DMA -- KREG segments in flight per lane as 16-byte loads at
-// the DMA's addresses, written into one slab when their step comes -- so
-// the bytes in flight per CU are not capped by the LDS.
-template <bool SEEDED, int AUX, bool ALN, int KREG = 0>
+template <bool SEEDED, int AUX, bool ALN>
 __global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict__ arena, uint64_t arena_bytes,
                                                        const FileSpan *__restrict__ files,
                                                        const uint32_t *__restrict__ order, uint32_t nfiles,
@@ -218,7 +214,7 @@ __global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict
     using Sh = FsShape;
     constexpr uint32_t CH = Sh::kChunks, SEG = Sh::kSeg, NU = Sh::kUnits, PIECE = Sh::kPiece, SLAB = Sh::kSlab,
                        NDMA = Sh::kDma;
-    __shared__ __attribute__((aligned(16))) uint8_t slab[(KREG ? 1 : 2) * SLAB];  // two segments in flight
+    __shared__ __attribute__((aligned(16))) uint8_t slab[2 * SLAB];  // two segments in flight
     const uint32_t lane = threadIdx.x;
     const uint32_t lane_file = blockIdx.x * 64 + lane;
     const bool active = lane_file < nfiles;
@@ -281,12 +277,22 @@ __global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict
         }                                                                                                      \
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                     \
     } while (0)
+    // Two segments in flight per wave: segment s + 2 is issued into the slab
+    // segment s was just copied out of
+    RSG_FS_DMA(0u, 0u);
+    if (S > 1) RSG_FS_DMA(1u, 1u);
     uint32_t h[4];
     md4_init(h);
     uint32_t carry = seed;  // seeded: the message word before the chunk's data words
     uint32_t X[16];
     const uint32_t tail_seg = (uint32_t)(nfull / CH), tail_i = (uint32_t)(nfull % CH);
-    auto hash_seg = [&](uint32_t s) {
+#pragma unroll 1
+    for (uint32_t s = 0; s < S; s++) {
+        // segment s has landed once at most the younger segment's NDMA DMAs are pending
+        if (s + 1 < S) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        RSG_FS_READ(s & 1u);
+        if (s + 2 < S) RSG_FS_DMA(s + 2, s & 1u);  // in flight while segments s and s + 1 hash
         if (s <= tail_seg && s < nseg) {
 #pragma unroll
             for (uint32_t i = 0; i < CH; i++) {
@@ -310,46 +316,6 @@ __global__ __launch_bounds__(64) void file_sums_staged(const uint8_t *__restrict
                 md4_compress(h, X);
             }
         }
-    };
-    if constexpr (KREG == 0) {
-        // Two segments in flight per wave: segment s + 2 is issued into the
-        // slab segment s was just copied out of
-        RSG_FS_DMA(0u, 0u);
-        if (S > 1) RSG_FS_DMA(1u, 1u);
-#pragma unroll 1
-        for (uint32_t s = 0; s < S; s++) {
-            // segment s has landed once at most the younger segment's NDMA DMAs are pending
-            if (s + 1 < S) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            RSG_FS_READ(s & 1u);
-            if (s + 2 < S) RSG_FS_DMA(s + 2, s & 1u);  // in flight while segments s and s + 1 hash
-            hash_seg(s);
-        }
-    } else {
-        FsVec G[KREG][NDMA];
-        auto gload = [&](uint32_t k, uint32_t s) {
-#pragma unroll
-            for (uint32_t i = 0; i < NDMA; i++)
-                G[k][i] = *reinterpret_cast<const FsVec *>(ua[i] + (uint64_t)SEG * min(s, un[i]));
-        };
-#pragma unroll
-        for (uint32_t k = 0; k < (uint32_t)KREG; k++)
-            if (k < S) gload(k, k);
-#pragma unroll 1
-        for (uint32_t s0 = 0; s0 < S; s0 += KREG) {
-#pragma unroll
-            for (uint32_t k = 0; k < (uint32_t)KREG; k++) {
-                const uint32_t s = s0 + k;
-                if (s >= S) break;
-#pragma unroll
-                for (uint32_t i = 0; i < NDMA; i++)
-                    *(volatile __attribute__((address_space(3))) FsVec *)(slab + 1024u * i + 16u * lane) = G[k][i];
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                RSG_FS_READ(0u);
-                if (s + KREG < S) gload(k, s + KREG);
-                hash_seg(s);
-            }
-        }
     }
 #undef RSG_FS_DMA
 #undef RSG_FS_READ
@@ -370,10 +336,6 @@ hipError_t launch_file_sums(const uint8_t *arena, uint64_t arena_bytes, const Fi
     const dim3 grid((nfiles + 63) / 64), block(64);
     auto kern = mode == 1 ? (aligned4 ? file_sums_staged<true, 0, true> : file_sums_staged<true, 0, false>)
                           : (aligned4 ? file_sums_staged<false, 0, true> : file_sums_staged<false, 0, false>);
-    static const int kreg = getenv("RSG_FS_REGS") ? atoi(getenv("RSG_FS_REGS")) : 0;  // A/B build only
-    if (aligned4 && kreg == 2) kern = mode == 1 ? file_sums_staged<true, 0, true, 2> : file_sums_staged<false, 0, true, 2>;
-    if (aligned4 && kreg == 3) kern = mode == 1 ? file_sums_staged<true, 0, true, 3> : file_sums_staged<false, 0, true, 3>;
-    if (aligned4 && kreg == 4) kern = mode == 1 ? file_sums_staged<true, 0, true, 4> : file_sums_staged<false, 0, true, 4>;
     hipLaunchKernelGGL(kern, grid, block, 0, stream, arena, arena_bytes, files, order, nfiles, seed, out);
     return hipGetLastError();
 }

@@ -100,7 +100,6 @@ struct rsg_ctx {
         int confirm_cus = 32;      // CUs a batch's rolls leave to the previous job's confirmation (0: serial)
         int recv_md4 = 0;          // receiveData's whole-file sums: 0 by size, 1 GPU, 2 host
         int fs_key_shift = 10;     // whole-file sums' lane order: length buckets of 2^shift bytes (40: arena order)
-        int fs_region_shift = 0;   // ... region-major in arena regions of 2^shift bytes (0: off)
     } opts;
     DevBuf d_res;
     // multi-GPU

@@ -1584,7 +1584,6 @@ rsg_status rsg_testing_search_option(rsg_ctx *ctx, int32_t option, int32_t value
         case 4: if (value < 0 || value > 1024) break; o.confirm_cus = value; return RSG_OK;
         case 5: if (value < 0 || value > 2) break; o.recv_md4 = value; return RSG_OK;
         case 6: if (value < 0 || value > 40) break; o.fs_key_shift = value; return RSG_OK;
-        case 7: if (value != 0 && (value < 12 || value > 40)) break; o.fs_region_shift = value; return RSG_OK;
         default: return fail(ctx, RSG_ERR_INVALID, "unknown option %d", option);
     }
     return fail(ctx, RSG_ERR_INVALID, "option %d: bad value %d", option, value);

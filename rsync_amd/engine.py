@@ -555,7 +555,7 @@ class Engine:
         return [(b.status(k), b.matches(k, as_arrays) if b.status(k) == _lib.OK else []) for k in range(b.n)]
 
     SEARCH_OPTIONS = {"path": 0, "host_tables": 1, "force_table_ovf": 2, "spec": 3, "confirm_cus": 4, "recv_md4": 5,
-                      "fs_key_shift": 6, "fs_region_shift": 7}
+                      "fs_key_shift": 6}
 
     def set_option(self, name: str, value: int):
         """rsg_testing_search_option: one of SEARCH_OPTIONS on this context
